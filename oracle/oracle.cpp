@@ -1,0 +1,735 @@
+// CPU ORACLE -- test infrastructure only (see oracle.h). Restates the reference's photon life cycle.
+#include "oracle.h"
+
+#include <algorithm>
+#include <atomic>
+#include <cfloat>
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../skirt_amd/csrc/host/model.hpp"
+#include "../skirt_amd/csrc/host/outputs.hpp"
+
+using namespace skirt;
+
+namespace {
+
+thread_local std::string g_error;
+
+// ============================================================ random numbers
+
+// Philox4x32-10 (Salmon et al. 2011, "Parallel random numbers: as easy as 1, 2, 3"), written out
+// independently of the device engine's implementation so each can check the other.
+void philox(const uint32_t in[4], const uint32_t key[2], uint32_t out[4]) {
+    uint32_t c0 = in[0], c1 = in[1], c2 = in[2], c3 = in[3];
+    uint32_t k0 = key[0], k1 = key[1];
+    for (int round = 0; round < 10; round++) {
+        uint64_t p0 = (uint64_t)0xD2511F53u * c0;
+        uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
+        uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+        uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+        uint32_t n0 = hi1 ^ c1 ^ k0, n1 = lo1, n2 = hi0 ^ c3 ^ k1, n3 = lo0;
+        c0 = n0; c1 = n1; c2 = n2; c3 = n3;
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+    out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+}
+
+class Rng {
+public:
+    virtual ~Rng() = default;
+    virtual double uniform() = 0;
+};
+
+class MTRng final : public Rng {
+public:
+    explicit MTRng(MTRandom* mt) : mt_(mt) {}
+    double uniform() override { return mt_->uniform(); }
+private:
+    MTRandom* mt_;
+};
+
+// one stream per packet: key = seed, counter = (block, tag, packet_lo, packet_hi); two 32-bit words
+// make one 53-bit uniform in the open interval (0,1)
+class PhiloxRng final : public Rng {
+public:
+    PhiloxRng(uint64_t seed, uint32_t tag) : tag_(tag) { key_[0] = (uint32_t)seed; key_[1] = (uint32_t)(seed >> 32); }
+    void start(uint64_t packet) { packet_ = packet; block_ = 0; have_ = 0; }
+    double uniform() override {
+        if (have_ == 0) {
+            uint32_t ctr[4] = {block_++, tag_, (uint32_t)packet_, (uint32_t)(packet_ >> 32)};
+            philox(ctr, key_, w_);
+            have_ = 4;
+        }
+        uint32_t a = w_[4 - have_], b = w_[5 - have_];
+        have_ -= 2;
+        uint64_t x = ((uint64_t)(a >> 5) << 26) | (uint64_t)(b >> 6);
+        return ((double)x + 0.5) * (1.0 / 9007199254740992.0);
+    }
+private:
+    uint32_t key_[2];
+    uint32_t tag_;
+    uint64_t packet_ = 0;
+    uint32_t block_ = 0;
+    uint32_t w_[4];
+    int have_ = 0;
+};
+
+// Random::exponcutoff (Random.cpp:162-175)
+double exponcutoff(Rng& r, double xmax) {
+    if (xmax == 0.0) return 0.0;
+    else if (xmax < 1e-10) return r.uniform() * xmax;
+    double x = -log(1.0 - r.uniform() * (1.0 - exp(-xmax)));
+    while (x > xmax) x = -log(1.0 - r.uniform() * (1.0 - exp(-xmax)));
+    return x;
+}
+
+struct Vec3 { double x, y, z; };
+
+// Direction(theta, phi) (Direction.cpp)
+Vec3 directionThetaPhi(double theta, double phi) {
+    const double eps = 1e-8;
+    if (theta <= eps) return {0, 0, 1};
+    if (theta >= M_PI - eps) return {0, 0, -1};
+    double st = sin(theta);
+    return {st * cos(phi), st * sin(phi), cos(theta)};
+}
+
+// Random::direction() (Random.cpp:179-184)
+Vec3 isotropic(Rng& r) {
+    double theta = acos(2.0 * r.uniform() - 1.0);
+    double phi = 2.0 * M_PI * r.uniform();
+    return directionThetaPhi(theta, phi);
+}
+
+// Random::direction(bfk, costheta) (Random.cpp:188-222)
+Vec3 rotated(Rng& r, Vec3 k, double costheta) {
+    double phi = 2.0 * M_PI * r.uniform();
+    double cosphi = cos(phi), sinphi = sin(phi);
+    double sintheta = sqrt(fabs((1.0 - costheta) * (1.0 + costheta)));
+    double kx = k.x, ky = k.y, kz = k.z;
+    if (kz > 0.99999) return {cosphi * sintheta, sinphi * sintheta, costheta};
+    if (kz < -0.99999) return {cosphi * sintheta, sinphi * sintheta, -costheta};
+    double root = sqrt((1.0 - kz) * (1.0 + kz));
+    return {sintheta / root * (-kx * kz * cosphi + ky * sinphi) + kx * costheta,
+            -sintheta / root * (ky * kz * cosphi + kx * sinphi) + ky * costheta,
+            root * sintheta * cosphi + kz * costheta};
+}
+
+// ============================================================ paths
+
+struct Segment { int m; double ds, s, dtau, tau; };
+
+struct Path {
+    std::vector<Segment> v;
+    double s = 0;
+    void clear() { v.clear(); s = 0; }
+    void add(int m, double ds) {  // DustGridPath::addSegment
+        if (ds > 0) { s += ds; v.push_back({m, ds, s, 0, 0}); }
+    }
+};
+
+// CartesianDustGrid::path (CartesianDustGrid.cpp:136-283)
+void cartesianPath(const CartesianGrid& g, Vec3 r, Vec3 k, Path& p) {
+    p.clear();
+    double kx = k.x, ky = k.y, kz = k.z, x = r.x, y = r.y, z = r.z, ds, dsx, dsy, dsz;
+    const std::vector<double>&xv = g.xv, &yv = g.yv, &zv = g.zv;
+    if (x < g.xmin) {
+        if (kx <= 0.0) return p.clear();
+        ds = (g.xmin - x) / kx; p.add(-1, ds);
+        x = g.xmin + 1e-8 * (xv[1] - xv[0]); y += ky * ds; z += kz * ds;
+    } else if (x > g.xmax) {
+        if (kx >= 0.0) return p.clear();
+        ds = (g.xmax - x) / kx; p.add(-1, ds);
+        x = g.xmax - 1e-8 * (xv[g.Nx] - xv[g.Nx - 1]); y += ky * ds; z += kz * ds;
+    }
+    if (y < g.ymin) {
+        if (ky <= 0.0) return p.clear();
+        ds = (g.ymin - y) / ky; p.add(-1, ds);
+        x += kx * ds; y = g.ymin + 1e-8 * (yv[1] - yv[0]); z += kz * ds;
+    } else if (y > g.ymax) {
+        if (ky >= 0.0) return p.clear();
+        ds = (g.ymax - y) / ky; p.add(-1, ds);
+        x += kx * ds; y = g.ymax - 1e-8 * (yv[g.Ny] - yv[g.Ny - 1]); z += kz * ds;
+    }
+    if (z < g.zmin) {
+        if (kz <= 0.0) return p.clear();
+        ds = (g.zmin - z) / kz; p.add(-1, ds);
+        x += kx * ds; y += ky * ds; z = g.zmin + 1e-8 * (zv[1] - zv[0]);
+    } else if (z > g.zmax) {
+        if (kz >= 0.0) return p.clear();
+        ds = (g.zmax - z) / kz; p.add(-1, ds);
+        x += kx * ds; y += ky * ds; z = g.zmax - 1e-8 * (zv[g.Nz] - zv[g.Nz - 1]);
+    }
+    if (x < g.xmin || x > g.xmax || y < g.ymin || y > g.ymax || z < g.zmin || z > g.zmax) return p.clear();
+    auto clip = [](const std::vector<double>& v, double q) {  // NR::locate_clip
+        int n = (int)v.size();
+        if (q < v[0]) return 0;
+        int jl = -1, ju = n - 1;
+        while (ju - jl > 1) { int jm = (ju + jl) >> 1; if (q < v[jm]) ju = jm; else jl = jm; }
+        return jl;
+    };
+    int i = clip(xv, x), j = clip(yv, y), kk = clip(zv, z);
+    while (true) {
+        int m = kk + g.Nz * j + g.Nz * g.Ny * i;
+        double xE = (kx < 0.0) ? xv[i] : xv[i + 1];
+        double yE = (ky < 0.0) ? yv[j] : yv[j + 1];
+        double zE = (kz < 0.0) ? zv[kk] : zv[kk + 1];
+        dsx = (fabs(kx) > 1e-15) ? (xE - x) / kx : DBL_MAX;
+        dsy = (fabs(ky) > 1e-15) ? (yE - y) / ky : DBL_MAX;
+        dsz = (fabs(kz) > 1e-15) ? (zE - z) / kz : DBL_MAX;
+        if (dsx <= dsy && dsx <= dsz) {
+            ds = dsx; p.add(m, ds);
+            i += (kx < 0.0) ? -1 : 1;
+            if (i >= g.Nx || i < 0) return;
+            x = xE; y += ky * ds; z += kz * ds;
+        } else if (dsy < dsx && dsy <= dsz) {
+            ds = dsy; p.add(m, ds);
+            j += (ky < 0.0) ? -1 : 1;
+            if (j >= g.Ny || j < 0) return;
+            x += kx * ds; y = yE; z += kz * ds;
+        } else if (dsz < dsx && dsz < dsy) {
+            ds = dsz; p.add(m, ds);
+            kk += (kz < 0.0) ? -1 : 1;
+            if (kk >= g.Nz || kk < 0) return;
+            x += kx * ds; y += ky * ds; z = zE;
+        } else {
+            return;  // NaN guard: the reference would loop forever here
+        }
+    }
+}
+
+// TreeNode::whichnode(r) from the root (TreeNode.cpp:70-80), OctTreeNode::child(r)
+int rootWhichnode(const OctreeGrid& t, double x, double y, double z) {
+    const double* b = &t.box[0];
+    if (!(x >= b[0] && x <= b[3] && y >= b[1] && y <= b[4] && z >= b[2] && z <= b[5])) return -1;
+    int l = 0;
+    while (t.firstChild[l] >= 0) {
+        int c0 = t.firstChild[l];
+        const double* cb = &t.box[6 * (size_t)c0];
+        l = c0 + (x < cb[3] ? 0 : 1) + (y < cb[4] ? 0 : 2) + (z < cb[5] ? 0 : 4);
+    }
+    return l;
+}
+
+// TreeDustGrid::path, TopDown and Neighbor search (TreeDustGrid.cpp:390-521); moveInside
+// (DustGridPath.cpp:57-150)
+void octreePath(const OctreeGrid& t, Vec3 r, Vec3 k, Path& p) {
+    p.clear();
+    double kx = k.x, ky = k.y, kz = k.z, rx = r.x, ry = r.y, rz = r.z;
+    const double eps = t.eps;
+    const double bx0 = t.box[0], by0 = t.box[1], bz0 = t.box[2], bx1 = t.box[3], by1 = t.box[4], bz1 = t.box[5];
+    // moveInside
+    {
+        bool outside = false;
+        if (rx <= bx0) {
+            if (kx <= 0.0) outside = true;
+            else { double ds = (bx0 - rx) / kx; p.add(-1, ds); rx = bx0 + eps; ry += ky * ds; rz += kz * ds; }
+        } else if (rx >= bx1) {
+            if (kx >= 0.0) outside = true;
+            else { double ds = (bx1 - rx) / kx; p.add(-1, ds); rx = bx1 - eps; ry += ky * ds; rz += kz * ds; }
+        }
+        if (!outside) {
+            if (ry <= by0) {
+                if (ky <= 0.0) outside = true;
+                else { double ds = (by0 - ry) / ky; p.add(-1, ds); rx += kx * ds; ry = by0 + eps; rz += kz * ds; }
+            } else if (ry >= by1) {
+                if (ky >= 0.0) outside = true;
+                else { double ds = (by1 - ry) / ky; p.add(-1, ds); rx += kx * ds; ry = by1 - eps; rz += kz * ds; }
+            }
+        }
+        if (!outside) {
+            if (rz <= bz0) {
+                if (kz <= 0.0) outside = true;
+                else { double ds = (bz0 - rz) / kz; p.add(-1, ds); rx += kx * ds; ry += ky * ds; rz = bz0 + eps; }
+            } else if (rz >= bz1) {
+                if (kz >= 0.0) outside = true;
+                else { double ds = (bz1 - rz) / kz; p.add(-1, ds); rx += kx * ds; ry += ky * ds; rz = bz1 - eps; }
+            }
+        }
+        if (outside) { rx = ry = rz = INFINITY; }
+    }
+    int node = rootWhichnode(t, rx, ry, rz);
+    if (node < 0) return p.clear();
+    double x = rx, y = ry, z = rz;
+    while (node >= 0) {
+        const double* b = &t.box[6 * (size_t)node];
+        double xnext = (kx < 0.0) ? b[0] : b[3];
+        double ynext = (ky < 0.0) ? b[1] : b[4];
+        double znext = (kz < 0.0) ? b[2] : b[5];
+        double dsx = (fabs(kx) > 1e-15) ? (xnext - x) / kx : DBL_MAX;
+        double dsy = (fabs(ky) > 1e-15) ? (ynext - y) / ky : DBL_MAX;
+        double dsz = (fabs(kz) > 1e-15) ? (znext - z) / kz : DBL_MAX;
+        double ds;
+        int wall;
+        if (dsx <= dsy && dsx <= dsz) { ds = dsx; wall = (kx < 0.0) ? 0 : 1; }
+        else if (dsy <= dsx && dsy <= dsz) { ds = dsy; wall = (ky < 0.0) ? 2 : 3; }
+        else { ds = dsz; wall = (kz < 0.0) ? 4 : 5; }
+        p.add(t.cellnumber[node], ds);
+        x += (ds + eps) * kx;
+        y += (ds + eps) * ky;
+        z += (ds + eps) * kz;
+        int oldnode = node;
+        if (t.search == 0) {
+            node = rootWhichnode(t, x, y, z);
+        } else {
+            node = -1;
+            size_t q = 6 * (size_t)oldnode + wall;
+            for (int n = t.nbrOffset[q]; n < t.nbrOffset[q + 1]; n++) {
+                int c = t.nbrList[n];
+                const double* cb = &t.box[6 * (size_t)c];
+                if (x >= cb[0] && x <= cb[3] && y >= cb[1] && y <= cb[4] && z >= cb[2] && z <= cb[5]) { node = c; break; }
+            }
+            if (node < 0) node = rootWhichnode(t, x, y, z);
+        }
+        if (node == oldnode) {
+            x = nextafter(x, (kx < 0.0) ? -DBL_MAX : DBL_MAX);
+            y = nextafter(y, (ky < 0.0) ? -DBL_MAX : DBL_MAX);
+            z = nextafter(z, (kz < 0.0) ? -DBL_MAX : DBL_MAX);
+            node = rootWhichnode(t, x, y, z);
+            if (node == oldnode) break;
+        }
+    }
+}
+
+// ============================================================ simulation
+
+struct Tallies {
+    std::vector<double> labs;  // Ncells x Nlambda row-major (stellar)
+    std::vector<double> labsDust;
+    std::vector<std::vector<double>> frames, seds;  // per instrument
+    uint64_t segments = 0;
+};
+
+class Sim {
+public:
+    Sim(const Model& m) : M(m) {}
+
+    const Model& M;
+
+    void path(Vec3 r, Vec3 k, Path& p) const {
+        if (M.grid.kind == GridKind::Cartesian) cartesianPath(M.grid.cart, r, k, p);
+        else {
+            if (M.grid.tree.search == 2) throw std::runtime_error("Bookkeeping tree search is not supported");
+            octreePath(M.grid.tree, r, k, p);
+        }
+    }
+
+    void initTallies(Tallies& t) const {
+        if (M.hasDust && M.storeAbsorption) t.labs.assign((size_t)M.ncells() * M.wl.n(), 0.0);
+        t.frames.resize(M.instruments.size());
+        t.seds.resize(M.instruments.size());
+        for (size_t i = 0; i < M.instruments.size(); i++) {
+            const Instrument& ins = M.instruments[i];
+            if (ins.hasFrames()) t.frames[i].assign((size_t)ins.nslots() * M.wl.n() * ins.nframe(), 0.0);
+            if (ins.hasSeds()) t.seds[i].assign((size_t)ins.nslots() * M.wl.n(), 0.0);
+        }
+    }
+
+    struct Packet {
+        double L;
+        int ell;
+        Vec3 r, k;
+        int nscatt;
+        int stellar;  // component index, or -1 for dust emission
+    };
+
+    // Instrument::detect for the four distant-instrument kinds
+    void detect(Tallies& t, int i, const Packet& pp, Path& tmp) const {
+        const Instrument& ins = M.instruments[i];
+        int nscatt = pp.nscatt, ell = pp.ell, Nl = M.wl.n();
+        double L = pp.L;
+        int l = ins.kind == InstrumentKind::SED ? -1 : ins.pixel(pp.r.x, pp.r.y, pp.r.z);
+        if (ins.kind == InstrumentKind::Frame && l < 0) return;
+        double taupath = 0;
+        if (M.hasDust) {
+            Vec3 ko{ins.kobs[0], ins.kobs[1], ins.kobs[2]};
+            path(pp.r, ko, tmp);
+            t.segments += tmp.v.size();
+            for (auto& s : tmp.v) taupath += M.kapparho(s.m, ell) * s.ds;
+        }
+        double extf = exp(-taupath);
+        double Lextf = L * extf;
+        auto sed = [&](int slot, double v) { t.seds[i][(size_t)slot * Nl + ell] += v; };
+        auto frm = [&](int slot, double v) {
+            if (l >= 0) t.frames[i][((size_t)slot * Nl + ell) * ins.nframe() + l] += v;
+        };
+        if (ins.kind != InstrumentKind::Full) {
+            if (ins.hasSeds()) sed(0, Lextf);
+            if (ins.hasFrames()) frm(0, Lextf);
+            return;
+        }
+        for (int pass = 0; pass < 2; pass++) {
+            auto add = [&](int slot, double v) { if (pass == 0) sed(slot, v); else frm(slot, v); };
+            if (pp.stellar >= 0) {
+                if (nscatt == 0) {
+                    add(SlotTrav, L);
+                    if (M.hasDust) add(SlotStrDir, Lextf);
+                } else {
+                    add(SlotStrSca, Lextf);
+                    if (nscatt <= ins.scatteringLevels) add(SlotLevel0 + nscatt - 1, Lextf);
+                }
+            } else {
+                if (nscatt == 0) add(SlotDusDir, Lextf);
+                else add(SlotDusSca, Lextf);
+            }
+        }
+    }
+
+    // the photon life cycle after launch: MonteCarloSimulation.cpp:283-293
+    void lifeCycle(Tallies& t, Rng& rng, Packet& pp, double Lthreshold, bool peel, bool store,
+                   std::vector<double>* labs, Path& p, Path& tmp) const {
+        int Ncomp = M.ncomp();
+        int Nl = M.wl.n();
+        if (peel)
+            for (size_t i = 0; i < M.instruments.size(); i++) detect(t, (int)i, pp, tmp);  // peeloffemission
+        while (true) {
+            // DustSystem::fillOpticalDepth
+            path(pp.r, pp.k, p);
+            t.segments += p.v.size();
+            double tau = 0;
+            for (auto& s : p.v) {
+                double dtau = M.kapparho(s.m, pp.ell) * s.ds;
+                tau += dtau;
+                s.dtau = dtau;
+                s.tau = tau;
+            }
+            double taupath = p.v.empty() ? 0 : p.v.back().tau;
+            if (taupath < 0.0 || std::isnan(taupath) || std::isinf(taupath))
+                throw std::runtime_error("the optical depth along the path is not a positive number");
+            // simulateescapeandabsorption
+            double L = pp.L;
+            if (Ncomp == 1) {
+                double albedo = M.dust[0].mix.albedo[pp.ell];
+                double expfactor = -expm1(-taupath);
+                if (store) {
+                    int N = (int)p.v.size();
+                    for (int n = 0; n < N; n++) {
+                        int m = p.v[n].m;
+                        if (m != -1) {
+                            double taustart = (n == 0) ? 0.0 : p.v[n - 1].tau;
+                            double expfactorm = -expm1(-p.v[n].dtau);
+                            double Lintm = L * exp(-taustart) * expfactorm;
+                            double Labsm = (1.0 - albedo) * Lintm;
+                            (*labs)[(size_t)m * Nl + pp.ell] += Labsm;
+                        }
+                    }
+                }
+                pp.L = L * albedo * expfactor;
+            } else {
+                double Lsca = 0.0;
+                int N = (int)p.v.size();
+                for (int n = 0; n < N; n++) {
+                    int m = p.v[n].m;
+                    if (m != -1) {
+                        double ksca = 0.0, kext = 0.0;
+                        for (int h = 0; h < Ncomp; h++) {
+                            double rho = M.rho[(size_t)m * Ncomp + h];
+                            ksca += rho * M.dust[h].mix.ksca[pp.ell];
+                            kext += rho * M.dust[h].mix.kext[pp.ell];
+                        }
+                        double albedo = (kext > 0.0) ? ksca / kext : 0.0;
+                        double taustart = (n == 0) ? 0.0 : p.v[n - 1].tau;
+                        double expfactorm = -expm1(-p.v[n].dtau);
+                        double Lintm = L * exp(-taustart) * expfactorm;
+                        Lsca += albedo * Lintm;
+                        if (store) (*labs)[(size_t)m * Nl + pp.ell] += (1.0 - albedo) * Lintm;
+                    }
+                }
+                pp.L = Lsca;
+            }
+            if (pp.L <= 0 || (pp.L <= Lthreshold && pp.nscatt >= M.minScattEvents)) break;
+            // simulatepropagation
+            if (taupath != 0.0) {
+                double tauint;
+                double xi = M.scattBias;
+                if (xi == 0.0) tauint = exponcutoff(rng, taupath);
+                else {
+                    double X = rng.uniform();
+                    tauint = (X < xi) ? rng.uniform() * taupath : exponcutoff(rng, taupath);
+                    double pr = -exp(-tauint) / expm1(-taupath);
+                    double q = (1.0 - xi) * pr + xi / taupath;
+                    double weight = pr / q;
+                    pp.L = pp.L * weight;
+                }
+                // DustGridPath::pathlength (DustGridPath.cpp:162-173) with NR::locate on the tau column
+                double s = 0;
+                int N = (int)p.v.size();
+                if (N > 0 && tauint > 0) {
+                    int i;
+                    if (tauint < p.v[0].tau) i = -1;
+                    else if (p.v[N - 1].tau < tauint) i = N - 1;
+                    else {
+                        int jl = -1, ju = N;
+                        while (ju - jl > 1) { int jm = (ju + jl) >> 1; if (tauint < p.v[jm].tau) ju = jm; else jl = jm; }
+                        i = (jl <= 0) ? 0 : (jl >= N - 2) ? N - 2 : jl;
+                    }
+                    auto lin = [](double x, double x1, double x2, double f1, double f2) { return f1 + ((x - x1) / (x2 - x1)) * (f2 - f1); };
+                    if (i < 0) s = lin(tauint, 0, p.v[0].tau, 0, p.v[0].s);
+                    else if (i < N - 1) s = lin(tauint, p.v[i].tau, p.v[i + 1].tau, p.v[i].s, p.v[i + 1].s);
+                    else s = p.v[N - 1].s;
+                }
+                pp.r = {pp.r.x + s * pp.k.x, pp.r.y + s * pp.k.y, pp.r.z + s * pp.k.z};
+            }
+            // peeloffscattering (MonteCarloSimulation.cpp:319-363), unpolarized
+            if (peel) {
+                double wv[16];
+                bool ok = true;
+                if (Ncomp == 1) wv[0] = 1.0;
+                else {
+                    int m = M.grid.whichcell(pp.r.x, pp.r.y, pp.r.z);
+                    if (m == -1) ok = false;
+                    else {
+                        double sum = 0;
+                        for (int h = 0; h < Ncomp; h++) wv[h] = M.dust[h].mix.ksca[pp.ell] * M.rho[(size_t)m * Ncomp + h];
+                        for (int h = 0; h < Ncomp; h++) sum += wv[h];
+                        if (sum <= 0) ok = false;
+                        else for (int h = 0; h < Ncomp; h++) wv[h] /= sum;
+                    }
+                }
+                if (ok) {
+                    for (size_t i = 0; i < M.instruments.size(); i++) {
+                        const Instrument& ins = M.instruments[i];
+                        double I = 0;
+                        for (int h = 0; h < Ncomp; h++) {
+                            double cosalpha = pp.k.x * ins.kobs[0] + pp.k.y * ins.kobs[1] + pp.k.z * ins.kobs[2];
+                            double g = M.dust[h].mix.g[pp.ell];
+                            double tt = 1.0 + g * g - 2 * g * cosalpha;
+                            double w = wv[h] * ((1.0 - g) * (1.0 + g) / sqrt(tt * tt * tt));
+                            I += w * 1.0;
+                        }
+                        Packet ppp = pp;
+                        ppp.L = pp.L * I;
+                        ppp.k = {ins.kobs[0], ins.kobs[1], ins.kobs[2]};
+                        ppp.nscatt = pp.nscatt + 1;
+                        detect(t, (int)i, ppp, tmp);
+                    }
+                }
+            }
+            // simulatescattering: DustSystem::randomMixForPosition + HG sampling (DustMix.cpp:609-613)
+            int hmix = 0;
+            if (Ncomp > 1) {
+                int m = M.grid.whichcell(pp.r.x, pp.r.y, pp.r.z);
+                if (m >= 0) {
+                    std::vector<double> Xv(Ncomp + 1, 0.0);
+                    for (int h = 0; h < Ncomp; h++) Xv[h + 1] = Xv[h] + M.dust[h].mix.ksca[pp.ell] * M.rho[(size_t)m * Ncomp + h];
+                    double norm = Xv[Ncomp];
+                    for (auto& v : Xv) v /= norm;
+                    double X = rng.uniform();
+                    int jl;
+                    if (X < Xv[0]) jl = 0;
+                    else { int lo = -1, hi = Ncomp; while (hi - lo > 1) { int jm = (hi + lo) >> 1; if (X < Xv[jm]) hi = jm; else lo = jm; } jl = lo; }
+                    hmix = jl;
+                }
+            }
+            double g = M.dust[hmix].mix.g[pp.ell];
+            Vec3 knew;
+            if (fabs(g) < 1e-6) knew = isotropic(rng);
+            else {
+                double f = ((1.0 - g) * (1.0 + g)) / (1.0 - g + 2.0 * g * rng.uniform());
+                double costheta = (1.0 + g * g - f * f) / (2.0 * g);
+                knew = rotated(rng, pp.k, costheta);
+            }
+            pp.nscatt++;
+            pp.k = knew;
+        }
+    }
+
+    // StellarSystem::launch + GeometricStellarComp::launch + PlummerGeometry/SpheGeometry sampling
+    void launchStellar(Rng& rng, Packet& pp, int ell, double L) const {
+        int N = (int)M.starL.size();
+        int h = 0;
+        double Lw = L;
+        if (N > 1) {
+            double X = rng.uniform();
+            double xi = M.starEmissionBias;
+            if (X < xi) h = std::max(0, std::min(N - 1, static_cast<int>(N * X / xi)));
+            else {
+                const std::vector<double>& Xv = M.starX[ell];
+                double q = (X - xi) / (1.0 - xi);
+                int n = (int)Xv.size();
+                if (q < Xv[0]) h = 0;
+                else { int lo = -1, hi = n - 1; while (hi - lo > 1) { int jm = (hi + lo) >> 1; if (q < Xv[jm]) hi = jm; else lo = jm; } h = lo; }
+            }
+            double Lh = M.starL[h][ell];
+            if (Lh > 0) {
+                double Lmean = M.starLtot[ell] / N;
+                double weight = 1.0 / (1.0 - xi + xi * Lmean / Lh);
+                Lw = L * weight;
+            } else {
+                pp = Packet{0., ell, {0, 0, 0}, {0, 0, 1}, 0, h};
+                return;
+            }
+        }
+        const Geometry& geo = M.starGeom[h];
+        // PlummerGeometry::randomradius then SpheGeometry::generatePosition
+        double t = pow(rng.uniform(), 1.0 / 3.0);
+        double r = geo.c * t / sqrt((1.0 - t) * (1.0 + t));
+        Vec3 d = isotropic(rng);
+        Vec3 pos{r * d.x, r * d.y, r * d.z};
+        Vec3 k = isotropic(rng);
+        pp = Packet{Lw, ell, pos, k, 0, h};
+    }
+};
+
+}  // namespace
+
+struct OracleRun {
+    std::unique_ptr<Model> model;
+    Tallies tal;
+    double seconds = 0;
+    uint64_t packets = 0;
+};
+
+extern "C" {
+
+const char* oracle_last_error(void) { return g_error.c_str(); }
+
+void oracle_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) { philox(ctr, key, out); }
+
+OracleRun* oracle_run(const char* ski, const char* datadir, int rngKind, int nthreads, double packages,
+                      uint64_t seed, uint64_t packet_begin, uint64_t packet_end, int phases, const char* outprefix) {
+    try {
+        auto run = std::make_unique<OracleRun>();
+        // the MT stream must be seeded before setup, so the seed is read from the XML first
+        unsigned long theSeed = seed ? (unsigned long)seed : readSkiSeed(ski);
+        std::string dd = datadir && *datadir ? datadir : defaultDataDir();
+        MTRandom mt(theSeed);
+        run->model = std::make_unique<Model>(loadSki(ski, mt, dd));
+        Model& M = *run->model;
+        M.seed = theSeed;
+        if (packages > 0) M.packages = packages;
+        (void)phases;
+        Sim sim(M);
+        sim.initTallies(run->tal);
+        int Nl = M.wl.n();
+        uint64_t Npp = (uint64_t)std::ceil(M.packages);  // setChunkParams with one chunk
+        uint64_t total = Npp * (uint64_t)Nl;
+        uint64_t pb = packet_begin, pe = packet_end ? std::min<uint64_t>(packet_end, total) : total;
+        bool store = M.hasDust && M.storeAbsorption;
+        auto t0 = std::chrono::steady_clock::now();
+
+        if (rngKind == ORACLE_RNG_MT) {
+            // dostellaremissionchunk for chunk index ell = 0 .. Nlambda-1, one chunk per wavelength
+            MTRng rng(&mt);
+            Path p, tmp;
+            p.v.reserve(1024);
+            tmp.v.reserve(1024);
+            for (int ell = 0; ell < Nl; ell++) {
+                double L = M.starLtot[ell] / Npp;
+                if (!(L > 0)) continue;
+                double Lthreshold = L / M.minWeightReduction;
+                for (uint64_t i = 0; i < Npp; i++) {
+                    Sim::Packet pp;
+                    sim.launchStellar(rng, pp, ell, L);
+                    run->packets++;
+                    if (pp.L > 0) {
+                        if (M.hasDust)
+                            sim.lifeCycle(run->tal, rng, pp, Lthreshold, true, store, &run->tal.labs, p, tmp);
+                        else
+                            for (size_t q = 0; q < M.instruments.size(); q++) sim.detect(run->tal, (int)q, pp, tmp);
+                    }
+                }
+            }
+        } else {
+            int T = std::max(1, nthreads);
+            std::vector<Tallies> part(T);
+            std::vector<std::thread> th;
+            std::atomic<uint64_t> next{pb};
+            const uint64_t grain = 256;
+            std::vector<std::string> errs(T);
+            std::vector<uint64_t> cnt(T, 0);
+            for (int w = 0; w < T; w++) {
+                th.emplace_back([&, w] {
+                    try {
+                        Tallies& tl = part[w];
+                        sim.initTallies(tl);
+                        PhiloxRng rng(theSeed, 0);
+                        Path p, tmp;
+                        p.v.reserve(1024);
+                        tmp.v.reserve(1024);
+                        while (true) {
+                            uint64_t b = next.fetch_add(grain);
+                            if (b >= pe) break;
+                            uint64_t e = std::min(pe, b + grain);
+                            for (uint64_t pk = b; pk < e; pk++) {
+                                int ell = (int)(pk / Npp);
+                                double L = M.starLtot[ell] / Npp;
+                                if (!(L > 0)) continue;
+                                double Lthreshold = L / M.minWeightReduction;
+                                rng.start(pk);
+                                Sim::Packet pp;
+                                sim.launchStellar(rng, pp, ell, L);
+                                cnt[w]++;
+                                if (pp.L > 0) {
+                                    if (M.hasDust)
+                                        sim.lifeCycle(tl, rng, pp, Lthreshold, true, store, &tl.labs, p, tmp);
+                                    else
+                                        for (size_t q = 0; q < M.instruments.size(); q++) sim.detect(tl, (int)q, pp, tmp);
+                                }
+                            }
+                        }
+                    } catch (std::exception& ex) {
+                        errs[w] = ex.what();
+                    }
+                });
+            }
+            for (auto& x : th) x.join();
+            for (int w = 0; w < T; w++)
+                if (!errs[w].empty()) throw std::runtime_error(errs[w]);
+            // deterministic reduction in worker order
+            for (int w = 0; w < T; w++) {
+                Tallies& tl = part[w];
+                run->packets += cnt[w];
+                run->tal.segments += tl.segments;
+                for (size_t q = 0; q < tl.labs.size(); q++) run->tal.labs[q] += tl.labs[q];
+                for (size_t i = 0; i < tl.frames.size(); i++) {
+                    for (size_t q = 0; q < tl.frames[i].size(); q++) run->tal.frames[i][q] += tl.frames[i][q];
+                    for (size_t q = 0; q < tl.seds[i].size(); q++) run->tal.seds[i][q] += tl.seds[i][q];
+                }
+            }
+        }
+        run->seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        if (outprefix && *outprefix) {
+            writeOutputs(M, outprefix, run->tal.frames, run->tal.seds, run->tal.labs);
+        }
+        return run.release();
+    } catch (std::exception& ex) {
+        g_error = ex.what();
+        return nullptr;
+    }
+}
+
+const double* oracle_labs(OracleRun* r, int* ncells, int* nlambda) {
+    *ncells = r->model->ncells();
+    *nlambda = r->model->wl.n();
+    return r->tal.labs.empty() ? nullptr : r->tal.labs.data();
+}
+
+int oracle_num_instruments(OracleRun* r) { return (int)r->model->instruments.size(); }
+
+int oracle_instrument(OracleRun* r, int i, const double** frames, const double** seds, int* nslots, int* nframe,
+                      int* nlambda) {
+    if (i < 0 || i >= (int)r->model->instruments.size()) return -1;
+    const Instrument& ins = r->model->instruments[i];
+    *frames = r->tal.frames[i].empty() ? nullptr : r->tal.frames[i].data();
+    *seds = r->tal.seds[i].empty() ? nullptr : r->tal.seds[i].data();
+    *nslots = ins.nslots();
+    *nframe = ins.hasFrames() ? ins.nframe() : 0;
+    *nlambda = r->model->wl.n();
+    return 0;
+}
+
+double oracle_seconds(OracleRun* r) { return r->seconds; }
+uint64_t oracle_packets(OracleRun* r) { return r->packets; }
+uint64_t oracle_segments(OracleRun* r) { return r->tal.segments; }
+void oracle_free(OracleRun* r) { delete r; }
+
+}  // extern "C"

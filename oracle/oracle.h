@@ -1,0 +1,69 @@
+/* CPU ORACLE for the SKIRT photon-shooting hot path -- TEST INFRASTRUCTURE ONLY.
+ *
+ * This library is the checker, never the product: only tests/, __graft_entry__.smoke() and
+ * bench.py's cpu_baseline leg may load it. It restates, in plain single-threaded C++ that follows the
+ * reference line by line, the per-packet life cycle of SKIRT v7.3:
+ *   MonteCarloSimulation::dostellaremissionchunk   SKIRTcore/MonteCarloSimulation.cpp:265-301
+ *   peeloffemission / peeloffscattering           MonteCarloSimulation.cpp:305-363
+ *   simulateescapeandabsorption                   MonteCarloSimulation.cpp:438-515
+ *   simulatepropagation / simulatescattering      MonteCarloSimulation.cpp:519-549
+ *   PanMonteCarloSimulation dust phases           PanMonteCarloSimulation.cpp:187-344
+ *   CartesianDustGrid::path                       CartesianDustGrid.cpp:136-283
+ *   TreeDustGrid::path (TopDown, Neighbor)        TreeDustGrid.cpp:390-521, DustGridPath.cpp:46-173
+ *   FullInstrument/Simple/SED/Frame ::detect      FullInstrument.cpp:107-174 etc.
+ *   Random uniform/exponcutoff/direction          Random.cpp:89-222
+ *
+ * Two random-number modes:
+ *   ORACLE_RNG_MT     one MT19937 stream continuing from model setup, packets in the reference's
+ *                     order -- bit-for-bit the output of `skirt -t 1` (pinned by tests/golden).
+ *   ORACLE_RNG_PHILOX one Philox4x32-10 stream per packet, keyed exactly like the GPU engine
+ *                     (see DESIGN.md "Random numbers"), so GPU and oracle agree packet by packet.
+ * Model setup (ski parsing, grids, densities, tables) is shared with the product host library.
+ */
+#ifndef SKIRT_ORACLE_H
+#define SKIRT_ORACLE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum { ORACLE_RNG_MT = 0, ORACLE_RNG_PHILOX = 1 };
+enum { ORACLE_PHASE_STELLAR = 0, ORACLE_PHASE_ALL = 1 };
+
+typedef struct OracleRun OracleRun;
+
+/* Builds the model from `ski` and runs it on the CPU.
+ *  rng          ORACLE_RNG_MT or ORACLE_RNG_PHILOX
+ *  nthreads     worker threads (Philox mode only; MT mode is single-threaded by definition)
+ *  packages     if > 0, overrides the ski's packages (photon packets per wavelength)
+ *  seed         if nonzero, overrides the ski's random seed
+ *  packet_begin/packet_end  Philox mode only: restrict the stellar phase to this global packet range
+ *               (end == 0 means all packets)
+ *  outprefix    if non-NULL, writes SKIRT-format outputs (<prefix>_<instr>_sed.dat, FITS frames, ds_isrf)
+ * Returns NULL on failure (see oracle_last_error()). */
+OracleRun* oracle_run(const char* ski, const char* datadir, int rng, int nthreads, double packages,
+                      uint64_t seed, uint64_t packet_begin, uint64_t packet_end, int phases,
+                      const char* outprefix);
+const char* oracle_last_error(void);
+
+/* Labs(m, ell) row-major, Ncells x Nlambda (stellar + dust), as DustSystem::Labs */
+const double* oracle_labs(OracleRun* r, int* ncells, int* nlambda);
+/* instrument accumulators before calibration: frames [nslots][nlambda][nframe], seds [nslots][nlambda] */
+int oracle_instrument(OracleRun* r, int i, const double** frames, const double** seds, int* nslots,
+                      int* nframe, int* nlambda);
+int oracle_num_instruments(OracleRun* r);
+/* statistics: number of packets launched, path segments traversed, wall seconds of the photon phases */
+double oracle_seconds(OracleRun* r);
+uint64_t oracle_packets(OracleRun* r);
+uint64_t oracle_segments(OracleRun* r);
+void oracle_free(OracleRun* r);
+
+/* Philox4x32-10 known-answer access for tests: out[4] = philox(ctr[4], key[2]) */
+void oracle_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,906 @@
+// .ski file -> Model, including every setup step that consumes random numbers.
+//
+// The reference performs these steps in SimulationItem::setup() order (SimulationItem.cpp:18-31):
+// wavelength grid, stellar system (StellarSystem.cpp:35-52), dust mixes (DustMix.cpp:44-264), the dust
+// grid (TreeDustGrid.cpp:50-164 draws density samples while subdividing), then the cell densities
+// (DustSystem.cpp:63-178, 100 random positions per cell) and the instruments. Random draws happen only
+// in the tree subdivision and the cell density sampling, in that order; both are reproduced here on the
+// caller's UniformSource so that a single-threaded reference run and this setup produce bit-identical
+// densities and trees.
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <dlfcn.h>
+#include <fstream>
+#include <numeric>
+#include <sstream>
+#include <stdexcept>
+
+#include "model.hpp"
+#include "xml.hpp"
+
+namespace skirt {
+
+// ============================================================ small numeric helpers (Fundamentals/NR.hpp)
+namespace nr {
+
+// NR::locate_basic_impl / locate / locate_clip / locate_fail (NR.hpp Array versions)
+static int locateBasic(const std::vector<double>& xv, double x, int n) {
+    int jl = -1, ju = n;
+    while (ju - jl > 1) {
+        int jm = (ju + jl) >> 1;
+        if (x < xv[jm]) ju = jm;
+        else jl = jm;
+    }
+    return jl;
+}
+static int locate(const std::vector<double>& xv, double x) {
+    int n = (int)xv.size();
+    if (x == xv[n - 1]) return n - 2;
+    return locateBasic(xv, x, n);
+}
+static int locateFail(const std::vector<double>& xv, double x) {
+    int n = (int)xv.size();
+    if (x > xv[n - 1]) return -1;
+    return locateBasic(xv, x, n - 1);
+}
+static double interpolateLinLin(double x, double x1, double x2, double f1, double f2) {
+    return f1 + ((x - x1) / (x2 - x1)) * (f2 - f1);
+}
+static double interpolateLogLin(double x, double x1, double x2, double f1, double f2) {
+    x = std::log10(x);
+    x1 = std::log10(x1);
+    x2 = std::log10(x2);
+    return f1 + ((x - x1) / (x2 - x1)) * (f2 - f1);
+}
+static double interpolateLogLog(double x, double x1, double x2, double f1, double f2) {
+    x = std::log10(x);
+    x1 = std::log10(x1);
+    x2 = std::log10(x2);
+    bool logf = f1 > 0 && f2 > 0;
+    if (logf) {
+        f1 = std::log10(f1);
+        f2 = std::log10(f2);
+    }
+    double fx = f1 + ((x - x1) / (x2 - x1)) * (f2 - f1);
+    if (logf) fx = std::pow(10, fx);
+    return fx;
+}
+// NR::resample (NR.hpp:355-378)
+template <double interp(double, double, double, double, double)>
+static std::vector<double> resample(const std::vector<double>& xres, const std::vector<double>& xori,
+                                    const std::vector<double>& yori) {
+    int Nori = (int)xori.size();
+    double xmin = xori[0], xmax = xori[Nori - 1];
+    std::vector<double> yres(xres.size(), 0.0);
+    for (size_t l = 0; l < xres.size(); l++) {
+        double x = xres[l];
+        if (std::fabs(1.0 - x / xmin) < 1e-5) yres[l] = yori[0];
+        else if (std::fabs(1.0 - x / xmax) < 1e-5) yres[l] = yori[Nori - 1];
+        else if (x < xmin || x > xmax) yres[l] = 0.0;
+        else {
+            int k = locate(xori, x);
+            yres[l] = interp(x, xori[k], xori[k + 1], yori[k], yori[k + 1]);
+        }
+    }
+    return yres;
+}
+// NR::cdf with a source vector (NR.hpp:388-394)
+static void cdf(std::vector<double>& Pv, const std::vector<double>& pv) {
+    size_t n = pv.size();
+    Pv.assign(n + 1, 0.0);
+    for (size_t i = 0; i < n; i++) Pv[i + 1] = Pv[i] + pv[i];
+    double norm = Pv[n];
+    for (auto& v : Pv) v /= norm;
+}
+static double sum(const std::vector<double>& v) { return std::accumulate(v.begin(), v.end(), 0.); }
+
+}  // namespace nr
+
+// ============================================================ model member functions
+
+double Geometry::density(double x, double y, double z) const {
+    switch (kind) {
+    case GeometryKind::Plummer: {
+        double r = std::sqrt(x * x + y * y + z * z);  // Position::radius -> Vec::norm
+        double s = r / c;
+        return rho0 * std::pow(1.0 + s * s, -2.5);
+    }
+    }
+    return 0;
+}
+
+double WavelengthGrid::lambdamin(int ell) const {
+    return (ell == 0) ? lambda[0] : std::sqrt(lambda[ell - 1] * lambda[ell]);
+}
+double WavelengthGrid::lambdamax(int ell) const {
+    int N = n();
+    return (ell == N - 1) ? lambda[N - 1] : std::sqrt(lambda[ell] * lambda[ell + 1]);
+}
+
+void DustGrid::cellBox(int m, double b[6]) const {
+    if (kind == GridKind::Cartesian) {
+        const CartesianGrid& g = cart;
+        int i = m / (g.Nz * g.Ny), j = (m / g.Nz) % g.Ny, k = m % g.Nz;  // CartesianDustGrid::box
+        b[0] = g.xv[i]; b[1] = g.yv[j]; b[2] = g.zv[k];
+        b[3] = g.xv[i + 1]; b[4] = g.yv[j + 1]; b[5] = g.zv[k + 1];
+    } else {
+        int l = tree.idv[m];
+        for (int q = 0; q < 6; q++) b[q] = tree.box[6 * (size_t)l + q];
+    }
+}
+
+double DustGrid::cellVolume(int m) const {
+    double b[6];
+    cellBox(m, b);
+    return (b[3] - b[0]) * (b[4] - b[1]) * (b[5] - b[2]);
+}
+
+int DustGrid::whichcell(double x, double y, double z) const {
+    if (kind == GridKind::Cartesian) {
+        int i = nr::locateFail(cart.xv, x), j = nr::locateFail(cart.yv, y), k = nr::locateFail(cart.zv, z);
+        if (i < 0 || j < 0 || k < 0) return -1;
+        return k + cart.Nz * j + cart.Nz * cart.Ny * i;
+    }
+    const double* b = &tree.box[0];
+    if (!(x >= b[0] && x <= b[3] && y >= b[1] && y <= b[4] && z >= b[2] && z <= b[5])) return -1;
+    int l = 0;
+    while (tree.firstChild[l] >= 0) {
+        int c0 = tree.firstChild[l];
+        const double* cb = &tree.box[6 * (size_t)c0];
+        l = c0 + (x < cb[3] ? 0 : 1) + (y < cb[4] ? 0 : 2) + (z < cb[5] ? 0 : 4);
+    }
+    return tree.cellnumber[l];
+}
+
+int Instrument::pixel(double x, double y, double z) const {
+    double xpp = -sinphi * x + cosphi * y;
+    double ypp = -cosphi * costheta * x - sinphi * costheta * y + sintheta * z;
+    double xp = cospa * xpp - sinpa * ypp;
+    double yp = sinpa * xpp + cospa * ypp;
+    int i = static_cast<int>(std::floor((xp - xpmin) / xpsiz));
+    int j = static_cast<int>(std::floor((yp - ypmin) / ypsiz));
+    if (i < 0 || i >= Nx || j < 0 || j >= Ny) return -1;
+    return i + Nx * j;
+}
+
+double Model::kapparho(int m, int ell) const {
+    if (m < 0) return 0;
+    double result = 0;
+    int nc = ncomp();
+    for (int h = 0; h < nc; h++) result += dust[h].mix.kext[ell] * rho[(size_t)m * nc + h];
+    return result;
+}
+
+// ============================================================ data tables
+
+namespace {
+
+struct Table {
+    long nrows = 0, ncols = 0;
+    std::vector<double> v;
+    double at(long r, long c) const { return v[r * ncols + c]; }
+};
+
+Table readTable(const std::string& datadir, const std::string& name) {
+    std::string path = datadir + "/" + name;
+    FILE* f = std::fopen(path.c_str(), "rb");
+    if (!f) throw std::runtime_error("cannot open resource table " + path);
+    Table t;
+    int64_t hdr[2];
+    if (std::fread(hdr, sizeof(int64_t), 2, f) != 2) { std::fclose(f); throw std::runtime_error("bad table " + path); }
+    t.nrows = hdr[0];
+    t.ncols = hdr[1];
+    t.v.resize(t.nrows * t.ncols);
+    size_t got = std::fread(t.v.data(), sizeof(double), t.v.size(), f);
+    std::fclose(f);
+    if (got != t.v.size()) throw std::runtime_error("truncated table " + path);
+    return t;
+}
+
+// ============================================================ parsing helpers
+
+struct Ctx {
+    Units units;
+    std::string datadir;
+    UniformSource* rng;
+};
+
+double attr(const Ctx& c, const XmlElement* e, const char* key, const char* qty, double def) {
+    if (!e->has(key)) return def;
+    return c.units.parse(e->get(key), qty);
+}
+int attrInt(const XmlElement* e, const char* key, int def) {
+    if (!e->has(key)) return def;
+    return (int)std::lround(std::strtod(e->get(key).c_str(), nullptr));
+}
+bool attrBool(const XmlElement* e, const char* key, bool def) {
+    if (!e->has(key)) return def;
+    std::string v = e->get(key);
+    std::transform(v.begin(), v.end(), v.begin(), ::tolower);
+    return v == "true" || v == "yes" || v == "1";
+}
+std::vector<double> attrList(const Ctx& c, const XmlElement* e, const char* key, const char* qty) {
+    std::vector<double> out;
+    std::string s = e->get(key);
+    std::stringstream ss(s);
+    std::string item;
+    while (std::getline(ss, item, ',')) out.push_back(c.units.parse(item, qty));
+    return out;
+}
+const XmlElement* need(const XmlElement* e, const char* prop) {
+    const XmlElement* it = e->item(prop);
+    if (!it) throw std::runtime_error(std::string("missing property '") + prop + "' in " + e->name);
+    return it;
+}
+
+Geometry parseGeometry(const Ctx& c, const XmlElement* g) {
+    Geometry geo;
+    if (g->name == "PlummerGeometry") {
+        geo.kind = GeometryKind::Plummer;
+        geo.c = attr(c, g, "scale", "length", 0);
+        if (geo.c <= 0) throw std::runtime_error("the scale length c should be positive");
+        geo.rho0 = 0.75 / std::pow(geo.c, 3) / M_PI;
+    } else {
+        throw std::runtime_error("unsupported geometry " + g->name);
+    }
+    return geo;
+}
+
+// ------------------------------------------------------------ wavelength grids
+WavelengthGrid parseWavelengthGrid(const Ctx& c, const XmlElement* w) {
+    WavelengthGrid wl;
+    if (w->name == "OligoWavelengthGrid") {
+        wl.pan = false;
+        wl.lambda = attrList(c, w, "wavelengths", "wavelength");
+        std::sort(wl.lambda.begin(), wl.lambda.end());
+        wl.dlambda.resize(wl.lambda.size());
+        for (size_t ell = 0; ell < wl.lambda.size(); ell++) wl.dlambda[ell] = 0.001 * wl.lambda[ell];
+    } else if (w->name == "LogWavelengthGrid") {
+        wl.pan = true;
+        double lmin = attr(c, w, "minWavelength", "wavelength", 0);
+        double lmax = attr(c, w, "maxWavelength", "wavelength", 0);
+        int N = attrInt(w, "points", 0);
+        if (lmin <= 0 || lmax <= lmin || N < 3) throw std::runtime_error("invalid LogWavelengthGrid");
+        // NR::loggrid(_lambdav, lmin, lmax, N-1)  (LogWavelengthGrid.cpp, NR.hpp:269-275)
+        int n = N - 1;
+        wl.lambda.resize(n + 1);
+        double logxmin = std::log10(lmin);
+        double dlogx = std::log10(lmax / lmin) / n;
+        for (int i = 0; i <= n; i++) wl.lambda[i] = std::pow(10, logxmin + i * dlogx);
+        wl.dlambda.resize(N);
+        for (int ell = 0; ell < N; ell++) wl.dlambda[ell] = wl.lambdamax(ell) - wl.lambdamin(ell);
+    } else {
+        throw std::runtime_error("unsupported wavelength grid " + w->name);
+    }
+    for (int ell = 1; ell < wl.n(); ell++)
+        if (wl.lambda[ell] <= wl.lambda[ell - 1]) throw std::runtime_error("wavelengths should be sorted");
+    return wl;
+}
+
+// ------------------------------------------------------------ dust mixes
+// DustMix::setupSelfAfter part 1 (DustMix.cpp:47-89): population sums, albedo, g, kappa = sigma/mu
+void finishMix(DustMix& mix, const std::vector<double>& muv, const std::vector<std::vector<double>>& sabs,
+               const std::vector<std::vector<double>>& ssca, const std::vector<std::vector<double>>& gv, int Nlambda) {
+    int Npop = (int)muv.size();
+    if (Npop < 1) throw std::runtime_error("dust mixture must contain at least one dust population");
+    std::vector<double> sigmaabs(Nlambda), sigmasca(Nlambda), sigmaext(Nlambda);
+    mix.albedo.assign(Nlambda, 0);
+    mix.g.assign(Nlambda, 0);
+    for (int ell = 0; ell < Nlambda; ell++) {
+        double sumabs = 0.0, sumsca = 0.0, sumgsca = 0.0;
+        for (int c = 0; c < Npop; c++) {
+            sumabs += sabs[c][ell];
+            sumsca += ssca[c][ell];
+            sumgsca += gv[c][ell] * ssca[c][ell];
+        }
+        double sumext = sumabs + sumsca;
+        sigmaabs[ell] = sumabs;
+        sigmasca[ell] = sumsca;
+        sigmaext[ell] = sumext;
+        mix.albedo[ell] = sumext ? sumsca / sumext : 0.;
+        mix.g[ell] = sumsca ? sumgsca / sumsca : 0.;
+    }
+    double mu = 0.0;
+    for (int c = 0; c < Npop; c++) mu += muv[c];
+    mix.mu = mu;
+    mix.sigmaabs = sigmaabs;
+    mix.kabs.resize(Nlambda);
+    mix.ksca.resize(Nlambda);
+    mix.kext.resize(Nlambda);
+    for (int ell = 0; ell < Nlambda; ell++) {
+        mix.kabs[ell] = sigmaabs[ell] / mu;
+        mix.ksca[ell] = sigmasca[ell] / mu;
+        mix.kext[ell] = sigmaext[ell] / mu;
+    }
+}
+
+DustMix parseMix(const Ctx& c, const XmlElement* e, const WavelengthGrid& wl) {
+    DustMix mix;
+    mix.type = e->name;
+    int Nlambda = wl.n();
+    std::vector<double> muv;
+    std::vector<std::vector<double>> sabs, ssca, gv;
+    if (e->name == "SimpleOligoDustMix") {
+        // SimpleOligoDustMix.cpp setupSelfBefore: kappaabs = kext*(albedo+1), kappasca = kext*albedo,
+        // population mass 1/kext[0] (the reference's quirk is kept on purpose)
+        if (wl.pan) throw std::runtime_error("SimpleOligoDustMix requires an oligochromatic wavelength grid");
+        std::vector<double> kext = attrList(c, e, "opacities", "opacity");
+        std::vector<double> alb = attrList(c, e, "albedos", "");
+        std::vector<double> asy = attrList(c, e, "asymmetryParameters", "");
+        if ((int)kext.size() != Nlambda || (int)alb.size() != Nlambda || (int)asy.size() != Nlambda)
+            throw std::runtime_error("SimpleOligoDustMix property list length differs from the number of wavelengths");
+        std::vector<double> ka(Nlambda), ks(Nlambda), g(Nlambda);
+        for (int ell = 0; ell < Nlambda; ell++) {
+            ka[ell] = kext[ell] * (alb[ell] + 1.0);
+            ks[ell] = kext[ell] * alb[ell];
+            g[ell] = asy[ell];
+        }
+        double Mdust = 1.0 / kext[0];
+        if (Mdust > 0) { muv.push_back(Mdust); sabs.push_back(ka); ssca.push_back(ks); gv.push_back(g); }
+    } else if (e->name == "InterstellarDustMix") {
+        // InterstellarDustMix.cpp setupSelfBefore + DustMix::addpopulation with resampling
+        Table t = readTable(c.datadir, "InterstellarDustMix.bin");
+        const int N = 1064;
+        if (t.nrows != N || t.ncols != 6) throw std::runtime_error("unexpected InterstellarDustMix table shape");
+        std::vector<double> lambdav(N), kabsv(N), kscav(N), gvv(N);
+        for (int row = 0, k = N - 1; k >= 0; k--, row++) {
+            double lambda = t.at(row, 0), albedo = t.at(row, 1), asymmpar = t.at(row, 2), Kabs = t.at(row, 4);
+            lambda *= 1e-6;
+            Kabs *= 1e-1;
+            lambdav[k] = lambda;
+            kabsv[k] = Kabs;
+            kscav[k] = Kabs * albedo / (1.0 - albedo);
+            gvv[k] = asymmpar;
+        }
+        double eps = 0.5e-5;
+        if (wl.lambda[0] < lambdav[0] * (1 - eps) || wl.lambda[Nlambda - 1] > lambdav[N - 1] * (1 + eps))
+            throw std::runtime_error("dust properties not defined over the simulation's wavelength range");
+        muv.push_back(1.);
+        sabs.push_back(nr::resample<nr::interpolateLogLog>(wl.lambda, lambdav, kabsv));
+        ssca.push_back(nr::resample<nr::interpolateLogLog>(wl.lambda, lambdav, kscav));
+        gv.push_back(nr::resample<nr::interpolateLogLin>(wl.lambda, lambdav, gvv));
+    } else {
+        throw std::runtime_error("unsupported dust mix " + e->name);
+    }
+    finishMix(mix, muv, sabs, ssca, gv, Nlambda);
+    return mix;
+}
+
+// ------------------------------------------------------------ stellar components
+std::vector<double> sunLuminosityOligo(const Ctx& c, const WavelengthGrid& wl, const std::vector<double>& lum) {
+    // OligoStellarComp.cpp setupSelfBefore
+    Table t = readTable(c.datadir, "SunSED.bin");
+    int Ns = (int)t.nrows;
+    std::vector<double> lsun(Ns), Lsun(Ns);
+    for (int k = 0; k < Ns; k++) {
+        lsun[k] = t.at(k, 0) / 1e6;
+        Lsun[k] = t.at(k, 1) * 1e6;
+    }
+    std::vector<double> Lv(wl.n());
+    for (int ell = 0; ell < wl.n(); ell++) {
+        double lambda = wl.lambda[ell];
+        int k = nr::locateFail(lsun, lambda);
+        if (k < 0) throw std::runtime_error("the sun does not emit at the wavelength of the simulation");
+        double L = nr::interpolateLinLin(lambda, lsun[k], lsun[k + 1], Lsun[k], Lsun[k + 1]);
+        Lv[ell] = lum[ell] * L * wl.dlambda[ell];
+    }
+    return Lv;
+}
+
+std::vector<double> sunSedNormalized(const Ctx& c, const WavelengthGrid& wl) {
+    // SunSED.cpp setupSelfBefore -> SED::setemissivities (SED.cpp) -> setluminosities
+    Table t = readTable(c.datadir, "SunSED.bin");
+    int Ns = (int)t.nrows;
+    std::vector<double> lv(Ns), jv(Ns);
+    for (int k = 0; k < Ns; k++) {
+        lv[k] = t.at(k, 0) / 1e6;
+        jv[k] = t.at(k, 1);
+    }
+    std::vector<double> j = nr::resample<nr::interpolateLogLog>(wl.lambda, lv, jv);
+    std::vector<double> Lv(wl.n());
+    for (int ell = 0; ell < wl.n(); ell++) Lv[ell] = j[ell] * wl.dlambda[ell];
+    double s = nr::sum(Lv);
+    if (s <= 0) throw std::runtime_error("the total luminosity in the SED is zero or negative");
+    for (auto& v : Lv) v /= s;
+    return Lv;
+}
+
+// ------------------------------------------------------------ octree
+// TreeDustGrid::setupSelfBefore / subdivide (TreeDustGrid.cpp:50-233), OctTreeNode (OctTreeNode.cpp),
+// TreeNode neighbor bookkeeping (TreeNode.cpp). Nodes are kept as indices into flat arrays; the
+// neighbor lists are std::vector<int> per (node, wall) mutated in exactly the reference's order so that
+// sortneighbors() (std::sort, not stable) sees identical input sequences.
+enum Wall { BACK = 0, FRONT, LEFT, RIGHT, BOTTOM, TOP };
+
+struct TreeBuilder {
+    OctreeGrid& t;
+    std::vector<std::vector<int>> nb;  // 6 per node, created lazily (ensureneighborlists)
+    std::vector<char> hasLists;
+
+    explicit TreeBuilder(OctreeGrid& tree) : t(tree) {}
+
+    double* box(int l) { return &t.box[6 * (size_t)l]; }
+
+    int addNode(int father, double x0, double y0, double z0, double x1, double y1, double z1) {
+        int id = (int)t.firstChild.size();
+        t.box.insert(t.box.end(), {x0, y0, z0, x1, y1, z1});
+        t.firstChild.push_back(-1);
+        t.father.push_back(father);
+        t.level.push_back(father >= 0 ? t.level[father] + 1 : 0);
+        return id;
+    }
+
+    void createChildren(int l) {
+        // OctTreeNode::createchildren -> createchildren_splitpoint(id, center())
+        double b[6];
+        std::memcpy(b, box(l), sizeof b);
+        double rx = 0.5 * (b[0] + b[3]), ry = 0.5 * (b[1] + b[4]), rz = 0.5 * (b[2] + b[5]);
+        int first = (int)t.firstChild.size();
+        t.firstChild[l] = first;
+        addNode(l, b[0], b[1], b[2], rx, ry, rz);
+        addNode(l, rx, b[1], b[2], b[3], ry, rz);
+        addNode(l, b[0], ry, b[2], rx, b[4], rz);
+        addNode(l, rx, ry, b[2], b[3], b[4], rz);
+        addNode(l, b[0], b[1], rz, rx, ry, b[5]);
+        addNode(l, rx, b[1], rz, b[3], ry, b[5]);
+        addNode(l, b[0], ry, rz, rx, b[4], b[5]);
+        addNode(l, rx, ry, rz, b[3], b[4], b[5]);
+    }
+
+    void ensure(int l) {
+        if ((size_t)l >= hasLists.size()) { hasLists.resize(t.firstChild.size(), 0); nb.resize(6 * t.firstChild.size()); }
+        hasLists[l] = 1;
+    }
+    std::vector<int>& lst(int l, int wall) { return nb[6 * (size_t)l + wall]; }
+    void makeneighbors(int wall1, int n1, int n2) {
+        static const int complementing[] = {FRONT, BACK, RIGHT, LEFT, TOP, BOTTOM};
+        lst(n1, wall1).push_back(n2);
+        lst(n2, complementing[wall1]).push_back(n1);
+    }
+    void deleteneighbor(int l, int wall, int node) {
+        auto& v = lst(l, wall);
+        for (size_t i = 0; i < v.size(); i++)
+            if (v[i] == node) { v.erase(v.begin() + i); break; }
+    }
+
+    // OctTreeNode::addneighbors (OctTreeNode.cpp:51-182)
+    void addneighbors(int l) {
+        if (t.firstChild[l] < 0) return;
+        int c0 = t.firstChild[l];
+        int C[8];
+        for (int k = 0; k < 8; k++) C[k] = c0 + k;
+        ensure(l);
+        for (int k = 0; k < 8; k++) ensure(C[k]);
+        makeneighbors(FRONT, C[0], C[1]);
+        makeneighbors(RIGHT, C[0], C[2]);
+        makeneighbors(TOP, C[0], C[4]);
+        makeneighbors(RIGHT, C[1], C[3]);
+        makeneighbors(TOP, C[1], C[5]);
+        makeneighbors(FRONT, C[2], C[3]);
+        makeneighbors(TOP, C[2], C[6]);
+        makeneighbors(TOP, C[3], C[7]);
+        makeneighbors(FRONT, C[4], C[5]);
+        makeneighbors(RIGHT, C[4], C[6]);
+        makeneighbors(RIGHT, C[5], C[7]);
+        makeneighbors(FRONT, C[6], C[7]);
+        const double* cb = box(C[0]);
+        double xc = cb[3], yc = cb[4], zc = cb[5];
+        auto X0 = [&](int n) { return box(n)[0]; };
+        auto Y0 = [&](int n) { return box(n)[1]; };
+        auto Z0 = [&](int n) { return box(n)[2]; };
+        auto X1 = [&](int n) { return box(n)[3]; };
+        auto Y1 = [&](int n) { return box(n)[4]; };
+        auto Z1 = [&](int n) { return box(n)[5]; };
+        {
+            std::vector<int> ns = lst(l, BACK);
+            for (int n : ns) {
+                deleteneighbor(n, FRONT, l);
+                if (Y0(n) <= yc && Z0(n) <= zc) makeneighbors(FRONT, n, C[0]);
+                if (Y1(n) >= yc && Z0(n) <= zc) makeneighbors(FRONT, n, C[2]);
+                if (Y0(n) <= yc && Z1(n) >= zc) makeneighbors(FRONT, n, C[4]);
+                if (Y1(n) >= yc && Z1(n) >= zc) makeneighbors(FRONT, n, C[6]);
+            }
+        }
+        {
+            std::vector<int> ns = lst(l, FRONT);
+            for (int n : ns) {
+                deleteneighbor(n, BACK, l);
+                if (Y0(n) <= yc && Z0(n) <= zc) makeneighbors(BACK, n, C[1]);
+                if (Y1(n) >= yc && Z0(n) <= zc) makeneighbors(BACK, n, C[3]);
+                if (Y0(n) <= yc && Z1(n) >= zc) makeneighbors(BACK, n, C[5]);
+                if (Y1(n) >= yc && Z1(n) >= zc) makeneighbors(BACK, n, C[7]);
+            }
+        }
+        {
+            std::vector<int> ns = lst(l, LEFT);
+            for (int n : ns) {
+                deleteneighbor(n, RIGHT, l);
+                if (X0(n) <= xc && Z0(n) <= zc) makeneighbors(RIGHT, n, C[0]);
+                if (X1(n) >= xc && Z0(n) <= zc) makeneighbors(RIGHT, n, C[1]);
+                if (X0(n) <= xc && Z1(n) >= zc) makeneighbors(RIGHT, n, C[4]);
+                if (X1(n) >= xc && Z1(n) >= zc) makeneighbors(RIGHT, n, C[5]);
+            }
+        }
+        {
+            std::vector<int> ns = lst(l, RIGHT);
+            for (int n : ns) {
+                deleteneighbor(n, LEFT, l);
+                if (X0(n) <= xc && Z0(n) <= zc) makeneighbors(LEFT, n, C[2]);
+                if (X1(n) >= xc && Z0(n) <= zc) makeneighbors(LEFT, n, C[3]);
+                if (X0(n) <= xc && Z1(n) >= zc) makeneighbors(LEFT, n, C[6]);
+                if (X1(n) >= xc && Z1(n) >= zc) makeneighbors(LEFT, n, C[7]);
+            }
+        }
+        {
+            std::vector<int> ns = lst(l, BOTTOM);
+            for (int n : ns) {
+                deleteneighbor(n, TOP, l);
+                if (X0(n) <= xc && Y0(n) <= yc) makeneighbors(TOP, n, C[0]);
+                if (X1(n) >= xc && Y0(n) <= yc) makeneighbors(TOP, n, C[1]);
+                if (X0(n) <= xc && Y1(n) >= yc) makeneighbors(TOP, n, C[2]);
+                if (X1(n) >= xc && Y1(n) >= yc) makeneighbors(TOP, n, C[3]);
+            }
+        }
+        {
+            std::vector<int> ns = lst(l, TOP);
+            for (int n : ns) {
+                deleteneighbor(n, BOTTOM, l);
+                if (X0(n) <= xc && Y0(n) <= yc) makeneighbors(BOTTOM, n, C[4]);
+                if (X1(n) >= xc && Y0(n) <= yc) makeneighbors(BOTTOM, n, C[5]);
+                if (X0(n) <= xc && Y1(n) >= yc) makeneighbors(BOTTOM, n, C[6]);
+                if (X1(n) >= xc && Y1(n) >= yc) makeneighbors(BOTTOM, n, C[7]);
+            }
+        }
+    }
+
+    // TreeNode::sortneighbors with the LargerOverlap functor (TreeNode.cpp:98-140)
+    void sortneighbors(int l) {
+        if (!hasLists[l]) return;
+        const double* b = box(l);
+        for (int wall = 0; wall < 6; wall++) {
+            auto overlap = [&](int n) {
+                const double* o = box(n);
+                double a1, a2, b1, b2, c1, c2, d1, d2;  // rect (a1,b1)-(a2,b2) vs (c1,d1)-(c2,d2)
+                switch (wall) {
+                case BACK: case FRONT:
+                    a1 = b[1]; b1 = b[2]; a2 = b[4]; b2 = b[5]; c1 = o[1]; d1 = o[2]; c2 = o[4]; d2 = o[5]; break;
+                case LEFT: case RIGHT:
+                    a1 = b[0]; b1 = b[2]; a2 = b[3]; b2 = b[5]; c1 = o[0]; d1 = o[2]; c2 = o[3]; d2 = o[5]; break;
+                default:
+                    a1 = b[0]; b1 = b[1]; a2 = b[3]; b2 = b[4]; c1 = o[0]; d1 = o[1]; c2 = o[3]; d2 = o[4]; break;
+                }
+                return std::max(std::min(a2, c2) - std::max(a1, c1), 0.) *
+                       std::max(std::min(b2, d2) - std::max(b1, d1), 0.);
+            };
+            auto& v = lst(l, wall);
+            std::sort(v.begin(), v.end(), [&](int n1, int n2) { return overlap(n1) > overlap(n2); });
+        }
+    }
+};
+
+void buildOctree(const Ctx& c, const XmlElement* e, const Model& model, OctreeGrid& t) {
+    t.xmin = attr(c, e, "minX", "length", 0);
+    t.xmax = attr(c, e, "maxX", "length", 0);
+    t.ymin = attr(c, e, "minY", "length", 0);
+    t.ymax = attr(c, e, "maxY", "length", 0);
+    t.zmin = attr(c, e, "minZ", "length", 0);
+    t.zmax = attr(c, e, "maxZ", "length", 0);
+    if (t.xmax <= t.xmin || t.ymax <= t.ymin || t.zmax <= t.zmin) throw std::runtime_error("invalid grid extent");
+    t.minLevel = attrInt(e, "minLevel", 2);
+    t.maxLevel = attrInt(e, "maxLevel", 6);
+    std::string search = e->get("searchMethod", "Neighbor");
+    t.search = search == "TopDown" ? 0 : search == "Bookkeeping" ? 2 : 1;
+    int Nrandom = attrInt(e, "sampleCount", 100);
+    double maxOpticalDepth = attr(c, e, "maxOpticalDepth", "", 0);
+    double maxMassFraction = attr(c, e, "maxMassFraction", "", 1e-6);
+    double maxDensDispFraction = attr(c, e, "maxDensDispFraction", "", 0);
+    if (attrBool(e, "barycentric", false)) throw std::runtime_error("barycentric octree subdivision is not supported");
+    if (t.minLevel < 0 || t.maxLevel < 2 || t.maxLevel <= t.minLevel) throw std::runtime_error("invalid tree levels");
+
+    double wx = t.xmax - t.xmin, wy = t.ymax - t.ymin, wz = t.zmax - t.zmin;
+    t.eps = 1e-12 * std::sqrt(wx * wx + wy * wy + wz * wz);
+    double totalmass = 0;
+    for (auto& d : model.dust) totalmass += d.nf;  // CompDustDistribution::mass
+
+    TreeBuilder tb(t);
+    tb.addNode(-1, t.xmin, t.ymin, t.zmin, t.xmax, t.ymax, t.zmax);
+    std::vector<double> rhov(Nrandom);
+    for (size_t l = 0; l < t.firstChild.size(); l++) {
+        if (t.firstChild[l] >= 0) continue;
+        int level = t.level[l];
+        if (level <= t.minLevel) {
+            tb.createChildren((int)l);
+        } else if (level < t.maxLevel) {
+            // TreeNodeSampleDensityCalculator: Nrandom positions in the node, density of all components
+            double b[6];
+            std::memcpy(b, tb.box((int)l), sizeof b);
+            for (int n = 0; n < Nrandom; n++) {
+                double fx = c.rng->uniform(), fy = c.rng->uniform(), fz = c.rng->uniform();
+                double x = b[0] + fx * (b[3] - b[0]), y = b[1] + fy * (b[4] - b[1]), z = b[2] + fz * (b[5] - b[2]);
+                double rho = 0;
+                for (auto& d : model.dust) rho += d.density(x, y, z);
+                rhov[n] = rho;
+            }
+            double vol = (b[3] - b[0]) * (b[4] - b[1]) * (b[5] - b[2]);
+            double mass = nr::sum(rhov) / Nrandom * vol;
+            bool needDivision = (maxOpticalDepth == 0 && maxMassFraction == 0 && maxDensDispFraction == 0);
+            if (!needDivision && maxMassFraction > 0 && mass / totalmass >= maxMassFraction) needDivision = true;
+            if (!needDivision && maxOpticalDepth > 0 &&
+                constants::kappaV * mass / std::pow(vol, 2. / 3.) >= maxOpticalDepth)
+                needDivision = true;
+            if (!needDivision && maxDensDispFraction > 0) {
+                double mn = *std::min_element(rhov.begin(), rhov.end());
+                double mx = *std::max_element(rhov.begin(), rhov.end());
+                double disp = mx > 0 ? (mx - mn) / mx : 0;
+                if (disp >= maxDensDispFraction) needDivision = true;
+            }
+            if (needDivision) tb.createChildren((int)l);
+        }
+    }
+    int Nnodes = t.nnodes();
+    t.cellnumber.assign(Nnodes, -1);
+    t.idv.clear();
+    for (int l = 0; l < Nnodes; l++)
+        if (t.firstChild[l] < 0) {
+            t.cellnumber[l] = (int)t.idv.size();
+            t.idv.push_back(l);
+        }
+    // neighbor lists (always built: the device engine uses them whatever the search method)
+    tb.hasLists.assign(Nnodes, 0);
+    tb.nb.assign(6 * (size_t)Nnodes, {});
+    for (int l = 0; l < Nnodes; l++) tb.addneighbors(l);
+    for (int l = 0; l < Nnodes; l++) tb.sortneighbors(l);
+    t.nbrOffset.assign(6 * (size_t)Nnodes + 1, 0);
+    size_t total = 0;
+    for (size_t q = 0; q < 6 * (size_t)Nnodes; q++) total += tb.nb[q].size();
+    t.nbrList.reserve(total);
+    for (size_t q = 0; q < 6 * (size_t)Nnodes; q++) {
+        t.nbrOffset[q] = (int)t.nbrList.size();
+        t.nbrList.insert(t.nbrList.end(), tb.nb[q].begin(), tb.nb[q].end());
+    }
+    t.nbrOffset[6 * (size_t)Nnodes] = (int)t.nbrList.size();
+}
+
+// ------------------------------------------------------------ instruments
+Instrument parseInstrument(const Ctx& c, const XmlElement* e) {
+    Instrument ins;
+    ins.name = e->get("instrumentName", "");
+    if (e->name == "FullInstrument") ins.kind = InstrumentKind::Full;
+    else if (e->name == "SimpleInstrument") ins.kind = InstrumentKind::Simple;
+    else if (e->name == "SEDInstrument") ins.kind = InstrumentKind::SED;
+    else if (e->name == "FrameInstrument") ins.kind = InstrumentKind::Frame;
+    else throw std::runtime_error("unsupported instrument " + e->name);
+    ins.distance = attr(c, e, "distance", "distance", 0);
+    ins.inclination = attr(c, e, "inclination", "posangle", 0);
+    ins.azimuth = attr(c, e, "azimuth", "posangle", 0);
+    ins.positionAngle = attr(c, e, "positionAngle", "posangle", 0);
+    if (ins.distance <= 0) throw std::runtime_error("instrument distance was not set");
+    // DistantInstrument::setupSelfBefore (DistantInstrument.cpp:27-50)
+    ins.costheta = std::cos(ins.inclination);
+    ins.sintheta = std::sin(ins.inclination);
+    ins.cosphi = std::cos(ins.azimuth);
+    ins.sinphi = std::sin(ins.azimuth);
+    ins.cospa = std::cos(ins.positionAngle);
+    ins.sinpa = std::sin(ins.positionAngle);
+    {
+        // Direction(theta, phi) (Direction.cpp)
+        double theta = ins.inclination, phi = ins.azimuth, eps = 1e-8;
+        if (theta < -eps || theta > M_PI + eps) throw std::runtime_error("theta should be between 0 and pi");
+        if (theta <= eps) { ins.kobs[0] = 0; ins.kobs[1] = 0; ins.kobs[2] = 1; }
+        else if (theta >= M_PI - eps) { ins.kobs[0] = 0; ins.kobs[1] = 0; ins.kobs[2] = -1; }
+        else {
+            double st = std::sin(theta);
+            ins.kobs[0] = st * std::cos(phi);
+            ins.kobs[1] = st * std::sin(phi);
+            ins.kobs[2] = std::cos(theta);
+        }
+    }
+    ins.kx[0] = +ins.cosphi * ins.costheta * ins.sinpa - ins.sinphi * ins.cospa;
+    ins.kx[1] = +ins.sinphi * ins.costheta * ins.sinpa + ins.cosphi * ins.cospa;
+    ins.kx[2] = -ins.sintheta * ins.sinpa;
+    ins.ky[0] = -ins.cosphi * ins.costheta * ins.cospa - ins.sinphi * ins.sinpa;
+    ins.ky[1] = -ins.sinphi * ins.costheta * ins.cospa + ins.cosphi * ins.sinpa;
+    ins.ky[2] = +ins.sintheta * ins.cospa;
+    if (ins.kind != InstrumentKind::SED) {
+        ins.fovx = attr(c, e, "fieldOfViewX", "length", 0);
+        ins.fovy = attr(c, e, "fieldOfViewY", "length", 0);
+        ins.Nx = attrInt(e, "pixelsX", 250);
+        ins.Ny = attrInt(e, "pixelsY", 250);
+        ins.xc = attr(c, e, "centerX", "length", 0);
+        ins.yc = attr(c, e, "centerY", "length", 0);
+        if (ins.Nx <= 0 || ins.Ny <= 0) throw std::runtime_error("number of pixels was not set");
+        if (ins.fovx <= 0 || ins.fovy <= 0) throw std::runtime_error("field of view was not set");
+        // SingleFrameInstrument::setupSelfBefore (SingleFrameInstrument.cpp:24-38)
+        ins.xpmin = ins.xc - 0.5 * ins.fovx;
+        ins.xpmax = ins.xc + 0.5 * ins.fovx;
+        ins.xpsiz = ins.fovx / ins.Nx;
+        ins.ypmin = ins.yc - 0.5 * ins.fovy;
+        ins.ypmax = ins.yc + 0.5 * ins.fovy;
+        ins.ypsiz = ins.fovy / ins.Ny;
+    }
+    if (ins.kind == InstrumentKind::Full) ins.scatteringLevels = attrInt(e, "scatteringLevels", 0);
+    return ins;
+}
+
+}  // namespace
+
+// ============================================================ loadSki
+
+Model loadSki(const std::string& path, UniformSource& rng, const std::string& datadir) {
+    auto doc = parseXmlFile(path);
+    if (doc->children.empty()) throw std::runtime_error("empty ski file");
+    const XmlElement* sim = doc->children.front().get();
+    Model m;
+    if (sim->name == "OligoMonteCarloSimulation") m.pan = false;
+    else if (sim->name == "PanMonteCarloSimulation") m.pan = true;
+    else throw std::runtime_error("unsupported simulation type " + sim->name);
+
+    const XmlElement* unitsEl = sim->item("units");
+    m.units_system = unitsEl ? unitsEl->name : "ExtragalacticUnits";
+    Ctx c{Units(m.units_system), datadir, &rng};
+
+    if (const XmlElement* r = sim->item("random")) m.seed = (unsigned long)attrInt(r, "seed", 4357);
+    m.packages = attr(c, sim, "packages", "", 1e6);
+    m.minWeightReduction = attr(c, sim, "minWeightReduction", "", 1e4);
+    m.minScattEvents = (int)attr(c, sim, "minScattEvents", "", 0);
+    m.scattBias = attr(c, sim, "scattBias", "", 0.5);
+    m.continuousScattering = attrBool(sim, "continuousScattering", false);
+    if (m.packages < 0 || m.packages > 1e15) throw std::runtime_error("invalid number of photon packages");
+    if (m.minWeightReduction < 1e3) throw std::runtime_error("the minimum weight reduction factor should be larger than 1000");
+    if (m.scattBias < 0 || m.scattBias > 1) throw std::runtime_error("the scattering bias should be between 0 and 1");
+    if (m.continuousScattering) throw std::runtime_error("continuousScattering is not supported by this engine");
+
+    m.wl = parseWavelengthGrid(c, need(sim, "wavelengthGrid"));
+    int Nlambda = m.wl.n();
+
+    // ---- stellar system
+    const XmlElement* ss = need(sim, "stellarSystem");
+    m.starEmissionBias = attr(c, ss, "emissionBias", "", 0.5);
+    for (const XmlElement* sc : ss->items("components")) {
+        m.starGeom.push_back(parseGeometry(c, need(sc, "geometry")));
+        if (sc->name == "OligoStellarComp") {
+            if (m.pan) throw std::runtime_error("OligoStellarComp requires an oligochromatic simulation");
+            std::vector<double> lum = attrList(c, sc, "luminosities", "");
+            if ((int)lum.size() != Nlambda) throw std::runtime_error("number of luminosities differs from number of wavelengths");
+            m.starL.push_back(sunLuminosityOligo(c, m.wl, lum));
+        } else if (sc->name == "PanStellarComp") {
+            const XmlElement* sed = need(sc, "sed");
+            const XmlElement* norm = need(sc, "normalization");
+            if (sed->name != "SunSED") throw std::runtime_error("unsupported stellar SED " + sed->name);
+            if (norm->name != "BolLuminosityStellarCompNormalization")
+                throw std::runtime_error("unsupported stellar normalization " + norm->name);
+            double Lsunits = attr(c, norm, "luminosity", "", 0);
+            if (Lsunits <= 0) throw std::runtime_error("the bolometric luminosity should be positive");
+            double Ltot = Lsunits * constants::Lsun;
+            std::vector<double> sedL = sunSedNormalized(c, m.wl);
+            std::vector<double> Lv(Nlambda);
+            for (int ell = 0; ell < Nlambda; ell++) Lv[ell] = Ltot * sedL[ell];
+            m.starL.push_back(Lv);
+        } else {
+            throw std::runtime_error("unsupported stellar component " + sc->name);
+        }
+    }
+    if (m.starL.empty()) throw std::runtime_error("there are no stellar components");
+    {
+        int Ncomp = (int)m.starL.size();
+        m.starLtot.assign(Nlambda, 0.0);
+        m.starX.assign(Nlambda, {});
+        for (int ell = 0; ell < Nlambda; ell++) {
+            for (int h = 0; h < Ncomp; h++) m.starLtot[ell] += m.starL[h][ell];
+            std::vector<double> pv(Ncomp);
+            for (int h = 0; h < Ncomp; h++) pv[h] = m.starL[h][ell];
+            nr::cdf(m.starX[ell], pv);
+        }
+    }
+
+    // ---- dust system
+    const XmlElement* ds = sim->item("dustSystem");
+    if (ds) {
+        m.hasDust = true;
+        bool pds = ds->name == "PanDustSystem";
+        if (pds != m.pan) throw std::runtime_error("dust system type does not match the simulation type");
+        m.sampleCount = attrInt(ds, "sampleCount", 100);
+        m.writeConvergence = attrBool(ds, "writeConvergence", true);
+        m.writeCellProperties = attrBool(ds, "writeCellProperties", false);
+        if (pds) {
+            m.dustEmission = ds->item("dustEmissivity") != nullptr;
+            m.selfAbsorption = m.dustEmission && attrBool(ds, "selfAbsorption", false);
+            m.dustEmissionBias = attr(c, ds, "emissionBias", "", 0.5);
+            m.emissionBoost = attr(c, ds, "emissionBoost", "", 1);
+            m.cycles = attrInt(ds, "cycles", 0);
+            m.writeISRF = attrBool(ds, "writeISRF", false);
+            m.storeAbsorption = m.dustEmission;
+        } else {
+            m.writeMeanIntensity = attrBool(ds, "writeMeanIntensity", false);
+            m.storeAbsorption = m.writeMeanIntensity;
+        }
+        const XmlElement* dd = need(ds, "dustDistribution");
+        if (dd->name != "CompDustDistribution") throw std::runtime_error("unsupported dust distribution " + dd->name);
+        for (const XmlElement* dc : dd->items("components")) {
+            DustComp comp;
+            comp.geom = parseGeometry(c, need(dc, "geometry"));
+            comp.mix = parseMix(c, need(dc, "mix"), m.wl);
+            const XmlElement* nrm = need(dc, "normalization");
+            if (nrm->name != "DustMassDustCompNormalization")
+                throw std::runtime_error("unsupported dust normalization " + nrm->name);
+            comp.nf = attr(c, nrm, "dustMass", "mass", 0);
+            m.dust.push_back(comp);
+        }
+        if (m.dust.empty()) throw std::runtime_error("dust distribution has no components");
+
+        const XmlElement* ge = need(ds, "dustGrid");
+        if (ge->name == "CartesianDustGrid") {
+            m.grid.kind = GridKind::Cartesian;
+            CartesianGrid& g = m.grid.cart;
+            g.xmin = attr(c, ge, "minX", "length", 0);
+            g.xmax = attr(c, ge, "maxX", "length", 0);
+            g.ymin = attr(c, ge, "minY", "length", 0);
+            g.ymax = attr(c, ge, "maxY", "length", 0);
+            g.zmin = attr(c, ge, "minZ", "length", 0);
+            g.zmax = attr(c, ge, "maxZ", "length", 0);
+            if (g.xmax <= g.xmin || g.ymax <= g.ymin || g.zmax <= g.zmin) throw std::runtime_error("invalid grid extent");
+            auto mesh = [&](const char* prop, int& N, std::vector<double>& v, double lo, double hi) {
+                const XmlElement* me = need(ge, prop);
+                if (me->name != "LinMesh") throw std::runtime_error("unsupported mesh " + me->name);
+                N = attrInt(me, "numBins", 100);
+                // LinMesh::mesh() = NR::lingrid(tv, 0, 1, N); _xv = mesh*(xmax-xmin) + xmin
+                double dx = (1.0 - 0.0) / N;
+                v.resize(N + 1);
+                for (int i = 0; i <= N; i++) v[i] = (0.0 + i * dx) * (hi - lo) + lo;
+            };
+            mesh("meshX", g.Nx, g.xv, g.xmin, g.xmax);
+            mesh("meshY", g.Ny, g.yv, g.ymin, g.ymax);
+            mesh("meshZ", g.Nz, g.zv, g.zmin, g.zmax);
+            m.grid.ncells = g.Nx * g.Ny * g.Nz;
+        } else if (ge->name == "OctTreeDustGrid") {
+            m.grid.kind = GridKind::Octree;
+            buildOctree(c, ge, m, m.grid.tree);
+            m.grid.ncells = (int)m.grid.tree.idv.size();
+        } else {
+            throw std::runtime_error("unsupported dust grid " + ge->name);
+        }
+
+        // DustSystem::setupSelfAfter: volumes, then densities sampled at sampleCount random positions
+        int Ncells = m.grid.ncells, Ncomp = m.ncomp();
+        m.volume.resize(Ncells);
+        for (int cell = 0; cell < Ncells; cell++) m.volume[cell] = m.grid.cellVolume(cell);
+        m.rho.assign((size_t)Ncells * Ncomp, 0.0);
+        std::vector<double> sumv(Ncomp);
+        for (int cell = 0; cell < Ncells; cell++) {
+            double b[6];
+            m.grid.cellBox(cell, b);
+            std::fill(sumv.begin(), sumv.end(), 0.0);
+            for (int n = 0; n < m.sampleCount; n++) {
+                double fx = rng.uniform(), fy = rng.uniform(), fz = rng.uniform();
+                double x = b[0] + fx * (b[3] - b[0]), y = b[1] + fy * (b[4] - b[1]), z = b[2] + fz * (b[5] - b[2]);
+                for (int h = 0; h < Ncomp; h++) sumv[h] += m.dust[h].density(x, y, z);
+            }
+            for (int h = 0; h < Ncomp; h++) m.rho[(size_t)cell * Ncomp + h] = 1.0 * sumv[h] / m.sampleCount;
+        }
+    }
+
+    // ---- instruments
+    if (const XmlElement* is = sim->item("instrumentSystem"))
+        for (const XmlElement* ie : is->items("instruments")) m.instruments.push_back(parseInstrument(c, ie));
+    return m;
+}
+
+std::string defaultDataDir() {
+    Dl_info info;
+    if (dladdr((void*)&defaultDataDir, &info) && info.dli_fname) {
+        std::string p(info.dli_fname);
+        size_t s = p.rfind('/');
+        std::string dir = (s == std::string::npos) ? "." : p.substr(0, s);
+        // the library lives in skirt_amd/ (or skirt_amd/lib); data is skirt_amd/data
+        for (const char* cand : {"/data", "/../data"}) {
+            std::string d = dir + cand;
+            std::ifstream f(d + "/SunSED.bin");
+            if (f) return d;
+        }
+    }
+    return "skirt_amd/data";
+}
+
+}  // namespace skirt

@@ -1,0 +1,174 @@
+// The simulation model built from a .ski file: everything the photon-shooting hot path reads.
+//
+// The reference spreads this state over its SimulationItem tree (MonteCarloSimulation, StellarSystem,
+// DustSystem, DustGrid, DustMix, Instrument subclasses). Here it is one plain struct of flat arrays,
+// built once on the host (build.cpp) and then handed to the device engine through the C ABI
+// (include/skirt_mcrt.h) or to the CPU checker in oracle/.
+#pragma once
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "mt_random.hpp"
+#include "units.hpp"
+
+namespace skirt {
+
+// ---------------------------------------------------------------- geometries
+// Reference: SKIRTcore/PlummerGeometry.cpp (density 49-54, randomradius 57-63), SpheGeometry.cpp
+// (generatePosition = randomradius then isotropic direction).
+enum class GeometryKind : int { Plummer = 0 };
+
+struct Geometry {
+    GeometryKind kind = GeometryKind::Plummer;
+    double c = 0;     // Plummer scale length
+    double rho0 = 0;  // 0.75/c^3/pi (PlummerGeometry.cpp setupSelfBefore)
+
+    double density(double x, double y, double z) const;
+};
+
+// ---------------------------------------------------------------- wavelength grid
+struct WavelengthGrid {
+    bool pan = false;  // issampledrange()
+    std::vector<double> lambda, dlambda;
+    int n() const { return (int)lambda.size(); }
+    double lambdamin(int ell) const;  // WavelengthGrid.cpp lambdamin/lambdamax
+    double lambdamax(int ell) const;
+};
+
+// ---------------------------------------------------------------- dust
+// Reference: SKIRTcore/DustMix.cpp:44-264 (per-wavelength tables), DustMix.cpp:440-443 quirks kept.
+struct DustMix {
+    std::string type;
+    std::vector<double> kabs, ksca, kext, albedo, g;  // per ell
+    // per-population cross sections (needed for dust emission equilibrium temperatures)
+    double mu = 0;
+    std::vector<double> sigmaabs;  // per ell, summed over populations
+};
+
+struct DustComp {
+    Geometry geom;
+    DustMix mix;
+    double nf = 0;  // normalization factor = dust mass (DustMassDustCompNormalization)
+    double density(double x, double y, double z) const { return nf * geom.density(x, y, z); }
+};
+
+// Cartesian grid: SKIRTcore/CartesianDustGrid.cpp
+struct CartesianGrid {
+    int Nx = 0, Ny = 0, Nz = 0;
+    double xmin = 0, xmax = 0, ymin = 0, ymax = 0, zmin = 0, zmax = 0;
+    std::vector<double> xv, yv, zv;  // N+1 borders each
+};
+
+// Octree grid: SKIRTcore/TreeDustGrid.cpp + OctTreeNode.cpp, flattened breadth-first exactly as the
+// reference's _tree vector: node l has children firstChild[l] .. firstChild[l]+7 (or -1 for a leaf).
+struct OctreeGrid {
+    double xmin = 0, xmax = 0, ymin = 0, ymax = 0, zmin = 0, zmax = 0;
+    double eps = 0;  // 1e-12 * |extent widths| (TreeDustGrid.cpp:76)
+    int minLevel = 2, maxLevel = 6;
+    int search = 1;  // 0 TopDown, 1 Neighbor, 2 Bookkeeping
+    std::vector<double> box;      // 6 per node: xmin ymin zmin xmax ymax zmax
+    std::vector<int> firstChild;  // per node, -1 for a leaf
+    std::vector<int> father;      // per node, -1 for the root
+    std::vector<int> level;       // per node
+    std::vector<int> cellnumber;  // per node, -1 for non-leaves
+    std::vector<int> idv;         // per cell: node index
+    // neighbor lists per (node, wall), walls ordered BACK FRONT LEFT RIGHT BOTTOM TOP (TreeNode.hpp)
+    std::vector<int> nbrOffset;   // 6*Nnodes+1
+    std::vector<int> nbrList;
+    int nnodes() const { return (int)firstChild.size(); }
+};
+
+enum class GridKind : int { Cartesian = 0, Octree = 1 };
+
+struct DustGrid {
+    GridKind kind = GridKind::Cartesian;
+    CartesianGrid cart;
+    OctreeGrid tree;
+    int ncells = 0;
+    void cellBox(int m, double b[6]) const;  // xmin ymin zmin xmax ymax zmax
+    double cellVolume(int m) const;
+    int whichcell(double x, double y, double z) const;
+};
+
+// ---------------------------------------------------------------- instruments
+// Reference: DistantInstrument.cpp:27-50 (angles, kobs, kx, ky), SingleFrameInstrument.cpp:24-38
+// (frame geometry) and :130-147 (pixelondetector), FullInstrument.cpp:107-174 (detect).
+enum class InstrumentKind : int { Full = 0, Simple = 1, SED = 2, Frame = 3 };
+
+// slots of the FullInstrument accumulation arrays (FullInstrument.cpp:58-86)
+enum FullSlot : int { SlotTrav = 0, SlotStrDir = 1, SlotStrSca = 2, SlotDusDir = 3, SlotDusSca = 4, SlotLevel0 = 5 };
+
+struct Instrument {
+    std::string name;
+    InstrumentKind kind = InstrumentKind::Full;
+    double distance = 0, inclination = 0, azimuth = 0, positionAngle = 0;
+    int Nx = 250, Ny = 250;
+    double fovx = 0, fovy = 0, xc = 0, yc = 0;
+    int scatteringLevels = 0;
+    // derived
+    double costheta = 1, sintheta = 0, cosphi = 1, sinphi = 0, cospa = 1, sinpa = 0;
+    double kobs[3] = {0, 0, 1}, kx[3] = {0, 0, 0}, ky[3] = {0, 0, 0};
+    double xpmin = 0, xpmax = 0, xpsiz = 0, ypmin = 0, ypmax = 0, ypsiz = 0;
+    int nframe() const { return Nx * Ny; }
+    bool hasFrames() const { return kind != InstrumentKind::SED; }
+    bool hasSeds() const { return kind != InstrumentKind::Frame; }
+    // number of accumulation slots (frames and SEDs share the slot index)
+    int nslots() const { return kind == InstrumentKind::Full ? SlotLevel0 + scatteringLevels : 1; }
+    int pixel(double x, double y, double z) const;
+};
+
+// ---------------------------------------------------------------- simulation
+struct Model {
+    bool pan = false;
+    std::string units_system = "ExtragalacticUnits";
+    unsigned long seed = 4357;
+
+    // MonteCarloSimulation properties (MonteCarloSimulation.cpp:31-35 defaults)
+    double packages = 1e6;
+    double minWeightReduction = 1e4;
+    int minScattEvents = 0;
+    double scattBias = 0.5;
+    bool continuousScattering = false;
+
+    WavelengthGrid wl;
+
+    // stellar system (StellarSystem.cpp)
+    std::vector<Geometry> starGeom;              // per component
+    std::vector<std::vector<double>> starL;      // [comp][ell] luminosity (W)
+    double starEmissionBias = 0.5;
+    std::vector<double> starLtot;                // per ell, sum over comps
+    std::vector<std::vector<double>> starX;      // per ell: normalized cumulative luminosity over comps
+
+    // dust system
+    bool hasDust = false;
+    std::vector<DustComp> dust;
+    DustGrid grid;
+    std::vector<double> rho;     // Ncells x Ncomp row-major (DustSystem::_rhovv)
+    std::vector<double> volume;  // per cell
+    bool storeAbsorption = false;   // DustSystem::storeabsorptionrates()
+    bool dustEmission = false;      // PanDustSystem::dustemission()
+    bool selfAbsorption = false;
+    double dustEmissionBias = 0.5;  // PanDustSystem emissionBias
+    double emissionBoost = 1;
+    int cycles = 0;
+    bool writeISRF = false, writeCellProperties = false, writeMeanIntensity = false, writeConvergence = false;
+    int sampleCount = 100;
+
+    std::vector<Instrument> instruments;
+
+    int ncomp() const { return (int)dust.size(); }
+    int ncells() const { return grid.ncells; }
+    // kappa_ext * rho summed over components (the KappaRho functor, DustSystem.cpp:465-491)
+    double kapparho(int m, int ell) const;
+};
+
+// Builds the model from a .ski file; `rng` supplies the setup random numbers (octree subdivision
+// sampling, cell density sampling) in the reference's order. `datadir` holds SunSED.bin etc.
+Model loadSki(const std::string& path, UniformSource& rng, const std::string& datadir);
+
+// directory holding the packaged resource tables (skirt_amd/data), located relative to this library
+std::string defaultDataDir();
+
+}  // namespace skirt

@@ -1,0 +1,92 @@
+"""ctypes binding of the CPU oracle (oracle/liboracle.so) -- test infrastructure only.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg load this module.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(REPO, "oracle", "liboracle.so")
+DATA_DIR = os.path.join(REPO, "skirt_amd", "data")
+
+RNG_MT = 0
+RNG_PHILOX = 1
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError("oracle not built: run `make -C oracle` (or __graft_entry__.build())")
+        L = ctypes.CDLL(LIB_PATH)
+        L.oracle_run.restype = ctypes.c_void_p
+        L.oracle_run.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_double,
+                                 ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int, ctypes.c_char_p]
+        L.oracle_last_error.restype = ctypes.c_char_p
+        L.oracle_labs.restype = ctypes.POINTER(ctypes.c_double)
+        L.oracle_labs.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]
+        L.oracle_num_instruments.argtypes = [ctypes.c_void_p]
+        L.oracle_instrument.argtypes = [ctypes.c_void_p, ctypes.c_int,
+                                        ctypes.POINTER(ctypes.POINTER(ctypes.c_double)),
+                                        ctypes.POINTER(ctypes.POINTER(ctypes.c_double)),
+                                        ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int),
+                                        ctypes.POINTER(ctypes.c_int)]
+        L.oracle_seconds.restype = ctypes.c_double
+        L.oracle_seconds.argtypes = [ctypes.c_void_p]
+        L.oracle_packets.restype = ctypes.c_uint64
+        L.oracle_packets.argtypes = [ctypes.c_void_p]
+        L.oracle_segments.restype = ctypes.c_uint64
+        L.oracle_segments.argtypes = [ctypes.c_void_p]
+        L.oracle_free.argtypes = [ctypes.c_void_p]
+        L.oracle_philox4x32_10.argtypes = [ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32),
+                                           ctypes.POINTER(ctypes.c_uint32)]
+        _lib = L
+    return _lib
+
+
+class OracleResult:
+    """Raw (uncalibrated) accumulators of one oracle run, copied into numpy arrays."""
+
+    def __init__(self, handle):
+        L = lib()
+        nc, nl = ctypes.c_int(), ctypes.c_int()
+        p = L.oracle_labs(handle, ctypes.byref(nc), ctypes.byref(nl))
+        self.ncells, self.nlambda = nc.value, nl.value
+        self.labs = (np.ctypeslib.as_array(p, shape=(self.ncells, self.nlambda)).copy() if p else None)
+        self.frames, self.seds = [], []
+        for i in range(L.oracle_num_instruments(handle)):
+            fp, sp = ctypes.POINTER(ctypes.c_double)(), ctypes.POINTER(ctypes.c_double)()
+            ns, nf, nlam = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+            L.oracle_instrument(handle, i, ctypes.byref(fp), ctypes.byref(sp), ctypes.byref(ns), ctypes.byref(nf),
+                                ctypes.byref(nlam))
+            self.frames.append(np.ctypeslib.as_array(fp, shape=(ns.value, nlam.value, nf.value)).copy()
+                               if fp else None)
+            self.seds.append(np.ctypeslib.as_array(sp, shape=(ns.value, nlam.value)).copy() if sp else None)
+        self.seconds = L.oracle_seconds(handle)
+        self.packets = L.oracle_packets(handle)
+        self.segments = L.oracle_segments(handle)
+
+
+def run(ski, rng=RNG_MT, threads=1, packages=0.0, seed=0, packet_begin=0, packet_end=0, outprefix=None):
+    L = lib()
+    h = L.oracle_run(ski.encode(), DATA_DIR.encode(), rng, threads, float(packages), seed, packet_begin,
+                     packet_end, 0, outprefix.encode() if outprefix else None)
+    if not h:
+        raise RuntimeError("oracle failed: " + L.oracle_last_error().decode())
+    try:
+        return OracleResult(h)
+    finally:
+        L.oracle_free(h)
+
+
+def philox(ctr, key):
+    L = lib()
+    c = (ctypes.c_uint32 * 4)(*ctr)
+    k = (ctypes.c_uint32 * 2)(*key)
+    o = (ctypes.c_uint32 * 4)()
+    L.oracle_philox4x32_10(c, k, o)
+    return list(o)
