@@ -1,0 +1,182 @@
+#!/usr/bin/env python3
+"""Photon packets per second of SKIRT's stellar emission phase on MI355X (BASELINE.json metric).
+
+One "step" is one stellar-emission phase (MonteCarloSimulation::runstellaremission,
+SKIRTcore/MonteCarloSimulation.cpp:251-261) over a fixed number of primary photon packets per GPU on the
+C3 workload: Pan simulation, 128^3-resolution octree (levels 3-7, Saftly mass-fraction refinement), 25
+wavelengths, peel-off to a 250x250 FullInstrument, Plummer stars + dust (benchmarks/c3_oct128.ski).
+Weak scaling: every rank shoots its own slice of the global packet index space and, for N > 1, the
+phase ends with the reference's reductions (Labs all-reduce, instrument all-reduce) done by RCCL.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2]
+       (N > 1: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...)
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+CONFIGS = {
+    # name: (ski, packets per wavelength per rank, segment geometry bytes, description)
+    "c3": ("benchmarks/c3_oct128.ski", 400000, 56, "C3 octree 128^3 (levels 3-7, mass fraction 1e-6), 25 lambda, peel-off"),
+    "c2": ("benchmarks/c2_cart64.ski", 1000000, 0, "C2 Cartesian 64^3, 10 lambda, peel-off"),
+}
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip-level parameters (spec)
+
+
+def algorithmic_bytes(stats, geom_bytes, ncomp):
+    """per segment the cell geometry (octree: 48 B box + 8 B index/neighbour;
+    Cartesian: 0, the mesh lives in LDS) plus 8*Ncomp B of density; 16 B read-modify-write per absorbed
+    segment (Labs) and per frame pixel update of a detection."""
+    segs = stats["segments_fill"] + stats["segments_walk"] + stats["segments_peel"]
+    return segs * (geom_bytes + 8 * ncomp) + stats["absorb_adds"] * 16 + stats["detects"] * 16
+
+
+def cpu_baseline(ski, target_seconds=15.0):
+    """The CPU oracle (a C++ restatement of the reference's photon loop, std::thread over packets with
+    lock-free tallies like the reference's Parallel + LockFree::add) on this host's cores, on a bounded
+    sample of the same workload: fewer packets per wavelength, all wavelengths. A short probe sizes the
+    sample to about `target_seconds`. Returns (packets/s, threads, sample description)."""
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import oracle_lib
+
+    threads = max(1, min(16, os.cpu_count() or 1))  # the GPU box grants 16 CPUs per GPU
+    probe = oracle_lib.run(ski, rng=oracle_lib.RNG_PHILOX, threads=threads, packages=200)
+    rate = probe.packets / max(probe.seconds, 1e-6)
+    nl = probe.nlambda
+    per = int(max(200, min(1e6, rate * target_seconds / nl)))
+    r = oracle_lib.run(ski, rng=oracle_lib.RNG_PHILOX, threads=threads, packages=per)
+    return r.packets / r.seconds, threads, "%d packets/wavelength x %d wavelengths = %d packets in %.1f s" % (
+        per, nl, r.packets, r.seconds)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
+    ap.add_argument("--packets-per-lambda", type=int, default=0, help="per rank; default per config")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--threshold", type=int, default=0, help="event batching threshold (0 = engine default)")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+
+    import skirt_amd
+
+    ski_rel, ppl_default, geom_bytes, desc = CONFIGS[args.config]
+    ski = os.path.join(REPO, ski_rel)
+    ppl = args.packets_per_lambda or ppl_default
+    sim = skirt_amd.Simulation(ski, packages=float(ppl * world))
+    info = sim.info
+    share = ppl * info.nlambda  # packets per rank per step
+    first = rank * share
+    sim.attach(local)
+    if args.threshold:
+        sim.configure(threshold=args.threshold)
+    stream = torch.cuda.current_stream()
+    sim.set_stream(stream.cuda_stream)
+    n_labs, n_instr = sim.tally_sizes()
+    labs = torch.zeros(max(1, n_labs), dtype=torch.float64, device="cuda")
+    instr = torch.zeros(max(1, n_instr), dtype=torch.float64, device="cuda")
+    sim.bind_tallies(labs.data_ptr(), instr.data_ptr())
+    sim.zero_tallies()
+
+    def step():
+        sim.run_stellar(first, share)
+        if world > 1:
+            # phase end: PanDustSystem::sumResults (Labs) and Instrument::sumResults, over RCCL/xGMI
+            dist.all_reduce(labs)
+            dist.all_reduce(instr)
+
+    for _ in range(args.warmup):
+        step()
+        sim.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    s0 = sim.stats()
+    kernel_ms = []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+        sim.synchronize()
+        kernel_ms.append(sim.stats()["kernel_ms"])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    s1 = sim.stats()
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    delta = {k: s1[k] - s0[k] for k in s1 if k != "kernel_ms"}
+    packets_all = share * world * args.steps
+    value = packets_all / elapsed
+    avg_kernel_s = sum(kernel_ms) / len(kernel_ms) / 1e3
+    bytes_per_launch = algorithmic_bytes(delta, geom_bytes, info.ncomp) / args.steps
+    achieved = bytes_per_launch / avg_kernel_s / 1e9
+    segs = delta["segments_fill"] + delta["segments_walk"] + delta["segments_peel"]
+
+    result = {
+        "metric": "photon packets/sec (whole node), 128^3 octree, 1/2/4/8 MI355X + HBM%",
+        "value": value,
+        "unit": "photon packets/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (Plummer stars + Plummer dust model of the reference's survey probes; no datasets)",
+        "config": {
+            "workload": desc,
+            "ski": ski_rel,
+            "cells": info.ncells,
+            "octree_nodes": info.nnodes,
+            "wavelengths": info.nlambda,
+            "packets_per_step_per_gpu": share,
+            "parallelism": "dp%d (packet sharding, RCCL all-reduce of Labs + instrument tallies per phase)" % world,
+            "segments_per_packet": segs / max(1, delta["packets"]),
+        },
+        "roofline": {
+            "bound": "hbm",
+            "achieved": achieved,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS,
+            "traffic": None,
+            "kernel": "stellarKernel<octree>" if info.grid_kind == 1 else "stellarKernel<cartesian>",
+            "kernel_ms_avg": avg_kernel_s * 1e3,
+            "algorithmic_bytes_per_launch": bytes_per_launch,
+        },
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        v, cores, sample = cpu_baseline(ski)
+        result["cpu_baseline"] = {"value": v, "unit": "photon packets/s", "cores": cores, "kind": "port",
+                                  "sample": sample}
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

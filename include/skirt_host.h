@@ -1,0 +1,62 @@
+/* skirt_host.h -- C API of the host side: .ski file -> model -> MI355X engine -> SKIRT-format outputs.
+ *
+ * This is the native replacement of the reference's simulation driver for the photon-shooting phases
+ * (Simulation::setupAndRun, SKIRTcore/Simulation.cpp:65-75; MonteCarloSimulation::runstellaremission,
+ * MonteCarloSimulation.cpp:251-261; MonteCarloSimulation::write, :553-558). Setup (ski parsing, grid
+ * construction, cell density sampling, optical tables, instrument geometry) runs on the host exactly as
+ * in the reference; the photon loop runs on the GPU through include/skirt_mcrt.h.
+ *
+ * Multi-GPU: one process per GPU. Each process loads the same ski, attaches its device and runs a slice
+ * of the global packet index space (skirt_sim_run_stellar(first, count)); the caller sums the device
+ * tallies across processes (RCCL all-reduce) before calling skirt_sim_write on one rank.
+ */
+#ifndef SKIRT_HOST_H
+#define SKIRT_HOST_H
+
+#include <stdint.h>
+
+#include "skirt_mcrt.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct SkirtSim SkirtSim;
+
+typedef struct {
+    int pan;                    /* PanMonteCarloSimulation (1) or Oligo (0) */
+    int ncells, nlambda, ncomp, ninstruments, grid_kind;
+    int nnodes;                 /* octree nodes (0 for Cartesian) */
+    uint64_t npp;               /* photon packets per wavelength (ceil(packages)) */
+    uint64_t total_packets;     /* npp * nlambda for the stellar phase */
+    uint64_t seed;
+    int store_absorption, has_dust;
+    double setup_seconds;
+} SkirtSimInfo;
+
+/* Parses the ski file and performs the host setup. packages > 0 overrides the ski's packages,
+ * seed != 0 overrides its random seed. datadir NULL = the packaged skirt_amd/data. Returns NULL on
+ * failure (skirt_sim_error). */
+SkirtSim* skirt_sim_load(const char* ski, const char* datadir, double packages, uint64_t seed);
+int skirt_sim_info(SkirtSim* sim, SkirtSimInfo* info);
+/* creates the engine on HIP device `device` and uploads grid, media, sources and instruments */
+int skirt_sim_attach(SkirtSim* sim, int device);
+SkirtMcrt* skirt_sim_engine(SkirtSim* sim);
+/* stellar emission over global packets [first, first+count) (count 0 = all); asynchronous */
+int skirt_sim_run_stellar(SkirtSim* sim, uint64_t first, uint64_t count);
+/* waits and copies the device tallies into the host accumulators */
+int skirt_sim_fetch(SkirtSim* sim);
+/* host accumulators after skirt_sim_fetch (same layouts as include/skirt_mcrt.h) */
+const double* skirt_sim_labs(SkirtSim* sim);
+const double* skirt_sim_instrument(SkirtSim* sim, int i, int* nslots, int* nframe, int* has_frames, int* has_seds);
+/* replaces the host accumulators (e.g. after an all-reduce done by the caller) */
+int skirt_sim_set_tallies(SkirtSim* sim, const double* labs, const double* instr);
+/* writes <prefix>_<instrument>_sed.dat, FITS frames and ds_isrf / ds_cellprops files */
+int skirt_sim_write(SkirtSim* sim, const char* prefix);
+const char* skirt_sim_error(void);
+void skirt_sim_free(SkirtSim* sim);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,155 @@
+/* skirt_mcrt.h -- C ABI of the MI355X photon-packet engine (the drop-in boundary).
+ *
+ * The reference runs every photon phase as Parallel::call(this, &X::do...chunk, assigner) over
+ * std::threads (SKIRTcore/Parallel.cpp:76-111), each chunk calling the plugin surface concurrently:
+ *   StellarComp::launch            SKIRTcore/StellarComp.hpp:42, StellarSystem.cpp:116-158
+ *   DustGrid::path / whichcell     SKIRTcore/DustGrid.hpp:70-106 (CartesianDustGrid, TreeDustGrid)
+ *   DustSystem::fillOpticalDepth / opticaldepth / absorb   SKIRTcore/DustSystem.hpp:352,366,397
+ *   Instrument::detect             SKIRTcore/Instrument.hpp:69-87, FullInstrument.cpp:107-174
+ * This ABI replaces those call sites (MonteCarloSimulation.cpp:256-257 stellar emission,
+ * PanMonteCarloSimulation.cpp:144-145 self-absorption, :260-261 dust emission) with one device launch
+ * per phase. The host describes the grid, media, sources and instruments once as flat arrays; each
+ * run call shoots a contiguous range of global packet indices, so the packet space can be sharded
+ * over GPUs (one process per GPU) with results independent of the shard count.
+ *
+ * Conventions: plain C, host owns every host buffer, all functions return 0 on success and a nonzero
+ * SKIRT_ERR_* code on failure (message via skirt_mcrt_last_error), no exceptions cross the boundary.
+ * Run calls are asynchronous on the engine's HIP stream; skirt_mcrt_synchronize or any download
+ * waits for completion. One context per simulation per GPU; a context is not reentrant.
+ * Layouts: Labs is row-major (cell, wavelength) like DustSystem::_Labs*vv (Table.hpp:104-105).
+ * Instrument tallies are per instrument [nslots][nlambda][nframe] frames followed by
+ * [nslots][nlambda] SEDs, slots as in FullInstrument (trav, strdir, strsca, dusdir, dussca,
+ * scattering levels...) or a single "total" slot for Simple/SED/Frame instruments.
+ */
+#ifndef SKIRT_MCRT_H
+#define SKIRT_MCRT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SKIRT_MCRT_ABI_VERSION 1
+
+enum {
+    SKIRT_OK = 0,
+    SKIRT_ERR_ARG = 1,       /* invalid argument / inconsistent sizes */
+    SKIRT_ERR_HIP = 2,       /* a HIP runtime call failed */
+    SKIRT_ERR_STATE = 3,     /* call order violated (e.g. run before upload) */
+    SKIRT_ERR_NUMERIC = 4,   /* "optical depth along the path is not a positive number" (DustSystem.cpp:976-979) */
+    SKIRT_ERR_UNSUPPORTED = 5
+};
+
+enum { SKIRT_GRID_CARTESIAN = 0, SKIRT_GRID_OCTREE = 1 };
+enum { SKIRT_TREE_TOPDOWN = 0, SKIRT_TREE_NEIGHBOR = 1 };
+enum { SKIRT_GEOM_PLUMMER = 0 };
+enum { SKIRT_INSTR_FULL = 0, SKIRT_INSTR_SIMPLE = 1, SKIRT_INSTR_SED = 2, SKIRT_INSTR_FRAME = 3 };
+enum { SKIRT_PHASE_STELLAR = 0, SKIRT_PHASE_DUST_EMISSION = 1, SKIRT_PHASE_DUST_SELFABS = 2 };
+
+typedef struct SkirtMcrt SkirtMcrt;
+
+/* Dust grid (replaces DustGrid::path/whichcell). Cartesian: border arrays of nx+1, ny+1, nz+1
+ * values, cell index m = k + nz*j + nz*ny*i (CartesianDustGrid.cpp:305-308). Octree: the reference's
+ * breadth-first node vector (TreeDustGrid.cpp:50-164): per node a box {xmin,ymin,zmin,xmax,ymax,zmax},
+ * the index of its first of 8 consecutive children (-1 for a leaf) and its cell number (-1 for
+ * non-leaves); neighbor lists per (node, wall) in CSR form, walls BACK FRONT LEFT RIGHT BOTTOM TOP,
+ * each list sorted by decreasing overlap (TreeNode::sortneighbors). */
+typedef struct {
+    int kind;
+    int ncells;
+    int nx, ny, nz;
+    const double *xv, *yv, *zv;
+    int nnodes;
+    const double* box;          /* 6 * nnodes */
+    const int* first_child;     /* nnodes */
+    const int* cellnumber;      /* nnodes */
+    const int* nbr_offset;      /* 6 * nnodes + 1 */
+    const int* nbr_list;        /* nbr_offset[6*nnodes] entries */
+    double eps;                 /* TreeDustGrid::_eps = 1e-12 * |extent widths| */
+    int search;                 /* SKIRT_TREE_* */
+} SkirtGridDesc;
+
+/* Dust media (replaces DustSystem::density and the KappaRho functor, DustSystem.cpp:465-491).
+ * rho is ncells x ncomp row-major; the optical tables are ncomp x nlambda row-major. */
+typedef struct {
+    int ncells, ncomp, nlambda;
+    const double* rho;
+    const double* kext;
+    const double* ksca;
+    const double* albedo;
+    const double* g;            /* Henyey-Greenstein asymmetry parameter */
+} SkirtMediaDesc;
+
+/* Stellar sources (replaces StellarSystem::launch, StellarSystem.cpp:116-158). */
+typedef struct {
+    int ncomp, nlambda;
+    const int* geom_kind;       /* ncomp, SKIRT_GEOM_* */
+    const double* geom_param;   /* ncomp x 4: Plummer {c, rho0, 0, 0} */
+    const double* lum;          /* ncomp x nlambda, W */
+    const double* lumtot;       /* nlambda, sum over components */
+    const double* cdf;          /* nlambda x (ncomp+1) normalized cumulative luminosity */
+    double emission_bias;
+} SkirtSourceDesc;
+
+/* Distant instruments (DistantInstrument.cpp:27-50, SingleFrameInstrument.cpp:24-38, 130-147). */
+typedef struct {
+    int kind;                   /* SKIRT_INSTR_* */
+    int nx, ny;
+    int scattering_levels;      /* FullInstrument only */
+    double kobs[3];
+    double sinphi, cosphi, sintheta, costheta, sinpa, cospa;
+    double xpmin, xpsiz, ypmin, ypsiz;
+} SkirtInstrDesc;
+
+/* MonteCarloSimulation properties used by the photon loop (MonteCarloSimulation.cpp:31-35). */
+typedef struct {
+    double min_weight_reduction;
+    int min_scatt_events;
+    double scatt_bias;
+    int store_absorption;       /* DustSystem::storeabsorptionrates() */
+    int has_dust;
+} SkirtPhaseParams;
+
+typedef struct {
+    uint64_t packets;           /* packets launched (primary, excluding peel-offs) */
+    uint64_t segments_fill;     /* grid segments walked by fillOpticalDepth-equivalent passes */
+    uint64_t segments_walk;     /* segments walked to locate interaction points */
+    uint64_t segments_peel;     /* segments walked by peel-off optical depth passes */
+    uint64_t detects;           /* peel-off detections */
+    uint64_t absorb_adds;       /* Labs atomic updates */
+    double kernel_ms;           /* device time of the last run call (HIP events on the engine stream) */
+} SkirtStats;
+
+int skirt_mcrt_abi_version(void);
+int skirt_mcrt_create(int device, SkirtMcrt** out);
+/* use an existing HIP stream (hipStream_t) instead of the engine's own; NULL restores the own stream */
+int skirt_mcrt_set_stream(SkirtMcrt* ctx, void* hip_stream);
+int skirt_mcrt_upload_grid(SkirtMcrt* ctx, const SkirtGridDesc* grid);
+int skirt_mcrt_upload_media(SkirtMcrt* ctx, const SkirtMediaDesc* media);
+int skirt_mcrt_upload_sources(SkirtMcrt* ctx, const SkirtSourceDesc* src);
+int skirt_mcrt_set_instruments(SkirtMcrt* ctx, const SkirtInstrDesc* instr, int n);
+/* device tally buffers: Labs (ncells*nlambda doubles, stored wavelength-major [nlambda][ncells] on the
+ * device) and the concatenated instrument tallies. Optionally bind caller-owned device memory of the
+ * sizes returned by skirt_mcrt_tally_sizes (e.g. torch tensors, so they can be all-reduced in place). */
+int skirt_mcrt_tally_sizes(SkirtMcrt* ctx, size_t* n_labs, size_t* n_instr);
+int skirt_mcrt_bind_tallies(SkirtMcrt* ctx, double* d_labs, double* d_instr);
+int skirt_mcrt_zero_tallies(SkirtMcrt* ctx);
+/* Stellar emission phase over global packet indices [first, first+count) of a phase with npp packets
+ * per wavelength (packet p has wavelength index p / npp). Asynchronous. */
+int skirt_mcrt_run_stellar(SkirtMcrt* ctx, uint64_t npp, uint64_t first, uint64_t count, uint64_t seed,
+                           const SkirtPhaseParams* params);
+int skirt_mcrt_synchronize(SkirtMcrt* ctx);
+/* Copies tallies to host (Labs converted to row-major cell x wavelength); either pointer may be NULL. */
+int skirt_mcrt_download(SkirtMcrt* ctx, double* labs, double* instr);
+int skirt_mcrt_stats(SkirtMcrt* ctx, SkirtStats* out);
+/* kernel configuration knobs (0 = default): threads per block, blocks, event batching threshold */
+int skirt_mcrt_configure(SkirtMcrt* ctx, int block, int grid, int event_threshold);
+const char* skirt_mcrt_last_error(SkirtMcrt* ctx);
+void skirt_mcrt_destroy(SkirtMcrt* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -301,11 +301,30 @@ void octreePath(const OctreeGrid& t, Vec3 r, Vec3 k, Path& p) {
 
 // ============================================================ simulation
 
+// LockFree::add (Fundamentals/LockFree.hpp:25-37): compare-and-swap loop on a double
+inline void lockFreeAdd(double* p, double v) {
+    uint64_t* q = reinterpret_cast<uint64_t*>(p);
+    uint64_t cur = __atomic_load_n(q, __ATOMIC_RELAXED);
+    while (true) {
+        double d;
+        std::memcpy(&d, &cur, 8);
+        d += v;
+        uint64_t nw;
+        std::memcpy(&nw, &d, 8);
+        if (__atomic_compare_exchange_n(q, &cur, nw, true, __ATOMIC_RELAXED, __ATOMIC_RELAXED)) return;
+    }
+}
+
 struct Tallies {
+    bool shared = false;       // threaded mode: one set of arrays updated with lock-free adds
+    void add(std::vector<double>& v, size_t i, double x) {
+        if (shared) lockFreeAdd(&v[i], x);
+        else v[i] += x;
+    }
     std::vector<double> labs;  // Ncells x Nlambda row-major (stellar)
     std::vector<double> labsDust;
     std::vector<std::vector<double>> frames, seds;  // per instrument
-    uint64_t segments = 0;
+    std::atomic<uint64_t> segments{0};
 };
 
 class Sim {
@@ -352,14 +371,14 @@ public:
         if (M.hasDust) {
             Vec3 ko{ins.kobs[0], ins.kobs[1], ins.kobs[2]};
             path(pp.r, ko, tmp);
-            t.segments += tmp.v.size();
+            t.segments.fetch_add(tmp.v.size(), std::memory_order_relaxed);
             for (auto& s : tmp.v) taupath += M.kapparho(s.m, ell) * s.ds;
         }
         double extf = exp(-taupath);
         double Lextf = L * extf;
-        auto sed = [&](int slot, double v) { t.seds[i][(size_t)slot * Nl + ell] += v; };
+        auto sed = [&](int slot, double v) { t.add(t.seds[i], (size_t)slot * Nl + ell, v); };
         auto frm = [&](int slot, double v) {
-            if (l >= 0) t.frames[i][((size_t)slot * Nl + ell) * ins.nframe() + l] += v;
+            if (l >= 0) t.add(t.frames[i], ((size_t)slot * Nl + ell) * ins.nframe() + l, v);
         };
         if (ins.kind != InstrumentKind::Full) {
             if (ins.hasSeds()) sed(0, Lextf);
@@ -393,7 +412,7 @@ public:
         while (true) {
             // DustSystem::fillOpticalDepth
             path(pp.r, pp.k, p);
-            t.segments += p.v.size();
+            t.segments.fetch_add(p.v.size(), std::memory_order_relaxed);
             double tau = 0;
             for (auto& s : p.v) {
                 double dtau = M.kapparho(s.m, pp.ell) * s.ds;
@@ -418,7 +437,7 @@ public:
                             double expfactorm = -expm1(-p.v[n].dtau);
                             double Lintm = L * exp(-taustart) * expfactorm;
                             double Labsm = (1.0 - albedo) * Lintm;
-                            (*labs)[(size_t)m * Nl + pp.ell] += Labsm;
+                            t.add(*labs, (size_t)m * Nl + pp.ell, Labsm);
                         }
                     }
                 }
@@ -440,7 +459,7 @@ public:
                         double expfactorm = -expm1(-p.v[n].dtau);
                         double Lintm = L * exp(-taustart) * expfactorm;
                         Lsca += albedo * Lintm;
-                        if (store) (*labs)[(size_t)m * Nl + pp.ell] += (1.0 - albedo) * Lintm;
+                        if (store) t.add(*labs, (size_t)m * Nl + pp.ell, (1.0 - albedo) * Lintm);
                     }
                 }
                 pp.L = Lsca;
@@ -640,17 +659,17 @@ OracleRun* oracle_run(const char* ski, const char* datadir, int rngKind, int nth
             }
         } else {
             int T = std::max(1, nthreads);
-            std::vector<Tallies> part(T);
+            Tallies& tl = run->tal;
+            tl.shared = true;
             std::vector<std::thread> th;
             std::atomic<uint64_t> next{pb};
-            const uint64_t grain = 256;
+            std::atomic<uint64_t> segs{0};
+            const uint64_t grain = 64;
             std::vector<std::string> errs(T);
             std::vector<uint64_t> cnt(T, 0);
             for (int w = 0; w < T; w++) {
                 th.emplace_back([&, w] {
                     try {
-                        Tallies& tl = part[w];
-                        sim.initTallies(tl);
                         PhiloxRng rng(theSeed, 0);
                         Path p, tmp;
                         p.v.reserve(1024);
@@ -684,17 +703,8 @@ OracleRun* oracle_run(const char* ski, const char* datadir, int rngKind, int nth
             for (auto& x : th) x.join();
             for (int w = 0; w < T; w++)
                 if (!errs[w].empty()) throw std::runtime_error(errs[w]);
-            // deterministic reduction in worker order
-            for (int w = 0; w < T; w++) {
-                Tallies& tl = part[w];
-                run->packets += cnt[w];
-                run->tal.segments += tl.segments;
-                for (size_t q = 0; q < tl.labs.size(); q++) run->tal.labs[q] += tl.labs[q];
-                for (size_t i = 0; i < tl.frames.size(); i++) {
-                    for (size_t q = 0; q < tl.frames[i].size(); q++) run->tal.frames[i][q] += tl.frames[i][q];
-                    for (size_t q = 0; q < tl.seds[i].size(); q++) run->tal.seds[i][q] += tl.seds[i][q];
-                }
-            }
+            for (int w = 0; w < T; w++) run->packets += cnt[w];
+            tl.shared = false;
         }
         run->seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
         if (outprefix && *outprefix) {

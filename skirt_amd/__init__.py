@@ -1,0 +1,200 @@
+"""skirt_amd -- MI355X-native photon-packet engine for SKIRT's photon-shooting hot path.
+
+The package is a thin Python face over the native library ``libskirt_amd.so`` (HIP kernels for gfx950
+plus the C++ host driver): ``include/skirt_mcrt.h`` is the engine's C ABI, ``include/skirt_host.h``
+the host driver (.ski -> model -> engine -> SKIRT-format outputs). Python is used only for plumbing
+(tests, benchmarking, torch.distributed/RCCL reductions across GPUs); no compute happens here and
+there is no CPU fallback: if the native library is missing, importing the engine fails loudly.
+
+Mirrors the reference's simulation interface for this path:
+    sim = Simulation("model.ski")            # Simulation::setup (SKIRTcore/Simulation.cpp:36-48)
+    sim.attach(device=0)
+    sim.run_stellar()                        # MonteCarloSimulation::runstellaremission (:251-261)
+    sim.fetch(); sim.write("out/model")      # MonteCarloSimulation::write (:553-558)
+"""
+import ctypes
+import os
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG_DIR, "libskirt_amd.so")
+DATA_DIR = os.path.join(PKG_DIR, "data")
+
+GRID_CARTESIAN, GRID_OCTREE = 0, 1
+
+
+class SkirtError(RuntimeError):
+    pass
+
+
+class SkirtStats(ctypes.Structure):
+    _fields_ = [("packets", ctypes.c_uint64), ("segments_fill", ctypes.c_uint64),
+                ("segments_walk", ctypes.c_uint64), ("segments_peel", ctypes.c_uint64),
+                ("detects", ctypes.c_uint64), ("absorb_adds", ctypes.c_uint64), ("kernel_ms", ctypes.c_double)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+class SkirtSimInfo(ctypes.Structure):
+    _fields_ = [("pan", ctypes.c_int), ("ncells", ctypes.c_int), ("nlambda", ctypes.c_int), ("ncomp", ctypes.c_int),
+                ("ninstruments", ctypes.c_int), ("grid_kind", ctypes.c_int), ("nnodes", ctypes.c_int),
+                ("npp", ctypes.c_uint64), ("total_packets", ctypes.c_uint64), ("seed", ctypes.c_uint64),
+                ("store_absorption", ctypes.c_int), ("has_dust", ctypes.c_int), ("setup_seconds", ctypes.c_double)]
+
+
+# every symbol declared by include/skirt_mcrt.h and include/skirt_host.h
+ABI_SYMBOLS = [
+    "skirt_mcrt_abi_version", "skirt_mcrt_create", "skirt_mcrt_set_stream", "skirt_mcrt_upload_grid",
+    "skirt_mcrt_upload_media", "skirt_mcrt_upload_sources", "skirt_mcrt_set_instruments",
+    "skirt_mcrt_tally_sizes", "skirt_mcrt_bind_tallies", "skirt_mcrt_zero_tallies", "skirt_mcrt_run_stellar",
+    "skirt_mcrt_synchronize", "skirt_mcrt_download", "skirt_mcrt_stats", "skirt_mcrt_configure",
+    "skirt_mcrt_last_error", "skirt_mcrt_destroy",
+    "skirt_sim_load", "skirt_sim_info", "skirt_sim_attach", "skirt_sim_engine", "skirt_sim_run_stellar",
+    "skirt_sim_fetch", "skirt_sim_labs", "skirt_sim_instrument", "skirt_sim_set_tallies", "skirt_sim_write",
+    "skirt_sim_error", "skirt_sim_free",
+]
+
+_lib = None
+
+
+def lib():
+    """The native library; raises SkirtError when it has not been built (no silent fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise SkirtError("native library %s is missing: run `make -C skirt_amd/csrc` "
+                             "(or __graft_entry__.build())" % LIB_PATH)
+        L = ctypes.CDLL(LIB_PATH)
+        vp, c_int, c_u64, c_dbl = ctypes.c_void_p, ctypes.c_int, ctypes.c_uint64, ctypes.c_double
+        L.skirt_sim_load.restype = vp
+        L.skirt_sim_load.argtypes = [ctypes.c_char_p, ctypes.c_char_p, c_dbl, c_u64]
+        L.skirt_sim_info.argtypes = [vp, ctypes.POINTER(SkirtSimInfo)]
+        L.skirt_sim_attach.argtypes = [vp, c_int]
+        L.skirt_sim_engine.restype = vp
+        L.skirt_sim_engine.argtypes = [vp]
+        L.skirt_sim_run_stellar.argtypes = [vp, c_u64, c_u64]
+        L.skirt_sim_fetch.argtypes = [vp]
+        L.skirt_sim_labs.restype = ctypes.POINTER(c_dbl)
+        L.skirt_sim_labs.argtypes = [vp]
+        L.skirt_sim_instrument.restype = ctypes.POINTER(c_dbl)
+        L.skirt_sim_instrument.argtypes = [vp, c_int] + [ctypes.POINTER(c_int)] * 4
+        L.skirt_sim_set_tallies.argtypes = [vp, ctypes.POINTER(c_dbl), ctypes.POINTER(c_dbl)]
+        L.skirt_sim_write.argtypes = [vp, ctypes.c_char_p]
+        L.skirt_sim_error.restype = ctypes.c_char_p
+        L.skirt_sim_free.argtypes = [vp]
+        L.skirt_mcrt_stats.argtypes = [vp, ctypes.POINTER(SkirtStats)]
+        L.skirt_mcrt_last_error.restype = ctypes.c_char_p
+        L.skirt_mcrt_last_error.argtypes = [vp]
+        L.skirt_mcrt_set_stream.argtypes = [vp, vp]
+        L.skirt_mcrt_tally_sizes.argtypes = [vp, ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(ctypes.c_size_t)]
+        L.skirt_mcrt_bind_tallies.argtypes = [vp, vp, vp]
+        L.skirt_mcrt_zero_tallies.argtypes = [vp]
+        L.skirt_mcrt_synchronize.argtypes = [vp]
+        L.skirt_mcrt_configure.argtypes = [vp, c_int, c_int, c_int]
+        _lib = L
+    return _lib
+
+
+class Simulation:
+    """One SKIRT simulation (a .ski file) driven through the native host library."""
+
+    def __init__(self, ski, packages=0.0, seed=0, datadir=None):
+        L = lib()
+        self._h = L.skirt_sim_load(os.fspath(ski).encode(), (datadir or DATA_DIR).encode(), float(packages), int(seed))
+        if not self._h:
+            raise SkirtError(L.skirt_sim_error().decode())
+        info = SkirtSimInfo()
+        L.skirt_sim_info(self._h, ctypes.byref(info))
+        self.info = info
+        self.attached = False
+
+    def _check(self, rc):
+        if rc != 0:
+            raise SkirtError(lib().skirt_sim_error().decode())
+
+    @property
+    def engine(self):
+        return lib().skirt_sim_engine(self._h)
+
+    def attach(self, device=0):
+        self._check(lib().skirt_sim_attach(self._h, device))
+        self.attached = True
+
+    def configure(self, grid=0, threshold=0):
+        self._check_engine(lib().skirt_mcrt_configure(self.engine, 0, grid, threshold))
+
+    def _check_engine(self, rc):
+        if rc != 0:
+            raise SkirtError(lib().skirt_mcrt_last_error(self.engine).decode())
+
+    def set_stream(self, stream_ptr):
+        self._check_engine(lib().skirt_mcrt_set_stream(self.engine, ctypes.c_void_p(stream_ptr)))
+
+    def tally_sizes(self):
+        a, b = ctypes.c_size_t(), ctypes.c_size_t()
+        lib().skirt_mcrt_tally_sizes(self.engine, ctypes.byref(a), ctypes.byref(b))
+        return a.value, b.value
+
+    def bind_tallies(self, labs_ptr, instr_ptr):
+        self._check_engine(lib().skirt_mcrt_bind_tallies(self.engine, ctypes.c_void_p(labs_ptr),
+                                                         ctypes.c_void_p(instr_ptr)))
+
+    def zero_tallies(self):
+        self._check_engine(lib().skirt_mcrt_zero_tallies(self.engine))
+
+    def run_stellar(self, first=0, count=0):
+        self._check(lib().skirt_sim_run_stellar(self._h, first, count))
+
+    def synchronize(self):
+        self._check_engine(lib().skirt_mcrt_synchronize(self.engine))
+
+    def fetch(self):
+        self._check(lib().skirt_sim_fetch(self._h))
+
+    def stats(self):
+        s = SkirtStats()
+        self._check_engine(lib().skirt_mcrt_stats(self.engine, ctypes.byref(s)))
+        return s.as_dict()
+
+    def labs(self):
+        p = lib().skirt_sim_labs(self._h)
+        if not p:
+            return None
+        return np.ctypeslib.as_array(p, shape=(self.info.ncells, self.info.nlambda)).copy()
+
+    def instrument(self, i):
+        """(frames [nslots, nlambda, nframe] or None, seds [nslots, nlambda] or None)"""
+        ns, nf, hf, hs = ctypes.c_int(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        p = lib().skirt_sim_instrument(self._h, i, ctypes.byref(ns), ctypes.byref(nf), ctypes.byref(hf),
+                                       ctypes.byref(hs))
+        if not p:
+            raise SkirtError("no instrument %d" % i)
+        nl = self.info.nlambda
+        n_frames = ns.value * nl * nf.value if hf.value else 0
+        arr = np.ctypeslib.as_array(p, shape=(n_frames + (ns.value * nl if hs.value else 0),)).copy()
+        frames = arr[:n_frames].reshape(ns.value, nl, nf.value) if hf.value else None
+        seds = arr[n_frames:].reshape(ns.value, nl) if hs.value else None
+        return frames, seds
+
+    def set_tallies(self, labs=None, instr=None):
+        P = ctypes.POINTER(ctypes.c_double)
+        la = np.ascontiguousarray(labs, dtype=np.float64) if labs is not None else None
+        ia = np.ascontiguousarray(instr, dtype=np.float64) if instr is not None else None
+        self._check(lib().skirt_sim_set_tallies(self._h, la.ctypes.data_as(P) if la is not None else None,
+                                                ia.ctypes.data_as(P) if ia is not None else None))
+
+    def write(self, prefix):
+        self._check(lib().skirt_sim_write(self._h, os.fspath(prefix).encode()))
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().skirt_sim_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

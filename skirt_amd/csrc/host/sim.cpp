@@ -1,0 +1,235 @@
+// Host driver: .ski -> Model -> device engine -> outputs (include/skirt_host.h).
+#include <chrono>
+#include <cmath>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../../include/skirt_host.h"
+#include "model.hpp"
+#include "outputs.hpp"
+
+using namespace skirt;
+
+namespace {
+thread_local std::string g_err;
+}
+
+struct SkirtSim {
+    Model m;
+    double setupSeconds = 0;
+    uint64_t npp = 0;
+    SkirtMcrt* eng = nullptr;
+    std::vector<double> labs;                 // Ncells x Nlambda
+    std::vector<double> instrAll;             // concatenated device layout
+    std::vector<size_t> instrOff;             // per instrument offset into instrAll
+    std::vector<std::vector<double>> frames, seds;
+    ~SkirtSim() {
+        if (eng) skirt_mcrt_destroy(eng);
+    }
+    size_t instrTotal() const {
+        size_t n = 0;
+        for (auto& ins : m.instruments) {
+            if (ins.hasFrames()) n += (size_t)ins.nslots() * m.wl.n() * ins.nframe();
+            if (ins.hasSeds()) n += (size_t)ins.nslots() * m.wl.n();
+        }
+        return n;
+    }
+    void splitInstr() {
+        frames.assign(m.instruments.size(), {});
+        seds.assign(m.instruments.size(), {});
+        size_t off = 0;
+        for (size_t i = 0; i < m.instruments.size(); i++) {
+            const Instrument& ins = m.instruments[i];
+            size_t nf = ins.hasFrames() ? (size_t)ins.nslots() * m.wl.n() * ins.nframe() : 0;
+            size_t ns = ins.hasSeds() ? (size_t)ins.nslots() * m.wl.n() : 0;
+            frames[i].assign(instrAll.begin() + off, instrAll.begin() + off + nf);
+            off += nf;
+            seds[i].assign(instrAll.begin() + off, instrAll.begin() + off + ns);
+            off += ns;
+        }
+    }
+};
+
+namespace {
+int check(SkirtSim* s, int rc) {
+    if (rc != SKIRT_OK) g_err = s && s->eng ? skirt_mcrt_last_error(s->eng) : "engine error";
+    return rc;
+}
+}  // namespace
+
+extern "C" {
+
+const char* skirt_sim_error(void) { return g_err.c_str(); }
+
+SkirtSim* skirt_sim_load(const char* ski, const char* datadir, double packages, uint64_t seed) {
+    try {
+        auto s = std::make_unique<SkirtSim>();
+        auto t0 = std::chrono::steady_clock::now();
+        unsigned long theSeed = seed ? (unsigned long)seed : readSkiSeed(ski);
+        MTRandom mt(theSeed);  // setup draws exactly like the reference (density / tree sampling)
+        s->m = loadSki(ski, mt, datadir && *datadir ? datadir : defaultDataDir());
+        s->m.seed = theSeed;
+        if (packages > 0) s->m.packages = packages;
+        s->npp = (uint64_t)std::ceil(s->m.packages);
+        s->setupSeconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        s->labs.assign(s->m.hasDust && s->m.storeAbsorption ? (size_t)s->m.ncells() * s->m.wl.n() : 0, 0.0);
+        s->instrAll.assign(s->instrTotal(), 0.0);
+        s->splitInstr();
+        return s.release();
+    } catch (std::exception& e) {
+        g_err = e.what();
+        return nullptr;
+    }
+}
+
+int skirt_sim_info(SkirtSim* s, SkirtSimInfo* o) {
+    if (!s || !o) return SKIRT_ERR_ARG;
+    o->pan = s->m.pan;
+    o->ncells = s->m.ncells();
+    o->nlambda = s->m.wl.n();
+    o->ncomp = s->m.ncomp();
+    o->ninstruments = (int)s->m.instruments.size();
+    o->grid_kind = s->m.grid.kind == GridKind::Octree ? SKIRT_GRID_OCTREE : SKIRT_GRID_CARTESIAN;
+    o->nnodes = s->m.grid.kind == GridKind::Octree ? s->m.grid.tree.nnodes() : 0;
+    o->npp = s->npp;
+    o->total_packets = s->npp * (uint64_t)s->m.wl.n();
+    o->seed = s->m.seed;
+    o->store_absorption = s->m.hasDust && s->m.storeAbsorption;
+    o->has_dust = s->m.hasDust;
+    o->setup_seconds = s->setupSeconds;
+    return SKIRT_OK;
+}
+
+int skirt_sim_attach(SkirtSim* s, int device) {
+    if (!s) return SKIRT_ERR_ARG;
+    if (s->eng) { skirt_mcrt_destroy(s->eng); s->eng = nullptr; }
+    int rc = skirt_mcrt_create(device, &s->eng);
+    if (rc) { g_err = "cannot create the engine on device " + std::to_string(device); return rc; }
+    const Model& m = s->m;
+    int Nl = m.wl.n();
+    if (m.hasDust) {
+        SkirtGridDesc g{};
+        g.ncells = m.ncells();
+        if (m.grid.kind == GridKind::Cartesian) {
+            g.kind = SKIRT_GRID_CARTESIAN;
+            g.nx = m.grid.cart.Nx; g.ny = m.grid.cart.Ny; g.nz = m.grid.cart.Nz;
+            g.xv = m.grid.cart.xv.data(); g.yv = m.grid.cart.yv.data(); g.zv = m.grid.cart.zv.data();
+        } else {
+            const OctreeGrid& t = m.grid.tree;
+            g.kind = SKIRT_GRID_OCTREE;
+            g.nnodes = t.nnodes();
+            g.box = t.box.data();
+            g.first_child = t.firstChild.data();
+            g.cellnumber = t.cellnumber.data();
+            g.nbr_offset = t.nbrOffset.data();
+            g.nbr_list = t.nbrList.data();
+            g.eps = t.eps;
+            g.search = t.search == 0 ? SKIRT_TREE_TOPDOWN : SKIRT_TREE_NEIGHBOR;
+            if (t.search == 2) { g_err = "Bookkeeping tree search is not supported by the engine"; return SKIRT_ERR_UNSUPPORTED; }
+        }
+        if ((rc = check(s, skirt_mcrt_upload_grid(s->eng, &g)))) return rc;
+        int nc = m.ncomp();
+        std::vector<double> kext(nc * Nl), ksca(nc * Nl), alb(nc * Nl), gg(nc * Nl);
+        for (int h = 0; h < nc; h++)
+            for (int ell = 0; ell < Nl; ell++) {
+                kext[h * Nl + ell] = m.dust[h].mix.kext[ell];
+                ksca[h * Nl + ell] = m.dust[h].mix.ksca[ell];
+                alb[h * Nl + ell] = m.dust[h].mix.albedo[ell];
+                gg[h * Nl + ell] = m.dust[h].mix.g[ell];
+            }
+        SkirtMediaDesc md{m.ncells(), nc, Nl, m.rho.data(), kext.data(), ksca.data(), alb.data(), gg.data()};
+        if ((rc = check(s, skirt_mcrt_upload_media(s->eng, &md)))) return rc;
+    }
+    int ns = (int)m.starL.size();
+    std::vector<int> gk(ns, SKIRT_GEOM_PLUMMER);
+    std::vector<double> gp(4 * ns, 0.0), lum(ns * Nl), cdf(Nl * (ns + 1));
+    for (int h = 0; h < ns; h++) {
+        gp[4 * h] = m.starGeom[h].c;
+        gp[4 * h + 1] = m.starGeom[h].rho0;
+        for (int ell = 0; ell < Nl; ell++) lum[h * Nl + ell] = m.starL[h][ell];
+    }
+    for (int ell = 0; ell < Nl; ell++)
+        for (int q = 0; q <= ns; q++) cdf[ell * (ns + 1) + q] = m.starX[ell][q];
+    SkirtSourceDesc sd{ns, Nl, gk.data(), gp.data(), lum.data(), m.starLtot.data(), cdf.data(), m.starEmissionBias};
+    if ((rc = check(s, skirt_mcrt_upload_sources(s->eng, &sd)))) return rc;
+    std::vector<SkirtInstrDesc> ids;
+    for (const Instrument& ins : m.instruments) {
+        SkirtInstrDesc d{};
+        d.kind = (int)ins.kind;
+        d.nx = ins.Nx; d.ny = ins.Ny;
+        d.scattering_levels = ins.scatteringLevels;
+        for (int q = 0; q < 3; q++) d.kobs[q] = ins.kobs[q];
+        d.sinphi = ins.sinphi; d.cosphi = ins.cosphi; d.sintheta = ins.sintheta; d.costheta = ins.costheta;
+        d.sinpa = ins.sinpa; d.cospa = ins.cospa;
+        d.xpmin = ins.xpmin; d.xpsiz = ins.xpsiz; d.ypmin = ins.ypmin; d.ypsiz = ins.ypsiz;
+        ids.push_back(d);
+    }
+    if ((rc = check(s, skirt_mcrt_set_instruments(s->eng, ids.data(), (int)ids.size())))) return rc;
+    size_t nl = 0, ni = 0;
+    skirt_mcrt_tally_sizes(s->eng, &nl, &ni);
+    if (ni != s->instrAll.size()) { g_err = "instrument tally size mismatch"; return SKIRT_ERR_STATE; }
+    return check(s, skirt_mcrt_zero_tallies(s->eng));
+}
+
+SkirtMcrt* skirt_sim_engine(SkirtSim* s) { return s ? s->eng : nullptr; }
+
+int skirt_sim_run_stellar(SkirtSim* s, uint64_t first, uint64_t count) {
+    if (!s || !s->eng) { g_err = "no engine attached"; return SKIRT_ERR_STATE; }
+    uint64_t total = s->npp * (uint64_t)s->m.wl.n();
+    if (count == 0) count = total - std::min(first, total);
+    SkirtPhaseParams p{s->m.minWeightReduction, s->m.minScattEvents, s->m.scattBias,
+                       s->m.hasDust && s->m.storeAbsorption ? 1 : 0, s->m.hasDust ? 1 : 0};
+    return check(s, skirt_mcrt_run_stellar(s->eng, s->npp, first, count, s->m.seed, &p));
+}
+
+int skirt_sim_fetch(SkirtSim* s) {
+    if (!s || !s->eng) { g_err = "no engine attached"; return SKIRT_ERR_STATE; }
+    int rc = check(s, skirt_mcrt_download(s->eng, s->labs.empty() ? nullptr : s->labs.data(),
+                                          s->instrAll.empty() ? nullptr : s->instrAll.data()));
+    if (rc) return rc;
+    s->splitInstr();
+    return SKIRT_OK;
+}
+
+const double* skirt_sim_labs(SkirtSim* s) { return s && !s->labs.empty() ? s->labs.data() : nullptr; }
+
+const double* skirt_sim_instrument(SkirtSim* s, int i, int* nslots, int* nframe, int* hasFrames, int* hasSeds) {
+    if (!s || i < 0 || i >= (int)s->m.instruments.size()) return nullptr;
+    const Instrument& ins = s->m.instruments[i];
+    if (nslots) *nslots = ins.nslots();
+    if (nframe) *nframe = ins.hasFrames() ? ins.nframe() : 0;
+    if (hasFrames) *hasFrames = ins.hasFrames();
+    if (hasSeds) *hasSeds = ins.hasSeds();
+    size_t off = 0;
+    for (int q = 0; q < i; q++) {
+        const Instrument& o = s->m.instruments[q];
+        if (o.hasFrames()) off += (size_t)o.nslots() * s->m.wl.n() * o.nframe();
+        if (o.hasSeds()) off += (size_t)o.nslots() * s->m.wl.n();
+    }
+    return s->instrAll.data() + off;
+}
+
+int skirt_sim_set_tallies(SkirtSim* s, const double* labs, const double* instr) {
+    if (!s) return SKIRT_ERR_ARG;
+    if (labs && !s->labs.empty()) std::copy(labs, labs + s->labs.size(), s->labs.begin());
+    if (instr && !s->instrAll.empty()) std::copy(instr, instr + s->instrAll.size(), s->instrAll.begin());
+    s->splitInstr();
+    return SKIRT_OK;
+}
+
+int skirt_sim_write(SkirtSim* s, const char* prefix) {
+    if (!s || !prefix) return SKIRT_ERR_ARG;
+    try {
+        writeOutputs(s->m, prefix, s->frames, s->seds, s->labs);
+    } catch (std::exception& e) {
+        g_err = e.what();
+        return SKIRT_ERR_ARG;
+    }
+    return SKIRT_OK;
+}
+
+void skirt_sim_free(SkirtSim* s) { delete s; }
+
+}  // extern "C"
