@@ -1,24 +1,28 @@
-// MI355X photon-packet engine: persistent-wavefront HIP kernels + the C ABI of include/skirt_mcrt.h.
+// MI355X photon-packet engine: HIP kernels for gfx950 + the C ABI of include/skirt_mcrt.h.
 //
-// One kernel launch runs one photon phase over a contiguous range of global packet indices. Every
-// lane of every wavefront is a photon "slot" that runs the reference's per-packet life cycle
-// (MonteCarloSimulation.cpp:265-301 launch -> peel-off -> fill/absorb -> propagate -> peel-off ->
-// scatter) as a state machine whose expensive part -- walking a ray through the dust grid -- is one
-// uniform loop body for all lanes. Ray kinds:
-//   PEEL  optical depth to the grid edge towards an instrument (DustSystem::opticaldepth,
-//         DustGridPath::opticalDepth, DustGridPath.hpp:97-108), then Instrument::detect;
-//   FILL  fillOpticalDepth + simulateescapeandabsorption fused into one streaming pass (absorption of
-//         segment n needs only tau_{n-1} and dtau_n, MonteCarloSimulation.cpp:447-470), f64 atomics
-//         into Labs;
-//   WALK  the same path walked again up to the sampled optical depth, replacing the stored segment
-//         vector + NR::locate of DustGridPath::pathlength (DustGridPath.cpp:162-173) -- no per-lane
-//         path buffer ever touches HBM.
-// Lanes whose ray ended wait until enough lanes of the wave are waiting (ballot count >= threshold),
-// then all of them run their event code together (launch, detect, sampling, scattering) and start
-// their next ray, so the divergent event code is amortized over many lanes. New packets are claimed
-// 64 at a time with one atomic per wave (ballot + mbcnt).
-// Arithmetic follows the reference operation by operation (IEEE f64 division, exp/expm1/log), so a
-// packet's history matches the CPU oracle's Philox mode to rounding.
+// A photon phase (MonteCarloSimulation::dostellaremissionchunk, MonteCarloSimulation.cpp:265-301)
+// runs as a wavefront pipeline over a pool of packet slots resident in HBM:
+//
+//   eventKernel  one thread per active slot: consumes the result of the slot's last ray and runs the
+//                packet's event code in the reference's order -- launch (StellarSystem::launch),
+//                escape/absorption bookkeeping and termination (simulateescapeandabsorption),
+//                interaction sampling (simulatepropagation), propagation, peel-off weights
+//                (peeloffscattering) and scattering (simulatescattering) -- then queues the packet's
+//                next rays: its next FILL or WALK ray plus one PEEL ray per instrument. A finished
+//                slot claims the next global packet index at once.
+//   traceKernel  persistent: every lane pulls rays from the queue (one atomic per wave, ballot +
+//                mbcnt) and walks them through the dust grid, one uniform loop body for all lanes:
+//     FILL  DustSystem::fillOpticalDepth + the absorption of simulateescapeandabsorption fused in one
+//           streaming pass (segment n needs only exp(-tau_{n-1}) and dtau_n,
+//           MonteCarloSimulation.cpp:447-470), f64 atomics into Labs; result: tau of the path;
+//     WALK  the same path again up to the sampled optical depth, interpolating inside the crossing
+//           segment like DustGridPath::pathlength (DustGridPath.cpp:162-173); result: the distance;
+//     PEEL  optical depth to the grid edge towards an instrument (DustSystem::opticaldepth), then
+//           Instrument::detect into LDS-privatized SED sums and f64 frame atomics.
+// Peel-off detections only add to tallies, so they run concurrently with the packet's next FILL ray;
+// the random-number sequence of every packet is exactly the reference's. The trace kernel holds only
+// the ray in registers (the heavy event code lives in the other kernel), which keeps its occupancy
+// high enough to hide the latency of the density / tree gathers.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -38,20 +42,38 @@ namespace {
 constexpr double kDblMax = 1.7976931348623157e308;
 constexpr int kBlock = 256;
 
-// ------------------------------------------------------------------ device-side descriptors
+// ------------------------------------------------------------------ descriptors
 struct DevInstr {
-    int kind, nx, ny, nslots, levels, sedOff;  // sedOff: offset of this instrument's SEDs in LDS accumulator
-    long long frameBase;                        // offset of frames in the global instrument tally
-    long long sedBase;                          // offset of SEDs in the global instrument tally
+    int kind, nx, ny, nslots, levels, sedOff;  // sedOff: offset of this instrument's SEDs in the LDS sums
+    long long frameBase;                        // offset of the frames in the global instrument tally
+    long long sedBase;                          // offset of the SEDs in the global instrument tally
     double kobs[3];
     double sinphi, cosphi, sintheta, costheta, sinpa, cospa;
     double xpmin, xpsiz, ypmin, ypsiz;
 };
 
+enum RayMode : unsigned { RAY_NONE = 0, RAY_PEEL = 1, RAY_FILL = 2, RAY_WALK = 3 };
+enum State : int { S_NEW = 0, S_FILL = 2, S_WALK = 3 };
+// peel-off categories (which FullInstrument arrays a detection adds to, FullInstrument.cpp:115-171)
+enum PeelCat : unsigned { CAT_STAR_DIRECT = 0, CAT_STAR_SCATTERED = 1, CAT_DUST_DIRECT = 2, CAT_DUST_SCATTERED = 3 };
+
+// one queued ray, 64 bytes
+struct RayRec {
+    double x, y, z, dx, dy, dz;
+    double param;    // FILL: packet luminosity L; WALK: optical depth to reach; PEEL: peel-off luminosity
+    int idx;         // FILL/WALK: slot; PEEL: frame pixel (-1: none)
+    unsigned flags;  // mode | cat << 2 | instrument << 4 | scattering level << 10 | ell << 18
+};
+__device__ __forceinline__ unsigned rayMode(unsigned f) { return f & 3u; }
+__device__ __forceinline__ unsigned rayCat(unsigned f) { return (f >> 2) & 3u; }
+__device__ __forceinline__ int rayInstr(unsigned f) { return (int)((f >> 4) & 63u); }
+__device__ __forceinline__ int rayLevel(unsigned f) { return (int)((f >> 10) & 255u); }
+__device__ __forceinline__ int rayEll(unsigned f) { return (int)(f >> 18); }
+
 struct Args {
     // grid
     int nx, ny, nz, ncells;
-    const double* xv;            // nx+1 | ny+1 | nz+1 concatenated (copied to LDS)
+    const double* mesh;          // Cartesian borders x | y | z (staged in LDS)
     double gx0, gx1, gy0, gy1, gz0, gz1;
     const double* box;           // octree
     const int* firstChild;
@@ -63,10 +85,9 @@ struct Args {
     // media
     int ncomp, nlambda;
     const double* rho;
-    const double* optics;        // [4][ncomp][nlambda]: kext, ksca, albedo, g (copied to LDS)
+    const double* optics;        // [4][ncomp][nlambda]: kext, ksca, albedo, g
     // sources
     int nstar;
-    const int* geomKind;
     const double* geomParam;
     const double* lum;
     const double* lumtot;
@@ -74,8 +95,8 @@ struct Args {
     double emissionBias;
     // instruments
     int ninstr;
-    const DevInstr* instr;       // copied to LDS
-    int nsed;                    // total SED accumulator doubles (LDS)
+    const DevInstr* instr;
+    int nsed;
     // phase
     unsigned long long npp, first, end, seed;
     unsigned int tag;
@@ -85,56 +106,124 @@ struct Args {
     int store, hasDust;
     // tallies
     double* labs;                // [nlambda][ncells]
-    double* tally;               // instrument tallies
-    unsigned long long* counter; // packet claim counter (relative to first)
+    double* tally;
     unsigned int* error;
     unsigned long long* stats;   // packets, seg_fill, seg_walk, seg_peel, detects, absorbs
-    int threshold;
+    // slot pool (structure of arrays) and queues
+    int nslots;
+    double *srx, *sry, *srz, *skx, *sky, *skz, *sL, *sLth;
+    int *sell, *snscatt, *sstellar, *sstate;
+    uint32_t *splo, *sphi, *sblock, *sw2, *sw3, *shave;
+    double *resA, *resB;         // per slot: FILL -> tau, Lsca | WALK -> distance
+    RayRec* rays;
+    int* act[2];                 // active slot lists (double buffered)
+    unsigned long long* claim;   // next packet index (relative to first)
+    unsigned int* ctr;           // [0,1] ray counts, [2,3] active counts, [4] trace pull counter
+    int parity, init, threshold;
     int ldsMeshOff, ldsOptOff, ldsInstrOff, ldsSedOff;  // in doubles
 };
 
-enum RayMode : int { RAY_NONE = 0, RAY_PEEL = 1, RAY_FILL = 2, RAY_WALK = 3 };
-enum State : int { S_NEW = 0, S_PEEL = 1, S_FILL = 2, S_WALK = 3, S_DONE = 4 };
-
-__device__ inline void atomicAddF64(double* p, double v) {
+__device__ __forceinline__ void atomicAddF64(double* p, double v) {
     // explicit global address space: global_atomic_add_f64 instead of a flat atomic
     __hip_atomic_fetch_add((__attribute__((address_space(1))) double*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// ------------------------------------------------------------------ per-lane photon slot
-struct Slot {
-    // photon package (PhotonPackage.hpp: _L, _ell, _nscatt, _stellar, _bfr, _bfk)
-    double rx, ry, rz, kx, ky, kz, L, Lthreshold;
-    int ell, nscatt, stellar, state;
-    int peelScatter, instr;  // peel-off bookkeeping
-    // current ray
-    double x, y, z, dx, dy, dz;
-    double tau, s, target;
-    double ptau, ps, ptau2, ps2;  // WALK history (last two segment ends)
-    double Lsca;                  // FILL with several dust components
-    double bx0, by0, bz0, bx1, by1, bz1;  // octree: box of the current node
-    int ci, cj, ck;               // Cartesian cell indices / octree node in ci
-    int nseg, mode;
-    PacketRng rng;
-    // statistics
-    unsigned int segFill, segWalk, segPeel, detects, absorbs, packets;
+// the small tables staged in LDS
+struct Shared {
+    const double* mesh;
+    const double* kext;   // [ncomp][nlambda]
+    const double* ksca;
+    const double* alb;
+    const double* g;
+    const DevInstr* instr;
+    double* sed;
 };
 
-// ------------------------------------------------------------------ grid access helpers
+__device__ __forceinline__ Shared stageTables(const Args& a, double* lds, bool mesh) {
+    Shared sh;
+    double* m = lds + a.ldsMeshOff;
+    double* opt = lds + a.ldsOptOff;
+    double* idst = lds + a.ldsInstrOff;
+    sh.mesh = m;
+    sh.kext = opt;
+    sh.ksca = opt + a.ncomp * a.nlambda;
+    sh.alb = opt + 2 * a.ncomp * a.nlambda;
+    sh.g = opt + 3 * a.ncomp * a.nlambda;
+    sh.instr = reinterpret_cast<const DevInstr*>(idst);
+    sh.sed = lds + a.ldsSedOff;
+    const int nmesh = mesh ? (a.nx + a.ny + a.nz + 3) : 0;
+    for (int q = threadIdx.x; q < nmesh; q += blockDim.x) m[q] = a.mesh[q];
+    const int nopt = 4 * a.ncomp * a.nlambda;
+    for (int q = threadIdx.x; q < nopt; q += blockDim.x) opt[q] = a.optics[q];
+    const int ninw = a.ninstr * (int)(sizeof(DevInstr) / sizeof(double));
+    const double* isrc = reinterpret_cast<const double*>(a.instr);
+    for (int q = threadIdx.x; q < ninw; q += blockDim.x) idst[q] = isrc[q];
+    __syncthreads();
+    return sh;
+}
+
+__device__ __forceinline__ void flushStats(const Args& a, const unsigned long long (&vals)[6]) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int q = 0; q < 6; q++) {
+        unsigned long long v = vals[q];
+        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+        if (lane == 0 && v) atomicAdd(a.stats + q, v);
+    }
+}
+
+// ------------------------------------------------------------------ the ray (trace kernel registers)
+struct Ray {
+    double x, y, z;        // current position along the ray
+    double dx, dy, dz;     // direction
+    double ix, iy, iz;     // 1/direction (0 where |k| <= 1e-15: that axis is never crossed)
+    double tau, s;         // optical depth and path length covered so far
+    double kext;           // kappa_ext at the ray's wavelength (one dust component)
+    double param;          // see RayRec::param
+    double f1, f2;         // FILL: exp(-tau), Lsca | WALK: tau and s at the previous segment end
+    double bx0, by0, bz0, bx1, by1, bz1;  // octree: box of the current node
+    int ci, cj, ck;        // Cartesian cell indices | octree node in ci
+    int idx, ell;
+    unsigned flags, mode;
+};
+
+// ------------------------------------------------------------------ grids
 template <int GRID>
 struct Grid;
 
 // Cartesian grid: CartesianDustGrid.cpp:136-283 (mesh borders staged in LDS)
 template <>
 struct Grid<SKIRT_GRID_CARTESIAN> {
-    // returns false for an empty path; appends the up-to-three m=-1 entry segments through `seg`
+    __device__ static __forceinline__ int locateClip(const double* v, int n, double q) {  // NR::locate_clip
+        if (q < v[0]) return 0;
+        int jl = -1, ju = n - 1;
+        while (ju - jl > 1) {
+            const int jm = (ju + jl) >> 1;
+            if (q < v[jm]) ju = jm;
+            else jl = jm;
+        }
+        return jl;
+    }
+    __device__ static __forceinline__ int locateFail(const double* v, int n, double q) {  // NR::locate_fail
+        if (q > v[n - 1]) return -1;
+        int jl = -1, ju = n - 1;
+        while (ju - jl > 1) {
+            const int jm = (ju + jl) >> 1;
+            if (q < v[jm]) ju = jm;
+            else jl = jm;
+        }
+        return jl;
+    }
+
+    // the entry part of the path: up to three segments outside the grid (m = -1), then the first cell;
+    // false for an empty path
     template <class SegFn>
-    __device__ static inline bool begin(const Args& a, const double* __restrict__ mesh, Slot& sl, SegFn seg) {
-        const double* xv = mesh;
-        const double* yv = mesh + a.nx + 1;
+    __device__ static __forceinline__ bool begin(const Args& a, const Shared& sh, Ray& r, SegFn seg) {
+        const double* xv = sh.mesh;
+        const double* yv = xv + a.nx + 1;
         const double* zv = yv + a.ny + 1;
-        double kx = sl.dx, ky = sl.dy, kz = sl.dz, x = sl.x, y = sl.y, z = sl.z;
-        double d0 = 0, d1 = 0, d2 = 0;  // pending outside segments
+        const double kx = r.dx, ky = r.dy, kz = r.dz;
+        double x = r.x, y = r.y, z = r.z, d0 = 0, d1 = 0, d2 = 0;
         if (x < a.gx0) {
             if (kx <= 0.0) return false;
             d0 = (a.gx0 - x) / kx;
@@ -166,109 +255,85 @@ struct Grid<SKIRT_GRID_CARTESIAN> {
         if (d0 > 0) seg(-1, d0);
         if (d1 > 0) seg(-1, d1);
         if (d2 > 0) seg(-1, d2);
-        sl.x = x; sl.y = y; sl.z = z;
-        sl.ci = locateClip(xv, a.nx + 1, x);
-        sl.cj = locateClip(yv, a.ny + 1, y);
-        sl.ck = locateClip(zv, a.nz + 1, z);
+        r.x = x; r.y = y; r.z = z;
+        r.ci = locateClip(xv, a.nx + 1, x);
+        r.cj = locateClip(yv, a.ny + 1, y);
+        r.ck = locateClip(zv, a.nz + 1, z);
         return true;
     }
 
-    __device__ static inline int locateClip(const double* v, int n, double q) {  // NR::locate_clip
-        if (q < v[0]) return 0;
-        int jl = -1, ju = n - 1;
-        while (ju - jl > 1) {
-            int jm = (ju + jl) >> 1;
-            if (q < v[jm]) ju = jm;
-            else jl = jm;
-        }
-        return jl;
-    }
-
-    // one DDA step: emits (m, ds) through `seg`; returns false when the ray left the grid
+    // one grid step: emits (m, ds); false when the ray ends (left the grid or stopped by seg)
     template <class SegFn>
-    __device__ static inline bool step(const Args& a, const double* __restrict__ mesh, Slot& sl, SegFn seg) {
-        const double* xv = mesh;
-        const double* yv = mesh + a.nx + 1;
+    __device__ static __forceinline__ bool step(const Args& a, const Shared& sh, Ray& r, SegFn seg) {
+        const double* xv = sh.mesh;
+        const double* yv = xv + a.nx + 1;
         const double* zv = yv + a.ny + 1;
-        const double kx = sl.dx, ky = sl.dy, kz = sl.dz;
-        const int i = sl.ci, j = sl.cj, k = sl.ck;
+        const int i = r.ci, j = r.cj, k = r.ck;
         const int m = k + a.nz * j + a.nz * a.ny * i;
-        const double xE = (kx < 0.0) ? xv[i] : xv[i + 1];
-        const double yE = (ky < 0.0) ? yv[j] : yv[j + 1];
-        const double zE = (kz < 0.0) ? zv[k] : zv[k + 1];
-        const double dsx = (fabs(kx) > 1e-15) ? (xE - sl.x) / kx : kDblMax;
-        const double dsy = (fabs(ky) > 1e-15) ? (yE - sl.y) / ky : kDblMax;
-        const double dsz = (fabs(kz) > 1e-15) ? (zE - sl.z) / kz : kDblMax;
+        const double xE = (r.dx < 0.0) ? xv[i] : xv[i + 1];
+        const double yE = (r.dy < 0.0) ? yv[j] : yv[j + 1];
+        const double zE = (r.dz < 0.0) ? zv[k] : zv[k + 1];
+        const double dsx = (r.ix != 0.0) ? (xE - r.x) * r.ix : kDblMax;
+        const double dsy = (r.iy != 0.0) ? (yE - r.y) * r.iy : kDblMax;
+        const double dsz = (r.iz != 0.0) ? (zE - r.z) * r.iz : kDblMax;
         if (dsx <= dsy && dsx <= dsz) {
             if (!seg(m, dsx)) return false;
-            const int ni = i + ((kx < 0.0) ? -1 : 1);
+            const int ni = i + ((r.dx < 0.0) ? -1 : 1);
             if (ni >= a.nx || ni < 0) return false;
-            sl.ci = ni; sl.x = xE; sl.y += ky * dsx; sl.z += kz * dsx;
+            r.ci = ni; r.x = xE; r.y += r.dy * dsx; r.z += r.dz * dsx;
         } else if (dsy < dsx && dsy <= dsz) {
             if (!seg(m, dsy)) return false;
-            const int nj = j + ((ky < 0.0) ? -1 : 1);
+            const int nj = j + ((r.dy < 0.0) ? -1 : 1);
             if (nj >= a.ny || nj < 0) return false;
-            sl.cj = nj; sl.x += kx * dsy; sl.y = yE; sl.z += kz * dsy;
+            r.cj = nj; r.x += r.dx * dsy; r.y = yE; r.z += r.dz * dsy;
         } else if (dsz < dsx && dsz < dsy) {
             if (!seg(m, dsz)) return false;
-            const int nk = k + ((kz < 0.0) ? -1 : 1);
+            const int nk = k + ((r.dz < 0.0) ? -1 : 1);
             if (nk >= a.nz || nk < 0) return false;
-            sl.ck = nk; sl.x += kx * dsz; sl.y += ky * dsz; sl.z = zE;
+            r.ck = nk; r.x += r.dx * dsz; r.y += r.dy * dsz; r.z = zE;
         } else {
             return false;  // NaN direction; the reference would loop forever
         }
         return true;
     }
 
-    __device__ static inline int whichcell(const Args& a, const double* __restrict__ mesh, double x, double y, double z) {
-        const double* xv = mesh;
-        const double* yv = mesh + a.nx + 1;
+    __device__ static __forceinline__ int whichcell(const Args& a, const Shared& sh, double x, double y, double z) {
+        const double* xv = sh.mesh;
+        const double* yv = xv + a.nx + 1;
         const double* zv = yv + a.ny + 1;
-        int i = locateFail(xv, a.nx + 1, x), j = locateFail(yv, a.ny + 1, y), k = locateFail(zv, a.nz + 1, z);
+        const int i = locateFail(xv, a.nx + 1, x), j = locateFail(yv, a.ny + 1, y), k = locateFail(zv, a.nz + 1, z);
         if (i < 0 || j < 0 || k < 0) return -1;
         return k + a.nz * j + a.nz * a.ny * i;
-    }
-    __device__ static inline int locateFail(const double* v, int n, double q) {
-        if (q > v[n - 1]) return -1;
-        int jl = -1, ju = n - 1;
-        while (ju - jl > 1) {
-            int jm = (ju + jl) >> 1;
-            if (q < v[jm]) ju = jm;
-            else jl = jm;
-        }
-        return jl;
     }
 };
 
 // Octree grid: TreeDustGrid.cpp:390-521 (TopDown and Neighbor search), DustGridPath::moveInside
 template <>
 struct Grid<SKIRT_GRID_OCTREE> {
-    __device__ static inline void loadBox(const Args& a, int l, double& x0, double& y0, double& z0, double& x1,
-                                          double& y1, double& z1) {
+    __device__ static __forceinline__ void loadBox(const Args& a, int l, double& x0, double& y0, double& z0,
+                                                   double& x1, double& y1, double& z1) {
         const double2* b = reinterpret_cast<const double2*>(a.box + 6 * (size_t)l);
-        double2 p = b[0], q = b[1], r = b[2];
-        x0 = p.x; y0 = p.y; z0 = q.x; x1 = q.y; y1 = r.x; z1 = r.y;
+        const double2 p = b[0], q = b[1], w = b[2];
+        x0 = p.x; y0 = p.y; z0 = q.x; x1 = q.y; y1 = w.x; z1 = w.y;
     }
 
-    // TreeNode::whichnode from the root: returns the leaf node containing (x,y,z) or -1
-    __device__ static inline int rootWhichnode(const Args& a, double x, double y, double z, Slot& sl) {
+    // TreeNode::whichnode from the root + OctTreeNode::child(r): the leaf containing (x,y,z) or -1
+    __device__ static __forceinline__ int descend(const Args& a, double x, double y, double z) {
         if (!(x >= a.gx0 && x <= a.gx1 && y >= a.gy0 && y <= a.gy1 && z >= a.gz0 && z <= a.gz1)) return -1;
         int l = 0;
         int c0 = a.firstChild[0];
         while (c0 >= 0) {
-            // OctTreeNode::child(r): split point = rmax of child 0
-            const double* cb = a.box + 6 * (size_t)c0;
-            l = c0 + (x < cb[3] ? 0 : 1) + (y < cb[4] ? 0 : 2) + (z < cb[5] ? 0 : 4);
+            const double* cb = a.box + 6 * (size_t)c0 + 3;  // split point = rmax of child 0
+            l = c0 + (x < cb[0] ? 0 : 1) + (y < cb[1] ? 0 : 2) + (z < cb[2] ? 0 : 4);
             c0 = a.firstChild[l];
         }
-        loadBox(a, l, sl.bx0, sl.by0, sl.bz0, sl.bx1, sl.by1, sl.bz1);
         return l;
     }
 
     template <class SegFn>
-    __device__ static inline bool begin(const Args& a, const double* __restrict__, Slot& sl, SegFn seg) {
-        const double kx = sl.dx, ky = sl.dy, kz = sl.dz, eps = a.eps;
-        double rx = sl.x, ry = sl.y, rz = sl.z, d0 = 0, d1 = 0, d2 = 0;
+    __device__ static __forceinline__ bool begin(const Args& a, const Shared&, Ray& r, SegFn seg) {
+        const double kx = r.dx, ky = r.dy, kz = r.dz, eps = a.eps;
+        double rx = r.x, ry = r.y, rz = r.z, d0 = 0, d1 = 0, d2 = 0;
         if (rx <= a.gx0) {
             if (kx <= 0.0) return false;
             d0 = (a.gx0 - rx) / kx; rx = a.gx0 + eps; ry += ky * d0; rz += kz * d0;
@@ -290,37 +355,38 @@ struct Grid<SKIRT_GRID_OCTREE> {
             if (kz >= 0.0) return false;
             d2 = (a.gz1 - rz) / kz; rx += kx * d2; ry += ky * d2; rz = a.gz1 - eps;
         }
-        int node = rootWhichnode(a, rx, ry, rz, sl);
+        const int node = descend(a, rx, ry, rz);
         if (node < 0) return false;
         if (d0 > 0) seg(-1, d0);
         if (d1 > 0) seg(-1, d1);
         if (d2 > 0) seg(-1, d2);
-        sl.x = rx; sl.y = ry; sl.z = rz;
-        sl.ci = node;
+        r.x = rx; r.y = ry; r.z = rz;
+        r.ci = node;
+        loadBox(a, node, r.bx0, r.by0, r.bz0, r.bx1, r.by1, r.bz1);
         return true;
     }
 
     template <class SegFn>
-    __device__ static inline bool step(const Args& a, const double* __restrict__, Slot& sl, SegFn seg) {
-        const double kx = sl.dx, ky = sl.dy, kz = sl.dz;
-        const int node = sl.ci;
-        const double xnext = (kx < 0.0) ? sl.bx0 : sl.bx1;
-        const double ynext = (ky < 0.0) ? sl.by0 : sl.by1;
-        const double znext = (kz < 0.0) ? sl.bz0 : sl.bz1;
-        const double dsx = (fabs(kx) > 1e-15) ? (xnext - sl.x) / kx : kDblMax;
-        const double dsy = (fabs(ky) > 1e-15) ? (ynext - sl.y) / ky : kDblMax;
-        const double dsz = (fabs(kz) > 1e-15) ? (znext - sl.z) / kz : kDblMax;
+    __device__ static __forceinline__ bool step(const Args& a, const Shared&, Ray& r, SegFn seg) {
+        const int node = r.ci;
+        const double xnext = (r.dx < 0.0) ? r.bx0 : r.bx1;
+        const double ynext = (r.dy < 0.0) ? r.by0 : r.by1;
+        const double znext = (r.dz < 0.0) ? r.bz0 : r.bz1;
+        const double dsx = (r.ix != 0.0) ? (xnext - r.x) * r.ix : kDblMax;
+        const double dsy = (r.iy != 0.0) ? (ynext - r.y) * r.iy : kDblMax;
+        const double dsz = (r.iz != 0.0) ? (znext - r.z) * r.iz : kDblMax;
         double ds;
         int wall;
-        if (dsx <= dsy && dsx <= dsz) { ds = dsx; wall = (kx < 0.0) ? 0 : 1; }
-        else if (dsy <= dsx && dsy <= dsz) { ds = dsy; wall = (ky < 0.0) ? 2 : 3; }
-        else { ds = dsz; wall = (kz < 0.0) ? 4 : 5; }
+        if (dsx <= dsy && dsx <= dsz) { ds = dsx; wall = (r.dx < 0.0) ? 0 : 1; }
+        else if (dsy <= dsx && dsy <= dsz) { ds = dsy; wall = (r.dy < 0.0) ? 2 : 3; }
+        else { ds = dsz; wall = (r.dz < 0.0) ? 4 : 5; }
         if (!seg(a.cellnumber[node], ds)) return false;
-        double x = sl.x + (ds + a.eps) * kx;
-        double y = sl.y + (ds + a.eps) * ky;
-        double z = sl.z + (ds + a.eps) * kz;
+        double x = r.x + (ds + a.eps) * r.dx;
+        double y = r.y + (ds + a.eps) * r.dy;
+        double z = r.z + (ds + a.eps) * r.dz;
         int next = -1;
         if (a.search == SKIRT_TREE_NEIGHBOR) {
+            // TreeNode::whichnode(wall, r): the first neighbour across the exit wall that contains r
             const int q = 6 * node + wall;
             const int nb = a.nbrOffset[q], ne = a.nbrOffset[q + 1];
             for (int n = nb; n < ne; n++) {
@@ -329,262 +395,345 @@ struct Grid<SKIRT_GRID_OCTREE> {
                 loadBox(a, c, x0, y0, z0, x1, y1, z1);
                 if (x >= x0 && x <= x1 && y >= y0 && y <= y1 && z >= z0 && z <= z1) {
                     next = c;
-                    sl.bx0 = x0; sl.by0 = y0; sl.bz0 = z0; sl.bx1 = x1; sl.by1 = y1; sl.bz1 = z1;
+                    r.bx0 = x0; r.by0 = y0; r.bz0 = z0; r.bx1 = x1; r.by1 = y1; r.bz1 = z1;
                     break;
                 }
             }
         }
-        if (next < 0) next = rootWhichnode(a, x, y, z, sl);
-        if (next == node) {
-            // stuck: advance to the next representable coordinates (TreeDustGrid.cpp:502-519)
-            x = nextafter(x, (kx < 0.0) ? -kDblMax : kDblMax);
-            y = nextafter(y, (ky < 0.0) ? -kDblMax : kDblMax);
-            z = nextafter(z, (kz < 0.0) ? -kDblMax : kDblMax);
-            next = rootWhichnode(a, x, y, z, sl);
-            if (next == node) return false;
+        if (next < 0) {
+            next = descend(a, x, y, z);
+            if (next == node) {
+                // stuck: advance to the next representable coordinates (TreeDustGrid.cpp:502-519)
+                x = nextafter(x, (r.dx < 0.0) ? -kDblMax : kDblMax);
+                y = nextafter(y, (r.dy < 0.0) ? -kDblMax : kDblMax);
+                z = nextafter(z, (r.dz < 0.0) ? -kDblMax : kDblMax);
+                next = descend(a, x, y, z);
+                if (next == node) return false;
+            }
+            if (next >= 0) loadBox(a, next, r.bx0, r.by0, r.bz0, r.bx1, r.by1, r.bz1);
         }
-        sl.x = x; sl.y = y; sl.z = z;
-        sl.ci = next;
+        r.x = x; r.y = y; r.z = z;
+        r.ci = next;
         return next >= 0;
     }
 
-    __device__ static inline int whichcell(const Args& a, const double* __restrict__, double x, double y, double z) {
-        if (!(x >= a.gx0 && x <= a.gx1 && y >= a.gy0 && y <= a.gy1 && z >= a.gz0 && z <= a.gz1)) return -1;
-        int l = 0;
-        int c0 = a.firstChild[0];
-        while (c0 >= 0) {
-            const double* cb = a.box + 6 * (size_t)c0;
-            l = c0 + (x < cb[3] ? 0 : 1) + (y < cb[4] ? 0 : 2) + (z < cb[5] ? 0 : 4);
-            c0 = a.firstChild[l];
-        }
-        return a.cellnumber[l];
+    __device__ static __forceinline__ int whichcell(const Args& a, const Shared&, double x, double y, double z) {
+        const int l = descend(a, x, y, z);
+        return l < 0 ? -1 : a.cellnumber[l];
     }
 };
 
-// ------------------------------------------------------------------ the kernel
+// ================================================================== trace kernel
 template <int GRID, bool ONECOMP>
-__global__ void __launch_bounds__(kBlock) stellarKernel(const Args a) {
-    extern __shared__ __attribute__((aligned(16))) double lds[];
-    double* mesh = lds + a.ldsMeshOff;
-    double* opt = lds + a.ldsOptOff;
-    DevInstr* instr = reinterpret_cast<DevInstr*>(lds + a.ldsInstrOff);
-    double* sedAcc = lds + a.ldsSedOff;
+struct Tracer {
+    const Args& a;
+    const Shared& sh;
+    unsigned int segFill = 0, segWalk = 0, segPeel = 0, detects = 0, absorbs = 0;
 
-    // stage the mesh, the optical tables and the instruments in LDS
-    {
-        const int nmesh = (GRID == SKIRT_GRID_CARTESIAN) ? (a.nx + a.ny + a.nz + 3) : 0;
-        for (int q = threadIdx.x; q < nmesh; q += blockDim.x) mesh[q] = a.xv[q];
-        const int nopt = 4 * a.ncomp * a.nlambda;
-        for (int q = threadIdx.x; q < nopt; q += blockDim.x) opt[q] = a.optics[q];
-        const int ninw = a.ninstr * (int)(sizeof(DevInstr) / sizeof(double));
-        const double* isrc = reinterpret_cast<const double*>(a.instr);
-        double* idst = reinterpret_cast<double*>(instr);
-        for (int q = threadIdx.x; q < ninw; q += blockDim.x) idst[q] = isrc[q];
-        for (int q = threadIdx.x; q < a.nsed; q += blockDim.x) sedAcc[q] = 0.0;
-        __syncthreads();
-    }
-    const double* kextT = opt;
-    const double* kscaT = opt + a.ncomp * a.nlambda;
-    const double* albT = opt + 2 * a.ncomp * a.nlambda;
-    const double* gT = opt + 3 * a.ncomp * a.nlambda;
+    __device__ __forceinline__ double rho(int m, int h) const { return a.rho[(size_t)m * a.ncomp + h]; }
 
-    const int lane = threadIdx.x & 63;
-    Slot sl;
-    sl.state = S_NEW;
-    sl.mode = RAY_NONE;
-    sl.segFill = sl.segWalk = sl.segPeel = sl.detects = sl.absorbs = sl.packets = 0;
-    const unsigned long long total = a.end - a.first;
-
-    // kappa*rho summed over components (DustSystem.cpp:465-491 KappaRho)
-    auto kapparho = [&](int m, int ell) __attribute__((always_inline)) -> double {
-        if (m < 0) return 0.0;
-        if (ONECOMP) return 0.0 + kextT[ell] * a.rho[m];
-        double r = 0;
-        for (int h = 0; h < a.ncomp; h++) r += kextT[h * a.nlambda + ell] * a.rho[(size_t)m * a.ncomp + h];
-        return r;
-    };
-
-    // per-segment work of the three ray kinds; returns false to stop the ray (WALK found its point)
-    auto segment = [&](int m, double ds) __attribute__((always_inline)) -> bool {
+    // per-segment work; false stops the ray (a WALK reached its optical depth)
+    __device__ __forceinline__ bool segment(Ray& r, int m, double ds) {
         if (!(ds > 0)) return true;  // DustGridPath::addSegment skips ds <= 0
-        sl.s += ds;
-        sl.nseg++;
-        const double dtau = kapparho(m, sl.ell) * ds;
-        const double taustart = sl.tau;
-        sl.tau = taustart + dtau;
-        if (sl.mode == RAY_FILL) {
-            sl.segFill++;
-            if (m != -1) {
-                if (ONECOMP) {
-                    if (a.store) {
-                        const double expfactorm = -expm1(-dtau);
-                        const double Lintm = sl.L * exp(-taustart) * expfactorm;
-                        const double Labsm = (1.0 - albT[sl.ell]) * Lintm;
-                        atomicAddF64(a.labs + (size_t)sl.ell * a.ncells + m, Labsm);
-                        sl.absorbs++;
-                    }
-                } else {
+        r.s += ds;
+        double kr = 0.0;  // KappaRho functor (DustSystem.cpp:465-491)
+        if (m >= 0) {
+            if (ONECOMP) kr = r.kext * a.rho[m];
+            else for (int h = 0; h < a.ncomp; h++) kr += sh.kext[h * a.nlambda + r.ell] * rho(m, h);
+        }
+        const double dtau = kr * ds;
+        r.tau += dtau;
+        if (r.mode == RAY_FILL) {
+            segFill++;
+            if (m >= 0 && (!ONECOMP || a.store)) {
+                // L_abs = (1-albedo) L exp(-tau_{n-1}) (1 - exp(-dtau_n)); exp(-tau_{n-1}) is carried in f1
+                const double ef = -expm1(-dtau);
+                const double Lintm = r.param * r.f1 * ef;
+                r.f1 = r.f1 * (1.0 - ef);
+                double albedo;
+                if (ONECOMP) albedo = sh.alb[r.ell];
+                else {
                     double ksca = 0.0, kext = 0.0;
                     for (int h = 0; h < a.ncomp; h++) {
-                        const double rho = a.rho[(size_t)m * a.ncomp + h];
-                        ksca += rho * kscaT[h * a.nlambda + sl.ell];
-                        kext += rho * kextT[h * a.nlambda + sl.ell];
+                        ksca += rho(m, h) * sh.ksca[h * a.nlambda + r.ell];
+                        kext += rho(m, h) * sh.kext[h * a.nlambda + r.ell];
                     }
-                    const double albedo = (kext > 0.0) ? ksca / kext : 0.0;
-                    const double expfactorm = -expm1(-dtau);
-                    const double Lintm = sl.L * exp(-taustart) * expfactorm;
-                    sl.Lsca += albedo * Lintm;
-                    if (a.store) {
-                        atomicAddF64(a.labs + (size_t)sl.ell * a.ncells + m, (1.0 - albedo) * Lintm);
-                        sl.absorbs++;
-                    }
+                    albedo = (kext > 0.0) ? ksca / kext : 0.0;
+                    r.f2 += albedo * Lintm;
+                }
+                if (a.store) {
+                    atomicAddF64(a.labs + (size_t)r.ell * a.ncells + m, (1.0 - albedo) * Lintm);
+                    absorbs++;
                 }
             }
-        } else if (sl.mode == RAY_WALK) {
-            sl.segWalk++;
-            if (sl.tau > sl.target) return false;  // interaction point lies in this segment
-            sl.ptau2 = sl.ptau; sl.ps2 = sl.ps;
-            sl.ptau = sl.tau; sl.ps = sl.s;
+        } else if (r.mode == RAY_WALK) {
+            segWalk++;
+            if (r.tau > r.param) return false;  // the interaction point lies in this segment
+            r.f1 = r.tau;
+            r.f2 = r.s;
         } else {
-            sl.segPeel++;
+            segPeel++;
         }
         return true;
-    };
+    }
 
-    // starts a ray from the packet position; returns false if the path is empty
-    auto startRay = [&](int mode, double dx, double dy, double dz) __attribute__((always_inline)) -> bool {
-        sl.mode = mode;
-        sl.x = sl.rx; sl.y = sl.ry; sl.z = sl.rz;
-        sl.dx = dx; sl.dy = dy; sl.dz = dz;
-        sl.tau = 0; sl.s = 0; sl.nseg = 0;
-        sl.ptau = 0; sl.ps = 0; sl.ptau2 = 0; sl.ps2 = 0;
-        sl.Lsca = 0;
-        bool ok = Grid<GRID>::begin(a, mesh, sl, segment);
-        if (!ok) { sl.mode = RAY_NONE; sl.tau = 0; sl.s = 0; sl.nseg = 0; sl.ptau = sl.ps = sl.ptau2 = sl.ps2 = 0; }
-        return ok;
-    };
+    // load a queued ray and walk its entry part; false for an empty path
+    __device__ __forceinline__ bool start(Ray& r, const RayRec& q) {
+        r.x = q.x; r.y = q.y; r.z = q.z;
+        r.dx = q.dx; r.dy = q.dy; r.dz = q.dz;
+        r.param = q.param;
+        r.idx = q.idx;
+        r.flags = q.flags;
+        r.mode = rayMode(q.flags);
+        r.ell = rayEll(q.flags);
+        r.ix = (fabs(r.dx) > 1e-15) ? 1.0 / r.dx : 0.0;
+        r.iy = (fabs(r.dy) > 1e-15) ? 1.0 / r.dy : 0.0;
+        r.iz = (fabs(r.dz) > 1e-15) ? 1.0 / r.dz : 0.0;
+        r.tau = 0; r.s = 0;
+        r.kext = sh.kext[r.ell];
+        r.f1 = (r.mode == RAY_FILL) ? 1.0 : 0.0;
+        r.f2 = 0;
+        return Grid<GRID>::begin(a, sh, r, [&](int m, double ds) { return segment(r, m, ds); });
+    }
 
-    // Instrument::detect (FullInstrument.cpp:107-174, Simple/SED/Frame variants)
-    auto detect = [&](const DevInstr& ins, double Lp, int nscatt, double taupath) __attribute__((always_inline)) {
-        int l = -1;
-        if (ins.kind != SKIRT_INSTR_SED) {
-            const double x = sl.rx, y = sl.ry, z = sl.rz;
-            const double xpp = -ins.sinphi * x + ins.cosphi * y;
-            const double ypp = -ins.cosphi * ins.costheta * x - ins.sinphi * ins.costheta * y + ins.sintheta * z;
-            const double xp = ins.cospa * xpp - ins.sinpa * ypp;
-            const double yp = ins.sinpa * xpp + ins.cospa * ypp;
-            const int i = static_cast<int>(floor((xp - ins.xpmin) / ins.xpsiz));
-            const int j = static_cast<int>(floor((yp - ins.ypmin) / ins.ypsiz));
-            l = (i < 0 || i >= ins.nx || j < 0 || j >= ins.ny) ? -1 : i + ins.nx * j;
+    // the ray ended (grid edge, empty path or WALK target reached): deliver its result
+    __device__ __forceinline__ void finish(const Ray& r) {
+        if (r.mode == RAY_PEEL) {
+            // Instrument::detect (FullInstrument.cpp:107-174 and the Simple/SED/Frame variants)
+            const DevInstr& ins = sh.instr[rayInstr(r.flags)];
+            const double Lp = r.param;
+            const double Lextf = Lp * exp(-r.tau);
+            const int l = r.idx;
+            const int nl = a.nlambda;
+            const long long nframe = (long long)ins.nx * ins.ny;
+            detects++;
+            auto add = [&](int slot, double v) {
+                if (ins.kind != SKIRT_INSTR_FRAME) atomicAdd(&sh.sed[ins.sedOff + slot * nl + r.ell], v);
+                if (l >= 0 && ins.kind != SKIRT_INSTR_SED)
+                    atomicAddF64(a.tally + ins.frameBase + ((long long)slot * nl + r.ell) * nframe + l, v);
+            };
+            if (ins.kind != SKIRT_INSTR_FULL) { add(0, Lextf); return; }
+            switch (rayCat(r.flags)) {
+            case CAT_STAR_DIRECT:
+                add(0, Lp);
+                add(1, Lextf);
+                break;
+            case CAT_STAR_SCATTERED: {
+                add(2, Lextf);
+                const int lev = rayLevel(r.flags);
+                if (lev >= 1 && lev <= ins.levels) add(5 + lev - 1, Lextf);
+                break;
+            }
+            case CAT_DUST_DIRECT: add(3, Lextf); break;
+            default: add(4, Lextf); break;
+            }
+        } else if (r.mode == RAY_FILL) {
+            a.resA[r.idx] = r.tau;
+            if (!ONECOMP) a.resB[r.idx] = r.f2;
+        } else {
+            // DustGridPath::pathlength: interpolate inside the crossing segment; if the path ended first
+            // (target >= tau of the path), the end of the last segment
+            const double tauint = r.param;
+            double s = 0;
+            if (tauint > 0) {
+                if (r.tau > tauint) s = r.f2 + ((tauint - r.f1) / (r.tau - r.f1)) * (r.s - r.f2);
+                else s = r.f2;
+            }
+            a.resA[r.idx] = s;
         }
-        const double extf = exp(-taupath);
-        const double Lextf = Lp * extf;
+    }
+};
+
+template <int GRID, bool ONECOMP>
+__global__ void __launch_bounds__(kBlock) traceKernel(const Args a) {
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    Shared sh = stageTables(a, lds, GRID == SKIRT_GRID_CARTESIAN);
+    for (int q = threadIdx.x; q < a.nsed; q += blockDim.x) sh.sed[q] = 0.0;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        // reset the counters the next event iteration appends to (nobody else uses them now)
+        a.ctr[1 - a.parity] = 0;  // ray count of the next iteration
+        a.ctr[2 + a.parity] = 0;  // active list just consumed by the event kernel
+    }
+    __syncthreads();
+
+    Tracer<GRID, ONECOMP> T{a, sh};
+    const int lane = threadIdx.x & 63;
+    const unsigned int nrays = a.ctr[a.parity];
+    Ray r;
+    r.mode = RAY_NONE;
+    bool done = false;
+    while (true) {
+        const bool idle = (r.mode == RAY_NONE) && !done;
+        const unsigned long long imask = __ballot(idle);
+        const unsigned long long amask = __ballot(r.mode != RAY_NONE);
+        if (imask == 0 && amask == 0) break;
+        if (imask != 0 && (amask == 0 || __popcll(imask) >= a.threshold)) {
+            // idle lanes pull consecutive rays from the queue with one atomic per wave
+            const int leader = __ffsll((long long)imask) - 1;
+            unsigned int base = 0;
+            if (lane == leader) base = atomicAdd(a.ctr + 4, (unsigned int)__popcll(imask));
+            base = __shfl(base, leader);
+            if (idle) {
+                const unsigned int id = base + (unsigned int)__popcll(imask & ((1ull << lane) - 1ull));
+                if (id >= nrays) done = true;
+                else {
+                    const double2* src = reinterpret_cast<const double2*>(a.rays + id);
+                    const double2 p0 = src[0], p1 = src[1], p2 = src[2], p3 = src[3];
+                    RayRec q;
+                    q.x = p0.x; q.y = p0.y; q.z = p1.x; q.dx = p1.y; q.dy = p2.x; q.dz = p2.y; q.param = p3.x;
+                    int2 tail;
+                    memcpy(&tail, &p3.y, 8);
+                    q.idx = tail.x;
+                    q.flags = (unsigned)tail.y;
+                    if (!T.start(r, q)) { T.finish(r); r.mode = RAY_NONE; }
+                }
+            }
+        }
+#pragma unroll 1
+        for (int it = 0; it < 4; it++) {
+            if (r.mode != RAY_NONE) {
+                if (!Grid<GRID>::step(a, sh, r, [&](int m, double ds) { return T.segment(r, m, ds); })) {
+                    T.finish(r);
+                    r.mode = RAY_NONE;
+                }
+            }
+        }
+    }
+    // flush the per-workgroup SED sums and the statistics
+    __syncthreads();
+    for (int q = threadIdx.x; q < a.nsed; q += blockDim.x) {
+        const double v = sh.sed[q];
+        if (v != 0.0) {
+            int ii = 0;
+            while (ii + 1 < a.ninstr && sh.instr[ii + 1].sedOff <= q) ii++;
+            atomicAddF64(a.tally + sh.instr[ii].sedBase + (q - sh.instr[ii].sedOff), v);
+        }
+    }
+    const unsigned long long vals[6] = {0, T.segFill, T.segWalk, T.segPeel, T.detects, T.absorbs};
+    flushStats(a, vals);
+}
+
+// ================================================================== event kernel
+struct Packet {
+    double rx, ry, rz, kx, ky, kz, L, Lth;
+    int ell, nscatt, stellar, state;
+    PacketRng rng;
+};
+
+template <int GRID, bool ONECOMP>
+struct Events {
+    const Args& a;
+    const Shared& sh;
+    unsigned int packets = 0, detects = 0;
+
+    __device__ __forceinline__ double rho(int m, int h) const { return a.rho[(size_t)m * a.ncomp + h]; }
+
+    __device__ __forceinline__ void load(int s, Packet& p) const {
+        p.rx = a.srx[s]; p.ry = a.sry[s]; p.rz = a.srz[s];
+        p.kx = a.skx[s]; p.ky = a.sky[s]; p.kz = a.skz[s];
+        p.L = a.sL[s]; p.Lth = a.sLth[s];
+        p.ell = a.sell[s]; p.nscatt = a.snscatt[s]; p.stellar = a.sstellar[s]; p.state = a.sstate[s];
+        p.rng.k0 = (uint32_t)a.seed; p.rng.k1 = (uint32_t)(a.seed >> 32); p.rng.tag = a.tag;
+        p.rng.plo = a.splo[s]; p.rng.phi = a.sphi[s]; p.rng.block = a.sblock[s];
+        p.rng.w2 = a.sw2[s]; p.rng.w3 = a.sw3[s]; p.rng.have = a.shave[s];
+    }
+    __device__ __forceinline__ void store(int s, const Packet& p) const {
+        a.srx[s] = p.rx; a.sry[s] = p.ry; a.srz[s] = p.rz;
+        a.skx[s] = p.kx; a.sky[s] = p.ky; a.skz[s] = p.kz;
+        a.sL[s] = p.L; a.sLth[s] = p.Lth;
+        a.sell[s] = p.ell; a.snscatt[s] = p.nscatt; a.sstellar[s] = p.stellar; a.sstate[s] = p.state;
+        a.splo[s] = p.rng.plo; a.sphi[s] = p.rng.phi; a.sblock[s] = p.rng.block;
+        a.sw2[s] = p.rng.w2; a.sw3[s] = p.rng.w3; a.shave[s] = p.rng.have;
+    }
+
+    __device__ __forceinline__ int pixel(const DevInstr& ins, const Packet& p) const {
+        // SingleFrameInstrument::pixelondetector (SingleFrameInstrument.cpp:130-147)
+        const double xpp = -ins.sinphi * p.rx + ins.cosphi * p.ry;
+        const double ypp = -ins.cosphi * ins.costheta * p.rx - ins.sinphi * ins.costheta * p.ry + ins.sintheta * p.rz;
+        const double xp = ins.cospa * xpp - ins.sinpa * ypp;
+        const double yp = ins.sinpa * xpp + ins.cospa * ypp;
+        const int i = static_cast<int>(floor((xp - ins.xpmin) / ins.xpsiz));
+        const int j = static_cast<int>(floor((yp - ins.ypmin) / ins.ypsiz));
+        return (i < 0 || i >= ins.nx || j < 0 || j >= ins.ny) ? -1 : i + ins.nx * j;
+    }
+
+    // weight of the scattering peel-off towards instrument `ins` (MonteCarloSimulation.cpp:319-363,
+    // unpolarized; Henyey-Greenstein value DustMix.cpp:665-669); false aborts the peel-off
+    __device__ __forceinline__ bool peelWeight(const DevInstr& ins, const Packet& p, double kx, double ky, double kz,
+                                               double& I) const {
+        const double cosalpha = kx * ins.kobs[0] + ky * ins.kobs[1] + kz * ins.kobs[2];
+        if (ONECOMP) {
+            const double g = sh.g[p.ell];
+            const double t = 1.0 + g * g - 2 * g * cosalpha;
+            I = 0.0 + (1.0 * ((1.0 - g) * (1.0 + g) / sqrt(t * t * t))) * 1.0;
+            return true;
+        }
+        const int m = Grid<GRID>::whichcell(a, sh, p.rx, p.ry, p.rz);
+        if (m == -1) return false;
+        double sum = 0;
+        for (int h = 0; h < a.ncomp; h++) sum += sh.ksca[h * a.nlambda + p.ell] * rho(m, h);
+        if (sum <= 0) return false;
+        I = 0;
+        for (int h = 0; h < a.ncomp; h++) {
+            const double wv = sh.ksca[h * a.nlambda + p.ell] * rho(m, h) / sum;
+            const double g = sh.g[h * a.nlambda + p.ell];
+            const double t = 1.0 + g * g - 2 * g * cosalpha;
+            I += (wv * ((1.0 - g) * (1.0 + g) / sqrt(t * t * t))) * 1.0;
+        }
+        return true;
+    }
+
+    // Instrument::detect without a dust system (tau = 0): FullInstrument then holds only the
+    // transparent arrays (FullInstrument.cpp:58-60, 115-120)
+    __device__ __forceinline__ void detectNow(const DevInstr& ins, const Packet& p, double Lp, int l) {
         const int nl = a.nlambda;
         const long long nframe = (long long)ins.nx * ins.ny;
-        sl.detects++;
-        auto add = [&](int slot, double v) __attribute__((always_inline)) {
-            if (ins.kind != SKIRT_INSTR_FRAME) atomicAdd(&sedAcc[ins.sedOff + slot * nl + sl.ell], v);
-            if (l >= 0 && ins.kind != SKIRT_INSTR_SED)
-                atomicAddF64(a.tally + ins.frameBase + ((long long)slot * nl + sl.ell) * nframe + l, v);
-        };
-        if (ins.kind != SKIRT_INSTR_FULL) { add(0, Lextf); return; }
-        if (sl.stellar >= 0) {
-            if (nscatt == 0) {
-                add(0, Lp);
-                if (a.hasDust) add(1, Lextf);
-            } else {
-                add(2, Lextf);
-                if (nscatt <= ins.levels) add(5 + nscatt - 1, Lextf);
-            }
-        } else {
-            add(nscatt == 0 ? 3 : 4, Lextf);
-        }
-    };
+        detects++;
+        if (ins.kind != SKIRT_INSTR_FRAME) atomicAddF64(a.tally + ins.sedBase + p.ell, Lp);
+        if (l >= 0 && ins.kind != SKIRT_INSTR_SED) atomicAddF64(a.tally + ins.frameBase + (long long)p.ell * nframe + l, Lp);
+        (void)nl;
+    }
 
-    // component weights of the peel-off phase functions (MonteCarloSimulation.cpp:325-339)
-    auto peelWv = [&](double* wv) __attribute__((always_inline)) {
-        if (ONECOMP) return;
-        const int m = Grid<GRID>::whichcell(a, mesh, sl.rx, sl.ry, sl.rz);
-        double sum = 0;
-        for (int h = 0; h < a.ncomp; h++) wv[h] = kscaT[h * a.nlambda + sl.ell] * a.rho[(size_t)m * a.ncomp + h];
-        for (int h = 0; h < a.ncomp; h++) sum += wv[h];
-        for (int h = 0; h < a.ncomp; h++) wv[h] /= sum;
-    };
+    // Random::direction() (Random.cpp:179-184): theta = acos(2u-1), phi = 2 pi u', evaluated as
+    // cos(theta) = 2u-1, sin(theta) = sqrt(1-cos^2) and sin/cos(2 pi u') = sinpi/cospi(2u') -- the
+    // same values to rounding, without acos or a large-argument reduction. The reference's 1e-8
+    // pole cut-offs in Direction(theta, phi) are never reached by a deviate in (0,1).
+    __device__ __forceinline__ void isotropic(PacketRng& rng, double& x, double& y, double& z) const {
+        const double ct = 2.0 * rng.uniform() - 1.0;
+        const double u = rng.uniform();
+        const double st = sqrt((1.0 - ct) * (1.0 + ct));
+        double sp, cp;
+        sincospi(2.0 * u, &sp, &cp);
+        x = st * cp; y = st * sp; z = ct;
+    }
 
-    // peel-off weight of instrument `ins` for the current scattering (MonteCarloSimulation.cpp:319-363)
-    auto peelWeight = [&](const DevInstr& ins, const double* wv) __attribute__((always_inline)) -> double {
-        double I = 0;
-        for (int h = 0; h < (ONECOMP ? 1 : a.ncomp); h++) {
-            const double cosalpha = sl.kx * ins.kobs[0] + sl.ky * ins.kobs[1] + sl.kz * ins.kobs[2];
-            const double g = gT[h * a.nlambda + sl.ell];
-            const double t = 1.0 + g * g - 2 * g * cosalpha;
-            const double w = (ONECOMP ? 1.0 : wv[h]) * ((1.0 - g) * (1.0 + g) / sqrt(t * t * t));
-            I += w * 1.0;
-        }
-        return I;
-    };
-
-    // starts the next peel-off ray for instruments from sl.instr on; returns true if a ray was started,
-    // false if all remaining instruments were handled (detected without traversal or skipped)
-    auto nextPeel = [&]() __attribute__((always_inline)) -> bool {
-        while (sl.instr < a.ninstr) {
-            const DevInstr& ins = instr[sl.instr];
-            if (ins.kind == SKIRT_INSTR_FRAME) {
-                // FrameInstrument::detect computes tau only for packets that land on the frame
-                const double x = sl.rx, y = sl.ry, z = sl.rz;
-                const double xpp = -ins.sinphi * x + ins.cosphi * y;
-                const double ypp = -ins.cosphi * ins.costheta * x - ins.sinphi * ins.costheta * y + ins.sintheta * z;
-                const double xp = ins.cospa * xpp - ins.sinpa * ypp;
-                const double yp = ins.sinpa * xpp + ins.cospa * ypp;
-                const int i = static_cast<int>(floor((xp - ins.xpmin) / ins.xpsiz));
-                const int j = static_cast<int>(floor((yp - ins.ypmin) / ins.ypsiz));
-                if (i < 0 || i >= ins.nx || j < 0 || j >= ins.ny) { sl.instr++; continue; }
-            }
-            if (a.hasDust && startRay(RAY_PEEL, ins.kobs[0], ins.kobs[1], ins.kobs[2])) return true;
-            // empty path or no dust: tau = 0
-            double wv[8];
-            if (sl.peelScatter) peelWv(wv);
-            const double Lp = sl.peelScatter ? sl.L * peelWeight(ins, wv) : sl.L;
-            detect(ins, Lp, sl.peelScatter ? sl.nscatt + 1 : 0, 0.0);
-            sl.instr++;
-        }
-        return false;
-    };
-
-    // DustMix::scatteringDirectionAndPolarization (HG, DustMix.cpp:609-613) + Random::direction(k, costheta)
-    auto scatter = [&]() __attribute__((always_inline)) {
+    // simulatescattering: DustSystem::randomMixForPosition + DustMix::scatteringDirectionAndPolarization
+    // (HG, DustMix.cpp:609-613) + Random::direction(k, costheta) (Random.cpp:188-222)
+    __device__ __forceinline__ void scatter(Packet& p) const {
         int hmix = 0;
         if (!ONECOMP) {
-            // DustSystem::randomMixForPosition: NR::cdf over kappasca*rho, then NR::locate_clip
-            const int m = Grid<GRID>::whichcell(a, mesh, sl.rx, sl.ry, sl.rz);
+            const int m = Grid<GRID>::whichcell(a, sh, p.rx, p.ry, p.rz);
             if (m >= 0) {
                 double Xv[9];
                 Xv[0] = 0.0;
-                for (int h = 0; h < a.ncomp; h++) Xv[h + 1] = Xv[h] + kscaT[h * a.nlambda + sl.ell] * a.rho[(size_t)m * a.ncomp + h];
+                for (int h = 0; h < a.ncomp; h++) Xv[h + 1] = Xv[h] + sh.ksca[h * a.nlambda + p.ell] * rho(m, h);
                 const double norm = Xv[a.ncomp];
-                for (int h = 0; h <= a.ncomp; h++) Xv[h] /= norm;
-                const double X = sl.rng.uniform();
-                int sel = 0;
+                const double X = p.rng.uniform();
                 for (int h = 1; h < a.ncomp; h++)
-                    if (Xv[h] <= X) sel = h;
-                hmix = sel;
+                    if (Xv[h] / norm <= X) hmix = h;
             }
         }
-        const double g = gT[hmix * a.nlambda + sl.ell];
+        const double g = sh.g[hmix * a.nlambda + p.ell];
         double nx, ny, nz;
         if (fabs(g) < 1e-6) {
-            const double theta = acos(2.0 * sl.rng.uniform() - 1.0);
-            const double phi = 2.0 * M_PI * sl.rng.uniform();
-            if (theta <= 1e-8) { nx = 0; ny = 0; nz = 1; }
-            else if (theta >= M_PI - 1e-8) { nx = 0; ny = 0; nz = -1; }
-            else { const double st = sin(theta); nx = st * cos(phi); ny = st * sin(phi); nz = cos(theta); }
+            isotropic(p.rng, nx, ny, nz);
         } else {
-            const double f = ((1.0 - g) * (1.0 + g)) / (1.0 - g + 2.0 * g * sl.rng.uniform());
+            const double f = ((1.0 - g) * (1.0 + g)) / (1.0 - g + 2.0 * g * p.rng.uniform());
             const double costheta = (1.0 + g * g - f * f) / (2.0 * g);
-            const double phi = 2.0 * M_PI * sl.rng.uniform();
-            const double cosphi = cos(phi), sinphi = sin(phi);
+            double sinphi, cosphi;  // phi = 2 pi u (Random.cpp:190), as sinpi/cospi(2u)
+            sincospi(2.0 * p.rng.uniform(), &sinphi, &cosphi);
             const double sintheta = sqrt(fabs((1.0 - costheta) * (1.0 + costheta)));
-            const double kx = sl.kx, ky = sl.ky, kz = sl.kz;
+            const double kx = p.kx, ky = p.ky, kz = p.kz;
             if (kz > 0.99999) { nx = cosphi * sintheta; ny = sinphi * sintheta; nz = costheta; }
             else if (kz < -0.99999) { nx = cosphi * sintheta; ny = sinphi * sintheta; nz = -costheta; }
             else {
@@ -594,260 +743,247 @@ __global__ void __launch_bounds__(kBlock) stellarKernel(const Args a) {
                 nz = root * sintheta * cosphi + kz * costheta;
             }
         }
-        sl.nscatt++;
-        sl.kx = nx; sl.ky = ny; sl.kz = nz;
-    };
+        p.nscatt++;
+        p.kx = nx; p.ky = ny; p.kz = nz;
+    }
 
-    // after a peel-off round of a scattering event: scatter and start the next FILL ray
-    auto scatterAndFill = [&]() __attribute__((always_inline)) {
-        scatter();
-        sl.state = S_FILL;
-        if (!startRay(RAY_FILL, sl.kx, sl.ky, sl.kz)) sl.mode = RAY_NONE;  // empty path: FILL ends at once
-    };
-
-    // WALK end: propagate and begin the peel-off round of this scattering (or scatter directly)
-    auto propagateAndPeel = [&](double s) __attribute__((always_inline)) {
-        sl.rx = sl.rx + s * sl.kx;
-        sl.ry = sl.ry + s * sl.ky;
-        sl.rz = sl.rz + s * sl.kz;
-        bool ok = a.ninstr > 0;
-        if (ok && !ONECOMP) {
-            const int m = Grid<GRID>::whichcell(a, mesh, sl.rx, sl.ry, sl.rz);
-            if (m == -1) ok = false;
-            else {
-                double sum = 0;
-                for (int h = 0; h < a.ncomp; h++) sum += kscaT[h * a.nlambda + sl.ell] * a.rho[(size_t)m * a.ncomp + h];
-                if (sum <= 0) ok = false;
-            }
-        }
-        if (ok) {
-            sl.state = S_PEEL;
-            sl.peelScatter = 1;
-            sl.instr = 0;
-            if (nextPeel()) return;
-        }
-        scatterAndFill();
-    };
-
-    // ---------------------------------------------------------- event code: one packet transition
-    // Runs for a lane whose ray ended (or that needs a new packet); leaves it with a new ray, or in
-    // S_NEW (packet finished), or S_DONE.
-    auto transition = [&]() __attribute__((always_inline)) {
-        switch (sl.state) {
-        case S_PEEL: {
-            const DevInstr& ins = instr[sl.instr];
-            double Lp = sl.L;
-            if (sl.peelScatter) {
-                double wv[8];
-                peelWv(wv);
-                Lp = sl.L * peelWeight(ins, wv);
-            }
-            detect(ins, Lp, sl.peelScatter ? sl.nscatt + 1 : 0, sl.tau);
-            sl.instr++;
-            if (nextPeel()) return;
-            if (sl.peelScatter) { scatterAndFill(); return; }
-            if (a.hasDust) {
-                sl.state = S_FILL;
-                if (!startRay(RAY_FILL, sl.kx, sl.ky, sl.kz)) sl.mode = RAY_NONE;
-                return;
-            }
-            sl.state = S_NEW;
-            return;
-        }
-        case S_FILL: {
-            // ray finished (or empty): simulateescapeandabsorption + termination + propagation sampling
-            const double taupath = sl.tau;
-            if (taupath < 0.0 || isnan(taupath) || isinf(taupath)) {
-                atomicOr(a.error, 1u);
-                sl.state = S_NEW;
-                return;
-            }
-            if (ONECOMP) {
-                const double albedo = albT[sl.ell];
-                const double expfactor = -expm1(-taupath);
-                sl.L = sl.L * albedo * expfactor;
-            } else {
-                sl.L = sl.Lsca;
-            }
-            if (sl.L <= 0 || (sl.L <= sl.Lthreshold && sl.nscatt >= a.minScatt)) { sl.state = S_NEW; return; }
-            if (taupath == 0.0) { propagateAndPeel(0.0); return; }
-            double tauint;
-            if (a.xi == 0.0) tauint = -1.0;
-            else {
-                const double X = sl.rng.uniform();
-                tauint = (X < a.xi) ? sl.rng.uniform() * taupath : -1.0;
-            }
-            if (tauint < 0.0) {
-                // Random::exponcutoff (Random.cpp:162-175)
-                if (taupath < 1e-10) tauint = sl.rng.uniform() * taupath;
-                else {
-                    double x = -log(1.0 - sl.rng.uniform() * (1.0 - exp(-taupath)));
-                    while (x > taupath) x = -log(1.0 - sl.rng.uniform() * (1.0 - exp(-taupath)));
-                    tauint = x;
-                }
-            }
-            if (a.xi != 0.0) {
-                const double p = -exp(-tauint) / expm1(-taupath);
-                const double q = (1.0 - a.xi) * p + a.xi / taupath;
-                const double weight = p / q;
-                sl.L = sl.L * weight;
-            }
-            sl.state = S_WALK;
-            sl.target = tauint;
-            if (!(tauint > 0) || !startRay(RAY_WALK, sl.kx, sl.ky, sl.kz)) { sl.mode = RAY_NONE; sl.nseg = 0; }
-            return;
-        }
-        case S_WALK: {
-            // DustGridPath::pathlength: the interaction segment was found (ray stopped) or the path ended
-            double s = 0;
-            const double tauint = sl.target;
-            if (sl.nseg > 0 && tauint > 0) {
-                if (sl.tau > tauint) {
-                    s = sl.ps + ((tauint - sl.ptau) / (sl.tau - sl.ptau)) * (sl.s - sl.ps);
-                } else if (sl.ptau < tauint || sl.nseg == 1) {
-                    s = sl.ps;  // last segment end
-                } else {
-                    s = sl.ps2 + ((tauint - sl.ptau2) / (sl.ptau - sl.ptau2)) * (sl.ps - sl.ps2);
-                }
-            }
-            propagateAndPeel(s);
-            return;
-        }
-        default:
-            return;
-        }
-    };
-
-    // launch a new packet: StellarSystem::launch + GeometricStellarComp::launch (Plummer)
-    auto launch = [&](unsigned long long p) __attribute__((always_inline)) {
-        const int ell = (int)(p / a.npp);
+    // StellarSystem::launch + GeometricStellarComp::launch + PlummerGeometry sampling; false when no
+    // packet results (wavelength without luminosity, or a selected component without luminosity)
+    __device__ __forceinline__ bool launch(Packet& p, unsigned long long idx) {
+        const int ell = (int)(idx / a.npp);
         const double L0 = a.lumtot[ell] / (double)a.npp;
-        if (!(L0 > 0)) { sl.state = S_NEW; return; }  // dostellaremissionchunk skips such wavelengths
-        sl.packets++;
-        sl.Lthreshold = L0 / a.minWeightReduction;
-        sl.rng.start(a.seed, a.tag, p);
-        sl.ell = ell;
+        if (!(L0 > 0)) return false;  // dostellaremissionchunk skips such wavelengths
+        packets++;
+        p.Lth = L0 / a.minWeightReduction;
+        p.rng.start(a.seed, a.tag, idx);
+        p.ell = ell;
         int h = 0;
         double L = L0;
         const int N = a.nstar;
         if (N > 1) {
-            const double X = sl.rng.uniform();
+            const double X = p.rng.uniform();
             const double xi = a.emissionBias;
             if (X < xi) h = max(0, min(N - 1, static_cast<int>(N * X / xi)));
             else {
                 const double* Xv = a.cdf + (size_t)ell * (N + 1);
                 const double q = (X - xi) / (1.0 - xi);
-                if (q < Xv[0]) h = 0;
-                else {
+                if (!(q < Xv[0])) {
                     int lo = -1, hi = N;
-                    while (hi - lo > 1) { int jm = (hi + lo) >> 1; if (q < Xv[jm]) hi = jm; else lo = jm; }
+                    while (hi - lo > 1) { const int jm = (hi + lo) >> 1; if (q < Xv[jm]) hi = jm; else lo = jm; }
                     h = lo;
                 }
             }
             const double Lh = a.lum[(size_t)h * a.nlambda + ell];
-            if (Lh > 0) {
-                const double Lmean = a.lumtot[ell] / N;
-                const double weight = 1.0 / (1.0 - xi + xi * Lmean / Lh);
-                L = L0 * weight;
-            } else {
-                sl.state = S_NEW;  // launched with zero luminosity
-                return;
+            if (!(Lh > 0)) return false;
+            const double Lmean = a.lumtot[ell] / N;
+            L = L0 * (1.0 / (1.0 - xi + xi * Lmean / Lh));
+        }
+        // PlummerGeometry::randomradius (t = u^(1/3)) and SpheGeometry::generatePosition, then the
+        // emission direction Random::direction()
+        const double c = a.geomParam[4 * h];
+        const double t = cbrt(p.rng.uniform());
+        const double rr = c * t / sqrt((1.0 - t) * (1.0 + t));
+        double ux, uy, uz;
+        isotropic(p.rng, ux, uy, uz);
+        p.rx = rr * ux; p.ry = rr * uy; p.rz = rr * uz;
+        isotropic(p.rng, p.kx, p.ky, p.kz);
+        p.L = L;
+        p.nscatt = 0;
+        p.stellar = h;
+        return true;
+    }
+
+    // simulatepropagation part 1: the optical depth of the interaction (Random::exponcutoff and the
+    // composite biasing with weight p/q, MonteCarloSimulation.cpp:519-534)
+    __device__ __forceinline__ double sampleTau(Packet& p, double taupath) const {
+        double tauint = -1.0;
+        if (a.xi != 0.0) {
+            const double X = p.rng.uniform();
+            if (X < a.xi) tauint = p.rng.uniform() * taupath;
+        }
+        if (tauint < 0.0) {
+            if (taupath < 1e-10) tauint = p.rng.uniform() * taupath;
+            else {
+                const double norm = 1.0 - exp(-taupath);
+                double x = -log(1.0 - p.rng.uniform() * norm);
+                while (x > taupath) x = -log(1.0 - p.rng.uniform() * norm);
+                tauint = x;
             }
         }
-        const double c = a.geomParam[4 * h];
-        // PlummerGeometry::randomradius, SpheGeometry::generatePosition, Random::direction() twice
-        const double t = pow(sl.rng.uniform(), 1.0 / 3.0);
-        const double r = c * t / sqrt((1.0 - t) * (1.0 + t));
-        double dx, dy, dz;
-        {
-            const double theta = acos(2.0 * sl.rng.uniform() - 1.0);
-            const double phi = 2.0 * M_PI * sl.rng.uniform();
-            if (theta <= 1e-8) { dx = 0; dy = 0; dz = 1; }
-            else if (theta >= M_PI - 1e-8) { dx = 0; dy = 0; dz = -1; }
-            else { const double st = sin(theta); dx = st * cos(phi); dy = st * sin(phi); dz = cos(theta); }
+        if (a.xi != 0.0) {
+            const double pr = -exp(-tauint) / expm1(-taupath);
+            const double q = (1.0 - a.xi) * pr + a.xi / taupath;
+            p.L = p.L * (pr / q);
         }
-        sl.rx = r * dx; sl.ry = r * dy; sl.rz = r * dz;
-        {
-            const double theta = acos(2.0 * sl.rng.uniform() - 1.0);
-            const double phi = 2.0 * M_PI * sl.rng.uniform();
-            if (theta <= 1e-8) { dx = 0; dy = 0; dz = 1; }
-            else if (theta >= M_PI - 1e-8) { dx = 0; dy = 0; dz = -1; }
-            else { const double st = sin(theta); dx = st * cos(phi); dy = st * sin(phi); dz = cos(theta); }
-        }
-        sl.kx = dx; sl.ky = dy; sl.kz = dz;
-        sl.L = L;
-        sl.nscatt = 0;
-        sl.stellar = h;
-        // peeloffemission
-        sl.state = S_PEEL;
-        sl.peelScatter = 0;
-        sl.instr = 0;
-        if (nextPeel()) return;
-        if (a.hasDust) {
-            sl.state = S_FILL;
-            if (!startRay(RAY_FILL, sl.kx, sl.ky, sl.kz)) sl.mode = RAY_NONE;
-            return;
-        }
-        sl.state = S_NEW;
-    };
+        return tauint;
+    }
+};
 
-    // ---------------------------------------------------------- main loop
-    while (true) {
-        const bool waiting = (sl.mode == RAY_NONE) && (sl.state != S_DONE);
-        const unsigned long long wmask = __ballot(waiting);
-        const unsigned long long rmask = __ballot(sl.mode != RAY_NONE);
-        if (wmask == 0 && rmask == 0) break;  // every lane is done
-        if (wmask != 0 && (rmask == 0 || __popcll(wmask) >= a.threshold)) {
-            bool inH = waiting;
-            while (true) {
-                // lanes that need a packet claim consecutive indices with one atomic per wave
-                const bool need = inH && sl.state == S_NEW;
-                const unsigned long long nmask = __ballot(need);
-                if (nmask) {
-                    const int cnt = __popcll(nmask);
-                    const int leader = __ffsll((long long)nmask) - 1;
-                    unsigned long long base = 0;
-                    if (lane == leader) base = atomicAdd(a.counter, (unsigned long long)cnt);
-                    base = __shfl(base, leader);
-                    if (need) {
-                        const unsigned long long rank = __popcll(nmask & ((1ull << lane) - 1ull));
-                        const unsigned long long idx = base + rank;
-                        if (idx >= total) sl.state = S_DONE;
-                        else launch(a.first + idx);
+// peel-off set queued by a slot in this iteration
+enum PeelKind : int { PEEL_NONE = 0, PEEL_EMISSION = 1, PEEL_SCATTER = 2 };
+
+template <int GRID, bool ONECOMP>
+__global__ void __launch_bounds__(kBlock) eventKernel(const Args a) {
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    Shared sh = stageTables(a, lds, GRID == SKIRT_GRID_CARTESIAN);
+    if (blockIdx.x == 0 && threadIdx.x == 0) a.ctr[4] = 0;  // the trace kernel's pull counter
+    Events<GRID, ONECOMP> E{a, sh};
+    const int lane = threadIdx.x & 63;
+    const unsigned long long total = a.end - a.first;
+    const unsigned int nwork = a.init ? (unsigned)a.nslots : a.ctr[2 + a.parity];
+    const int* actIn = a.act[a.parity];
+    int* actOut = a.act[1 - a.parity];
+    const unsigned int stride = gridDim.x * blockDim.x;
+    // every lane of a wave runs the same number of rounds (wave-collective claims and appends below)
+    const unsigned int rounds = (nwork + stride - 1) / stride;
+    for (unsigned int round = 0; round < rounds; round++) {
+        const unsigned int w = round * stride + blockIdx.x * blockDim.x + threadIdx.x;
+        const bool valid = w < nwork;
+        const int slot = valid ? (a.init ? (int)w : actIn[w]) : 0;
+        Packet p;
+        p.state = S_NEW;
+        if (valid && !a.init) E.load(slot, p);
+        int peel = PEEL_NONE;
+        unsigned mainMode = RAY_NONE;
+        double mainParam = 0;
+        double ox = 0, oy = 0, oz = 0;  // direction before scattering (peel-off weights)
+        if (valid && !a.init) {
+            if (p.state == S_FILL) {
+                // end of fillOpticalDepth + simulateescapeandabsorption; termination; simulatepropagation
+                const double taupath = a.resA[slot];
+                if (taupath < 0.0 || isnan(taupath) || isinf(taupath)) {
+                    atomicOr(a.error, 1u);
+                    p.state = S_NEW;
+                } else {
+                    if (ONECOMP) p.L = p.L * sh.alb[p.ell] * (-expm1(-taupath));
+                    else p.L = a.resB[slot];
+                    if (p.L <= 0 || (p.L <= p.Lth && p.nscatt >= a.minScatt)) {
+                        p.state = S_NEW;
+                    } else {
+                        p.state = S_WALK;
+                        double tauint = 0.0;  // taupath == 0: no propagation (MonteCarloSimulation.cpp:522)
+                        if (taupath != 0.0) tauint = E.sampleTau(p, taupath);
+                        if (tauint > 0) { mainMode = RAY_WALK; mainParam = tauint; }
+                        else a.resA[slot] = 0.0;
                     }
                 }
-                if (inH && !need && sl.state != S_DONE && sl.state != S_NEW) transition();
-                inH = inH && sl.state != S_DONE && sl.mode == RAY_NONE;
-                if (!__ballot(inH)) break;
+            }
+            if (p.state == S_WALK && mainMode == RAY_NONE) {
+                // propagate to the interaction point; peel-off round; scatter; next FILL
+                const double s = a.resA[slot];
+                p.rx = p.rx + s * p.kx;
+                p.ry = p.ry + s * p.ky;
+                p.rz = p.rz + s * p.kz;
+                bool ok = a.ninstr > 0;
+                if (ok && !ONECOMP) { double I; ok = E.peelWeight(sh.instr[0], p, p.kx, p.ky, p.kz, I); }
+                if (ok) { peel = PEEL_SCATTER; ox = p.kx; oy = p.ky; oz = p.kz; }
+                E.scatter(p);
+                mainMode = RAY_FILL;
+                mainParam = p.L;
+                p.state = S_FILL;
             }
         }
-        // advance every active ray by a few segments
-#pragma unroll 1
-        for (int it = 0; it < 4; it++) {
-            if (sl.mode != RAY_NONE) {
-                if (!Grid<GRID>::step(a, mesh, sl, segment)) sl.mode = RAY_NONE;
+        // slots without a packet claim the next global packet indices (one atomic per wave)
+        bool need = valid && p.state == S_NEW && mainMode == RAY_NONE;
+        while (__ballot(need)) {
+            const unsigned long long nmask = __ballot(need);
+            const int leader = __ffsll((long long)nmask) - 1;
+            unsigned long long base = 0;
+            if (lane == leader) base = atomicAdd(a.claim, (unsigned long long)__popcll(nmask));
+            base = __shfl(base, leader);
+            if (need) {
+                const unsigned long long idx = base + __popcll(nmask & ((1ull << lane) - 1ull));
+                if (idx >= total) need = false;  // exhausted: the slot retires
+                else if (E.launch(p, a.first + idx)) {
+                    if (a.hasDust) {
+                        peel = a.ninstr > 0 ? PEEL_EMISSION : PEEL_NONE;
+                        mainMode = RAY_FILL;
+                        mainParam = p.L;
+                        p.state = S_FILL;
+                        need = false;
+                    } else {
+                        // no dust system: tau = 0 for every peel-off and the packet ends here
+                        for (int i = 0; i < a.ninstr; i++) {
+                            const DevInstr& ins = sh.instr[i];
+                            const int l = ins.kind == SKIRT_INSTR_SED ? -1 : E.pixel(ins, p);
+                            if (ins.kind == SKIRT_INSTR_FRAME && l < 0) continue;
+                            E.detectNow(ins, p, p.L, l);
+                        }
+                    }
+                }
             }
         }
-    }
-
-    // flush per-workgroup SED accumulators and statistics
-    __syncthreads();
-    for (int q = threadIdx.x; q < a.nsed; q += blockDim.x) {
-        const double v = sedAcc[q];
-        if (v != 0.0) {
-            // map the LDS accumulator index back to the global SED tally
-            int ii = 0;
-            while (ii + 1 < a.ninstr && instr[ii + 1].sedOff <= q) ii++;
-            atomicAddF64(a.tally + instr[ii].sedBase + (q - instr[ii].sedOff), v);
+        // rays this lane queues: its peel-offs and its next FILL/WALK ray
+        int nray = 0;
+        if (peel != PEEL_NONE) {
+            for (int i = 0; i < a.ninstr; i++) {
+                const DevInstr& ins = sh.instr[i];
+                if (ins.kind == SKIRT_INSTR_FRAME && E.pixel(ins, p) < 0) continue;
+                nray++;
+            }
         }
-    }
-    unsigned long long vals[6] = {sl.packets, sl.segFill, sl.segWalk, sl.segPeel, sl.detects, sl.absorbs};
+        if (mainMode != RAY_NONE) nray++;
+        // wave-wide inclusive scan of nray; one atomic per wave reserves the queue space
+        int incl = nray;
 #pragma unroll
-    for (int q = 0; q < 6; q++) {
-        unsigned long long v = vals[q];
-        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
-        if (lane == 0 && v) atomicAdd(a.stats + q, v);
+        for (int off = 1; off < 64; off <<= 1) {
+            const int v = __shfl_up(incl, off);
+            if (lane >= off) incl += v;
+        }
+        const int totalRays = __shfl(incl, 63);
+        unsigned int qbase = 0;
+        if (totalRays > 0) {
+            if (lane == 63) qbase = atomicAdd(a.ctr + a.parity, (unsigned int)totalRays);
+            qbase = __shfl(qbase, 63);
+        }
+        unsigned int pos = qbase + (unsigned)(incl - nray);
+        auto emit = [&](double dx, double dy, double dz, double param, int idx, unsigned flags) {
+            double2* dst = reinterpret_cast<double2*>(a.rays + pos);
+            int2 tail = make_int2(idx, (int)flags);
+            double tailv;
+            memcpy(&tailv, &tail, 8);
+            dst[0] = make_double2(p.rx, p.ry);
+            dst[1] = make_double2(p.rz, dx);
+            dst[2] = make_double2(dy, dz);
+            dst[3] = make_double2(param, tailv);
+            pos++;
+        };
+        if (peel != PEEL_NONE) {
+            const unsigned ellBits = (unsigned)p.ell << 18;
+            for (int i = 0; i < a.ninstr; i++) {
+                const DevInstr& ins = sh.instr[i];
+                const int l = ins.kind == SKIRT_INSTR_SED ? -1 : E.pixel(ins, p);
+                if (ins.kind == SKIRT_INSTR_FRAME && l < 0) continue;
+                double Lp = p.L;
+                unsigned cat, level = 0;
+                if (peel == PEEL_EMISSION) {
+                    cat = p.stellar >= 0 ? CAT_STAR_DIRECT : CAT_DUST_DIRECT;
+                } else {
+                    double I = 0;
+                    E.peelWeight(ins, p, ox, oy, oz, I);  // the direction before scattering
+                    Lp = p.L * I;
+                    cat = p.stellar >= 0 ? CAT_STAR_SCATTERED : CAT_DUST_SCATTERED;
+                    level = (unsigned)min(p.nscatt, 255);  // nscatt already counts this scattering
+                }
+                emit(ins.kobs[0], ins.kobs[1], ins.kobs[2], Lp, l,
+                     RAY_PEEL | (cat << 2) | ((unsigned)i << 4) | (level << 10) | ellBits);
+            }
+        }
+        if (mainMode != RAY_NONE) emit(p.kx, p.ky, p.kz, mainParam, slot, mainMode | ((unsigned)p.ell << 18));
+        // the slot stays active while it has a FILL/WALK ray in flight
+        const bool active = mainMode != RAY_NONE;
+        const unsigned long long am = __ballot(active);
+        if (am) {
+            const int leader = __ffsll((long long)am) - 1;
+            unsigned int abase = 0;
+            if (lane == leader) abase = atomicAdd(a.ctr + 2 + (1 - a.parity), (unsigned int)__popcll(am));
+            abase = __shfl(abase, leader);
+            if (active) actOut[abase + __popcll(am & ((1ull << lane) - 1ull))] = slot;
+        }
+        if (valid) E.store(slot, p);
     }
+    const unsigned long long vals[6] = {E.packets, 0, 0, 0, E.detects, 0};
+    flushStats(a, vals);
 }
 
 }  // namespace
@@ -870,7 +1006,6 @@ struct SkirtMcrt {
     double *dRho = nullptr, *dOptics = nullptr;
     // sources
     int nstar = 0;
-    int* dGeomKind = nullptr;
     double *dGeomParam = nullptr, *dLum = nullptr, *dLumtot = nullptr, *dCdf = nullptr;
     double emissionBias = 0.5;
     // instruments
@@ -881,13 +1016,17 @@ struct SkirtMcrt {
     // tallies
     double *dLabs = nullptr, *dTally = nullptr;
     bool ownLabs = true, ownTally = true;
-    unsigned long long *dCounter = nullptr, *dStats = nullptr;
-    unsigned int* dError = nullptr;
+    unsigned long long *dClaim = nullptr, *dStats = nullptr;
+    unsigned int *dError = nullptr, *dCtr = nullptr, *hCtr = nullptr;
+    // slot pool
+    int nslots = 0, rayCap = 0;
+    void* dPool = nullptr;
+    size_t poolBytes = 0;
     // config
-    int block = kBlock, grid = 0, threshold = 16;
+    int traceGrid = 0, threshold = 16, slotsWanted = 0;
     double lastMs = 0;
-    size_t maxLds = 0;
     int numCUs = 0;
+    int lastIterations = 0;
 };
 
 namespace {
@@ -913,6 +1052,35 @@ int upload(SkirtMcrt* c, T*& dst, const T* src, size_t n) {
     return SKIRT_OK;
 }
 
+// slot pool: the ray queue, the SoA packet state, per-slot results and two active lists
+int ensurePool(SkirtMcrt* c, int nslots) {
+    const int rayCap = nslots * (1 + (int)c->instr.size());
+    const size_t need = (size_t)rayCap * sizeof(RayRec) + (size_t)nslots * (10 * 8 + 4 * 4 + 6 * 4 + 2 * 4) + 4096;
+    if (c->dPool && c->nslots == nslots && c->rayCap == rayCap) return SKIRT_OK;
+    if (c->dPool) { (void)hipFree(c->dPool); c->dPool = nullptr; }
+    HIPCHECK(c, hipMalloc(&c->dPool, need));
+    c->poolBytes = need;
+    c->nslots = nslots;
+    c->rayCap = rayCap;
+    return SKIRT_OK;
+}
+
+void carvePool(SkirtMcrt* c, Args& a) {
+    char* p = static_cast<char*>(c->dPool);
+    const size_t n = (size_t)c->nslots;
+    auto takeD = [&](double*& d) { d = reinterpret_cast<double*>(p); p += n * 8; };
+    auto takeI = [&](int*& d) { d = reinterpret_cast<int*>(p); p += n * 4; };
+    auto takeU = [&](uint32_t*& d) { d = reinterpret_cast<uint32_t*>(p); p += n * 4; };
+    a.rays = reinterpret_cast<RayRec*>(p);
+    p += (size_t)c->rayCap * sizeof(RayRec);
+    takeD(a.srx); takeD(a.sry); takeD(a.srz); takeD(a.skx); takeD(a.sky); takeD(a.skz); takeD(a.sL); takeD(a.sLth);
+    takeD(a.resA); takeD(a.resB);
+    takeI(a.sell); takeI(a.snscatt); takeI(a.sstellar); takeI(a.sstate);
+    takeU(a.splo); takeU(a.sphi); takeU(a.sblock); takeU(a.sw2); takeU(a.sw3); takeU(a.shave);
+    takeI(a.act[0]); takeI(a.act[1]);
+    a.nslots = c->nslots;
+}
+
 }  // namespace
 
 extern "C" {
@@ -926,18 +1094,17 @@ int skirt_mcrt_create(int device, SkirtMcrt** out) {
     c->device = device;
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
-        hipMalloc(&c->dCounter, sizeof(unsigned long long)) != hipSuccess ||
+        hipMalloc(&c->dClaim, sizeof(unsigned long long)) != hipSuccess ||
         hipMalloc(&c->dStats, 8 * sizeof(unsigned long long)) != hipSuccess ||
-        hipMalloc(&c->dError, sizeof(unsigned int)) != hipSuccess) {
+        hipMalloc(&c->dError, sizeof(unsigned int)) != hipSuccess ||
+        hipMalloc(&c->dCtr, 8 * sizeof(unsigned int)) != hipSuccess ||
+        hipHostMalloc(&c->hCtr, 8 * sizeof(unsigned int)) != hipSuccess) {
         delete c;
         return SKIRT_ERR_HIP;
     }
     c->stream = c->own;
     hipDeviceProp_t prop;
-    if (hipGetDeviceProperties(&prop, device) == hipSuccess) {
-        c->maxLds = prop.sharedMemPerBlock;
-        c->numCUs = prop.multiProcessorCount;
-    }
+    if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->numCUs = prop.multiProcessorCount;
     (void)hipMemset(c->dStats, 0, 8 * sizeof(unsigned long long));
     (void)hipMemset(c->dError, 0, sizeof(unsigned int));
     *out = c;
@@ -950,12 +1117,11 @@ int skirt_mcrt_set_stream(SkirtMcrt* c, void* s) {
     return SKIRT_OK;
 }
 
-int skirt_mcrt_configure(SkirtMcrt* c, int block, int grid, int threshold) {
+int skirt_mcrt_configure(SkirtMcrt* c, int slots, int grid, int threshold) {
     if (!c) return SKIRT_ERR_ARG;
-    if (block) {
-        if (block != kBlock) return fail(c, SKIRT_ERR_ARG, "only 256-thread blocks are compiled");
-    }
-    c->grid = grid;
+    if (slots < 0 || grid < 0 || threshold < 0) return fail(c, SKIRT_ERR_ARG, "negative configuration value");
+    c->slotsWanted = slots;
+    c->traceGrid = grid;
     if (threshold) c->threshold = std::max(1, std::min(64, threshold));
     return SKIRT_OK;
 }
@@ -983,10 +1149,10 @@ int skirt_mcrt_upload_grid(SkirtMcrt* c, const SkirtGridDesc* g) {
     } else if (g->kind == SKIRT_GRID_OCTREE) {
         if (g->nnodes < 1 || !g->box || !g->first_child || !g->cellnumber || !g->nbr_offset)
             return fail(c, SKIRT_ERR_ARG, "bad octree grid");
-        // validate the index arrays so that the kernel never reads out of bounds
+        // validate the index arrays so that the kernels never read out of bounds
         int nleaf = 0;
         for (int l = 0; l < g->nnodes; l++) {
-            int fc = g->first_child[l];
+            const int fc = g->first_child[l];
             if (fc >= 0 && (fc + 8 > g->nnodes || fc <= l)) return fail(c, SKIRT_ERR_ARG, "octree child index out of range");
             if (fc < 0) {
                 if (g->cellnumber[l] < 0 || g->cellnumber[l] >= g->ncells) return fail(c, SKIRT_ERR_ARG, "octree cell number out of range");
@@ -994,7 +1160,7 @@ int skirt_mcrt_upload_grid(SkirtMcrt* c, const SkirtGridDesc* g) {
             }
         }
         if (nleaf != g->ncells) return fail(c, SKIRT_ERR_ARG, "octree leaf count != ncells");
-        int nnbr = g->nbr_offset[6 * (size_t)g->nnodes];
+        const int nnbr = g->nbr_offset[6 * (size_t)g->nnodes];
         for (size_t q = 0; q < 6 * (size_t)g->nnodes; q++)
             if (g->nbr_offset[q] < 0 || g->nbr_offset[q] > g->nbr_offset[q + 1]) return fail(c, SKIRT_ERR_ARG, "bad neighbor offsets");
         for (int q = 0; q < nnbr; q++)
@@ -1023,10 +1189,11 @@ int skirt_mcrt_upload_media(SkirtMcrt* c, const SkirtMediaDesc* m) {
     if (c->gridKind < 0) return fail(c, SKIRT_ERR_STATE, "upload the grid before the media");
     if (m->ncells != c->ncells || m->ncomp < 1 || m->ncomp > 8 || m->nlambda < 1)
         return fail(c, SKIRT_ERR_ARG, "media sizes do not match the grid (1 <= ncomp <= 8)");
+    if (m->nlambda >= (1 << 14)) return fail(c, SKIRT_ERR_ARG, "at most 16383 wavelengths");
     HIPCHECK(c, hipSetDevice(c->device));
     c->ncomp = m->ncomp;
     c->nlambda = m->nlambda;
-    size_t nt = (size_t)m->ncomp * m->nlambda;
+    const size_t nt = (size_t)m->ncomp * m->nlambda;
     std::vector<double> opt(4 * nt);
     std::memcpy(opt.data(), m->kext, nt * sizeof(double));
     std::memcpy(opt.data() + nt, m->ksca, nt * sizeof(double));
@@ -1044,12 +1211,12 @@ int skirt_mcrt_upload_sources(SkirtMcrt* c, const SkirtSourceDesc* s) {
     for (int h = 0; h < s->ncomp; h++)
         if (s->geom_kind[h] != SKIRT_GEOM_PLUMMER) return fail(c, SKIRT_ERR_UNSUPPORTED, "unsupported source geometry");
     HIPCHECK(c, hipSetDevice(c->device));
+    if (c->nlambda && c->nlambda != s->nlambda) return fail(c, SKIRT_ERR_ARG, "sources and media disagree on nlambda");
+    if (s->nlambda >= (1 << 14)) return fail(c, SKIRT_ERR_ARG, "at most 16383 wavelengths");
     c->nstar = s->ncomp;
     c->emissionBias = s->emission_bias;
-    if (c->nlambda && c->nlambda != s->nlambda) return fail(c, SKIRT_ERR_ARG, "sources and media disagree on nlambda");
     c->nlambda = s->nlambda;
     int rc;
-    if ((rc = upload(c, c->dGeomKind, s->geom_kind, (size_t)s->ncomp))) return rc;
     if ((rc = upload(c, c->dGeomParam, s->geom_param, 4 * (size_t)s->ncomp))) return rc;
     if ((rc = upload(c, c->dLum, s->lum, (size_t)s->ncomp * s->nlambda))) return rc;
     if ((rc = upload(c, c->dLumtot, s->lumtot, (size_t)s->nlambda))) return rc;
@@ -1059,6 +1226,7 @@ int skirt_mcrt_upload_sources(SkirtMcrt* c, const SkirtSourceDesc* s) {
 
 int skirt_mcrt_set_instruments(SkirtMcrt* c, const SkirtInstrDesc* in, int n) {
     if (!c || n < 0 || (n > 0 && !in)) return SKIRT_ERR_ARG;
+    if (n > 63) return fail(c, SKIRT_ERR_ARG, "at most 63 instruments");
     if (c->nlambda < 1) return fail(c, SKIRT_ERR_STATE, "upload sources or media before instruments");
     HIPCHECK(c, hipSetDevice(c->device));
     c->instr.clear();
@@ -1073,16 +1241,17 @@ int skirt_mcrt_set_instruments(SkirtMcrt* c, const SkirtInstrDesc* in, int n) {
         if (d.kind != SKIRT_INSTR_SED && (d.nx < 1 || d.ny < 1)) return fail(c, SKIRT_ERR_ARG, "bad instrument frame size");
         if (d.kind == SKIRT_INSTR_SED) { d.nx = 0; d.ny = 0; }
         d.levels = d.kind == SKIRT_INSTR_FULL ? in[i].scattering_levels : 0;
+        if (d.levels < 0 || d.levels > 250) return fail(c, SKIRT_ERR_ARG, "scattering levels out of range");
         d.nslots = d.kind == SKIRT_INSTR_FULL ? 5 + d.levels : 1;
         for (int q = 0; q < 3; q++) d.kobs[q] = in[i].kobs[q];
         d.sinphi = in[i].sinphi; d.cosphi = in[i].cosphi; d.sintheta = in[i].sintheta; d.costheta = in[i].costheta;
         d.sinpa = in[i].sinpa; d.cospa = in[i].cospa;
         d.xpmin = in[i].xpmin; d.xpsiz = in[i].xpsiz; d.ypmin = in[i].ypmin; d.ypsiz = in[i].ypsiz;
         d.frameBase = off;
-        long long nframes = (d.kind == SKIRT_INSTR_SED) ? 0 : (long long)d.nslots * c->nlambda * d.nx * d.ny;
+        const long long nframes = (d.kind == SKIRT_INSTR_SED) ? 0 : (long long)d.nslots * c->nlambda * d.nx * d.ny;
         off += nframes;
         d.sedBase = off;
-        long long nseds = (d.kind == SKIRT_INSTR_FRAME) ? 0 : (long long)d.nslots * c->nlambda;
+        const long long nseds = (d.kind == SKIRT_INSTR_FRAME) ? 0 : (long long)d.nslots * c->nlambda;
         off += nseds;
         d.sedOff = sedOff;
         sedOff += (int)nseds;
@@ -1092,8 +1261,8 @@ int skirt_mcrt_set_instruments(SkirtMcrt* c, const SkirtInstrDesc* in, int n) {
     c->nsed = sedOff;
     int rc = upload(c, c->dInstr, c->instr.data(), c->instr.size());
     if (rc) return rc;
-    // (re)allocate owned tallies lazily at run time
     if (c->ownTally && c->dTally) { (void)hipFree(c->dTally); c->dTally = nullptr; }
+    if (c->dPool) { (void)hipFree(c->dPool); c->dPool = nullptr; c->nslots = 0; }
     return SKIRT_OK;
 }
 
@@ -1105,7 +1274,7 @@ int skirt_mcrt_tally_sizes(SkirtMcrt* c, size_t* nl, size_t* ni) {
 }
 
 static int ensureTallies(SkirtMcrt* c) {
-    size_t nl = (size_t)c->ncells * c->nlambda;
+    const size_t nl = (size_t)c->ncells * c->nlambda;
     if (!c->dLabs && nl) {
         HIPCHECK(c, hipMalloc(&c->dLabs, nl * sizeof(double)));
         HIPCHECK(c, hipMemsetAsync(c->dLabs, 0, nl * sizeof(double), c->stream));
@@ -1139,7 +1308,7 @@ int skirt_mcrt_zero_tallies(SkirtMcrt* c) {
     HIPCHECK(c, hipSetDevice(c->device));
     int rc = ensureTallies(c);
     if (rc) return rc;
-    size_t nl = (size_t)c->ncells * c->nlambda;
+    const size_t nl = (size_t)c->ncells * c->nlambda;
     if (c->dLabs && nl) HIPCHECK(c, hipMemsetAsync(c->dLabs, 0, nl * sizeof(double), c->stream));
     if (c->dTally && c->nInstrTally) HIPCHECK(c, hipMemsetAsync(c->dTally, 0, c->nInstrTally * sizeof(double), c->stream));
     HIPCHECK(c, hipMemsetAsync(c->dStats, 0, 8 * sizeof(unsigned long long), c->stream));
@@ -1159,24 +1328,30 @@ int skirt_mcrt_run_stellar(SkirtMcrt* c, uint64_t npp, uint64_t first, uint64_t 
     HIPCHECK(c, hipSetDevice(c->device));
     int rc = ensureTallies(c);
     if (rc) return rc;
-    if (count == 0) { c->lastMs = 0; return SKIRT_OK; }
+    c->lastMs = 0;
+    c->lastIterations = 0;
+    if (count == 0) return SKIRT_OK;
+    if (!c->dOptics) {  // a dust-free simulation still stages (zero) optical tables
+        std::vector<double> z(4 * (size_t)c->nlambda, 0.0);
+        if ((rc = upload(c, c->dOptics, z.data(), z.size()))) return rc;
+    }
+    // slot pool: enough packets in flight to fill the chip many times over, bounded by the phase size
+    int slots = c->slotsWanted > 0 ? c->slotsWanted : (1 << 21);
+    if ((uint64_t)slots > count) slots = (int)count;
+    slots = std::max(slots, 64);
+    if ((rc = ensurePool(c, slots))) return rc;
 
     Args a{};
     a.ncells = c->ncells;
     a.nx = c->nx; a.ny = c->ny; a.nz = c->nz;
-    a.xv = c->dMesh;
+    a.mesh = c->dMesh;
     a.gx0 = c->gx0; a.gx1 = c->gx1; a.gy0 = c->gy0; a.gy1 = c->gy1; a.gz0 = c->gz0; a.gz1 = c->gz1;
     a.box = c->dBox; a.firstChild = c->dFirstChild; a.cellnumber = c->dCellnumber;
     a.nbrOffset = c->dNbrOffset; a.nbrList = c->dNbrList; a.eps = c->eps; a.search = c->search;
     a.ncomp = std::max(1, c->ncomp); a.nlambda = c->nlambda;
     a.rho = c->dRho;
-    // a dust-free simulation still needs (zero) optical tables for the LDS staging
-    if (!c->dOptics) {
-        std::vector<double> z(4 * (size_t)c->nlambda, 0.0);
-        if ((rc = upload(c, c->dOptics, z.data(), z.size()))) return rc;
-    }
     a.optics = c->dOptics;
-    a.nstar = c->nstar; a.geomKind = c->dGeomKind; a.geomParam = c->dGeomParam; a.lum = c->dLum;
+    a.nstar = c->nstar; a.geomParam = c->dGeomParam; a.lum = c->dLum;
     a.lumtot = c->dLumtot; a.cdf = c->dCdf; a.emissionBias = c->emissionBias;
     a.ninstr = (int)c->instr.size(); a.instr = c->dInstr; a.nsed = c->nsed;
     a.npp = npp; a.first = first; a.end = first + count; a.seed = seed; a.tag = SKIRT_PHASE_STELLAR;
@@ -1185,12 +1360,14 @@ int skirt_mcrt_run_stellar(SkirtMcrt* c, uint64_t npp, uint64_t first, uint64_t 
     a.hasDust = p->has_dust ? 1 : 0;
     if (a.store && !c->dLabs) return fail(c, SKIRT_ERR_STATE, "no Labs buffer");
     a.labs = c->dLabs; a.tally = c->dTally;
-    a.counter = c->dCounter; a.error = c->dError; a.stats = c->dStats;
+    a.error = c->dError; a.stats = c->dStats;
+    a.claim = c->dClaim; a.ctr = c->dCtr;
     a.threshold = c->threshold;
-    // LDS layout (doubles)
+    carvePool(c, a);
+    // LDS layout (doubles): mesh | optics | instruments | SED sums
     int off = 0;
     a.ldsMeshOff = off;
-    off += (c->gridKind == SKIRT_GRID_CARTESIAN) ? (c->nx + c->ny + c->nz + 3) : 0;
+    off += (c->gridKind == SKIRT_GRID_CARTESIAN && a.hasDust) ? (c->nx + c->ny + c->nz + 3) : 0;
     off = (off + 1) & ~1;
     a.ldsOptOff = off;
     off += 4 * a.ncomp * a.nlambda;
@@ -1199,32 +1376,64 @@ int skirt_mcrt_run_stellar(SkirtMcrt* c, uint64_t npp, uint64_t first, uint64_t 
     off += a.ninstr * (int)(sizeof(DevInstr) / sizeof(double));
     a.ldsSedOff = off;
     off += c->nsed;
-    size_t lds = (size_t)off * sizeof(double);
-    if (lds > 160 * 1024) return fail(c, SKIRT_ERR_UNSUPPORTED, "tables do not fit in LDS (" + std::to_string(lds) + " bytes)");
-
-    HIPCHECK(c, hipMemsetAsync(c->dCounter, 0, sizeof(unsigned long long), c->stream));
-    int grid = c->grid;
-    if (grid <= 0) {
+    const size_t lds = (size_t)off * sizeof(double);
+    if (lds > 64 * 1024) return fail(c, SKIRT_ERR_UNSUPPORTED, "tables do not fit in LDS (" + std::to_string(lds) + " bytes)");
+    const bool octree = c->gridKind == SKIRT_GRID_OCTREE;
+    const bool one = a.ncomp == 1;
+    auto traceFn = octree ? (one ? (const void*)traceKernel<SKIRT_GRID_OCTREE, true> : (const void*)traceKernel<SKIRT_GRID_OCTREE, false>)
+                          : (one ? (const void*)traceKernel<SKIRT_GRID_CARTESIAN, true> : (const void*)traceKernel<SKIRT_GRID_CARTESIAN, false>);
+    int tgrid = c->traceGrid;
+    if (tgrid <= 0) {
         int per = 0;
-        auto kfn = (c->gridKind == SKIRT_GRID_OCTREE)
-                       ? (a.ncomp == 1 ? (const void*)stellarKernel<SKIRT_GRID_OCTREE, true> : (const void*)stellarKernel<SKIRT_GRID_OCTREE, false>)
-                       : (a.ncomp == 1 ? (const void*)stellarKernel<SKIRT_GRID_CARTESIAN, true> : (const void*)stellarKernel<SKIRT_GRID_CARTESIAN, false>);
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kfn, kBlock, lds) != hipSuccess || per < 1) per = 4;
-        grid = std::max(1, c->numCUs) * per;
-        // never more lanes than packets (each lane claims at least one packet)
-        unsigned long long maxBlocks = (count + kBlock - 1) / kBlock;
-        if ((unsigned long long)grid > maxBlocks) grid = (int)maxBlocks;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, traceFn, kBlock, lds) != hipSuccess || per < 1) per = 2;
+        tgrid = std::max(1, c->numCUs) * per;
     }
+    const int egrid = std::max(1, std::min((slots + kBlock - 1) / kBlock, std::max(1, c->numCUs) * 8));
+
+    HIPCHECK(c, hipMemsetAsync(c->dClaim, 0, sizeof(unsigned long long), c->stream));
+    HIPCHECK(c, hipMemsetAsync(c->dCtr, 0, 8 * sizeof(unsigned int), c->stream));
     HIPCHECK(c, hipEventRecord(c->ev0, c->stream));
-    int gk = (c->gridKind == SKIRT_GRID_OCTREE) ? SKIRT_GRID_OCTREE : SKIRT_GRID_CARTESIAN;
-    if (gk == SKIRT_GRID_OCTREE) {
-        if (a.ncomp == 1) hipLaunchKernelGGL((stellarKernel<SKIRT_GRID_OCTREE, true>), dim3(grid), dim3(kBlock), lds, c->stream, a);
-        else hipLaunchKernelGGL((stellarKernel<SKIRT_GRID_OCTREE, false>), dim3(grid), dim3(kBlock), lds, c->stream, a);
-    } else {
-        if (a.ncomp == 1) hipLaunchKernelGGL((stellarKernel<SKIRT_GRID_CARTESIAN, true>), dim3(grid), dim3(kBlock), lds, c->stream, a);
-        else hipLaunchKernelGGL((stellarKernel<SKIRT_GRID_CARTESIAN, false>), dim3(grid), dim3(kBlock), lds, c->stream, a);
+    auto launchEvent = [&](const Args& aa) {
+        if (octree) {
+            if (one) hipLaunchKernelGGL((eventKernel<SKIRT_GRID_OCTREE, true>), dim3(egrid), dim3(kBlock), lds, c->stream, aa);
+            else hipLaunchKernelGGL((eventKernel<SKIRT_GRID_OCTREE, false>), dim3(egrid), dim3(kBlock), lds, c->stream, aa);
+        } else {
+            if (one) hipLaunchKernelGGL((eventKernel<SKIRT_GRID_CARTESIAN, true>), dim3(egrid), dim3(kBlock), lds, c->stream, aa);
+            else hipLaunchKernelGGL((eventKernel<SKIRT_GRID_CARTESIAN, false>), dim3(egrid), dim3(kBlock), lds, c->stream, aa);
+        }
+    };
+    auto launchTrace = [&](const Args& aa) {
+        if (octree) {
+            if (one) hipLaunchKernelGGL((traceKernel<SKIRT_GRID_OCTREE, true>), dim3(tgrid), dim3(kBlock), lds, c->stream, aa);
+            else hipLaunchKernelGGL((traceKernel<SKIRT_GRID_OCTREE, false>), dim3(tgrid), dim3(kBlock), lds, c->stream, aa);
+        } else {
+            if (one) hipLaunchKernelGGL((traceKernel<SKIRT_GRID_CARTESIAN, true>), dim3(tgrid), dim3(kBlock), lds, c->stream, aa);
+            else hipLaunchKernelGGL((traceKernel<SKIRT_GRID_CARTESIAN, false>), dim3(tgrid), dim3(kBlock), lds, c->stream, aa);
+        }
+    };
+    // iteration it (parity q = it & 1): the event kernel consumes active list ctr[2+q] and queues rays
+    // into ctr[q] and the next active list into ctr[2+1-q]; the trace kernel walks the ctr[q] rays and
+    // resets ctr[1-q] and ctr[2+q] for the next iteration. The host polls the active count every few
+    // iterations -- the only host synchronization of the phase.
+    int it = 0;
+    const int pollEvery = 4;
+    while (true) {
+        a.parity = it & 1;
+        a.init = (it == 0) ? 1 : 0;
+        launchEvent(a);
+        HIPCHECK(c, hipGetLastError());
+        if (!a.hasDust) { it++; break; }  // without dust every packet completes inside the event kernel
+        launchTrace(a);
+        HIPCHECK(c, hipGetLastError());
+        it++;
+        if (it % pollEvery == 0) {
+            HIPCHECK(c, hipMemcpyAsync(c->hCtr, c->dCtr, 8 * sizeof(unsigned int), hipMemcpyDeviceToHost, c->stream));
+            HIPCHECK(c, hipStreamSynchronize(c->stream));
+            if (c->hCtr[2 + (it & 1)] == 0) break;  // no slot has a ray in flight: the phase is over
+        }
+        if (it > 10000000) return fail(c, SKIRT_ERR_STATE, "photon phase did not terminate");
     }
-    HIPCHECK(c, hipGetLastError());
+    c->lastIterations = it;
     HIPCHECK(c, hipEventRecord(c->ev1, c->stream));
     return SKIRT_OK;
 }
@@ -1245,7 +1454,7 @@ int skirt_mcrt_download(SkirtMcrt* c, double* labs, double* instr) {
     if (!c) return SKIRT_ERR_ARG;
     int rc = skirt_mcrt_synchronize(c);
     if (rc) return rc;
-    size_t nl = (size_t)c->ncells * c->nlambda;
+    const size_t nl = (size_t)c->ncells * c->nlambda;
     if (labs && nl) {
         if (!c->dLabs) return fail(c, SKIRT_ERR_STATE, "no Labs buffer");
         std::vector<double> t(nl);
@@ -1283,10 +1492,11 @@ void skirt_mcrt_destroy(SkirtMcrt* c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     void* bufs[] = {c->dMesh, c->dBox, c->dFirstChild, c->dCellnumber, c->dNbrOffset, c->dNbrList, c->dRho,
-                    c->dOptics, c->dGeomKind, c->dGeomParam, c->dLum, c->dLumtot, c->dCdf, c->dInstr,
-                    c->dCounter, c->dStats, c->dError};
+                    c->dOptics, c->dGeomParam, c->dLum, c->dLumtot, c->dCdf, c->dInstr,
+                    c->dClaim, c->dStats, c->dError, c->dCtr, c->dPool};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
+    if (c->hCtr) (void)hipHostFree(c->hCtr);
     if (c->ownLabs && c->dLabs) (void)hipFree(c->dLabs);
     if (c->ownTally && c->dTally) (void)hipFree(c->dTally);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
