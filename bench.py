@@ -62,7 +62,9 @@ def main():
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--packets-per-lambda", type=int, default=0, help="per rank; default per config")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--threshold", type=int, default=0, help="event batching threshold (0 = engine default)")
+    ap.add_argument("--threshold", type=int, default=0, help="idle lanes before a wave pulls rays (0 = engine default)")
+    ap.add_argument("--slots", type=int, default=0, help="packet slots in flight (0 = engine default)")
+    ap.add_argument("--trace-grid", type=int, default=0, help="trace kernel workgroups (0 = occupancy-derived)")
     args = ap.parse_args()
 
     import torch
@@ -85,8 +87,8 @@ def main():
     share = ppl * info.nlambda  # packets per rank per step
     first = rank * share
     sim.attach(local)
-    if args.threshold:
-        sim.configure(threshold=args.threshold)
+    if args.threshold or args.slots or args.trace_grid:
+        sim.configure(slots=args.slots, grid=args.trace_grid, threshold=args.threshold)
     stream = torch.cuda.current_stream()
     sim.set_stream(stream.cuda_stream)
     n_labs, n_instr = sim.tally_sizes()

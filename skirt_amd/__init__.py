@@ -18,7 +18,9 @@ import os
 import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG_DIR, "libskirt_amd.so")
+# SKIRT_AMD_LIB selects another build of the same library (e.g. a tuning variant built by
+# tools/build_variant.sh next to the default one)
+LIB_PATH = os.path.join(PKG_DIR, os.environ.get("SKIRT_AMD_LIB", "libskirt_amd.so"))
 DATA_DIR = os.path.join(PKG_DIR, "data")
 
 GRID_CARTESIAN, GRID_OCTREE = 0, 1
@@ -122,8 +124,10 @@ class Simulation:
         self._check(lib().skirt_sim_attach(self._h, device))
         self.attached = True
 
-    def configure(self, grid=0, threshold=0):
-        self._check_engine(lib().skirt_mcrt_configure(self.engine, 0, grid, threshold))
+    def configure(self, slots=0, grid=0, threshold=0):
+        """Engine knobs (0 = default): packet slots in flight, trace-kernel workgroups, and the number
+        of idle lanes that makes a wave pull new rays."""
+        self._check_engine(lib().skirt_mcrt_configure(self.engine, slots, grid, threshold))
 
     def _check_engine(self, rc):
         if rc != 0:

@@ -41,6 +41,10 @@ namespace {
 
 constexpr double kDblMax = 1.7976931348623157e308;
 constexpr int kBlock = 256;
+// occupancy attribute of the trace kernel (a build knob for tuning variants, tools/build_variant.sh)
+#ifndef SKIRT_TRACE_ATTR
+#define SKIRT_TRACE_ATTR
+#endif
 
 // ------------------------------------------------------------------ descriptors
 struct DevInstr {
@@ -70,6 +74,12 @@ __device__ __forceinline__ int rayInstr(unsigned f) { return (int)((f >> 4) & 63
 __device__ __forceinline__ int rayLevel(unsigned f) { return (int)((f >> 10) & 255u); }
 __device__ __forceinline__ int rayEll(unsigned f) { return (int)(f >> 18); }
 
+struct LeafEntry;
+
+// grid kinds of the kernels: SKIRT_GRID_CARTESIAN, SKIRT_GRID_OCTREE (leaf-map walk) and the octree
+// walked through the node arrays (trees deeper than kMaxMapLevel or not split at box centres)
+constexpr int kOctreeNodes = 16;
+
 struct Args {
     // grid
     int nx, ny, nz, ncells;
@@ -82,6 +92,10 @@ struct Args {
     const int* nbrList;
     double eps;
     int search;
+    const LeafEntry* leafMap;       // octree leaf map: Morton-ordered finest-level cells -> leaf
+    const double* treeT;         // octree split coordinates per axis, 3 x (mapN + 1) (staged in LDS)
+    int mapL, mapN;              // leaf map depth and 2^depth
+    double mapInvX, mapInvY, mapInvZ;
     // media
     int ncomp, nlambda;
     const double* rho;
@@ -123,6 +137,32 @@ struct Args {
     int ldsMeshOff, ldsOptOff, ldsInstrOff, ldsSedOff;  // in doubles
 };
 
+// One finest-level cell of the octree leaf map: the leaf node that covers it, that leaf's dust cell
+// number and level, and the leaf's density of dust component 0 (the one-component kernels need no
+// other gather per segment). 16 bytes, one global_load_dwordx4.
+struct __attribute__((aligned(16))) LeafEntry {
+    int node;
+    unsigned cl;  // cell | level << 27
+    double rho0;
+};
+constexpr int kLeafLevelShift = 27;
+constexpr unsigned kLeafCellMask = (1u << kLeafLevelShift) - 1u;
+constexpr int kMaxMapLevel = 9;  // 512^3 x 16 B = 2 GiB of HBM at most
+
+// Morton index of finest-level cell (x, y, z), 10 bits per axis: a ray's consecutive lookups mostly
+// hit the same or a neighbouring 2x2x2 block, i.e. the same 128-byte line
+__host__ __device__ __forceinline__ unsigned spread3(unsigned v) {
+    v &= 0x3ffu;
+    v = (v | (v << 16)) & 0x030000FFu;
+    v = (v | (v << 8)) & 0x0300F00Fu;
+    v = (v | (v << 4)) & 0x030C30C3u;
+    v = (v | (v << 2)) & 0x09249249u;
+    return v;
+}
+__host__ __device__ __forceinline__ unsigned morton3(unsigned x, unsigned y, unsigned z) {
+    return spread3(x) | (spread3(y) << 1) | (spread3(z) << 2);
+}
+
 __device__ __forceinline__ void atomicAddF64(double* p, double v) {
     // explicit global address space: global_atomic_add_f64 instead of a flat atomic
     __hip_atomic_fetch_add((__attribute__((address_space(1))) double*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -130,7 +170,7 @@ __device__ __forceinline__ void atomicAddF64(double* p, double v) {
 
 // the small tables staged in LDS
 struct Shared {
-    const double* mesh;
+    const double* mesh;   // Cartesian: mesh borders | octree with leaf map: split coordinates
     const double* kext;   // [ncomp][nlambda]
     const double* ksca;
     const double* alb;
@@ -139,7 +179,7 @@ struct Shared {
     double* sed;
 };
 
-__device__ __forceinline__ Shared stageTables(const Args& a, double* lds, bool mesh) {
+__device__ __forceinline__ Shared stageTables(const Args& a, double* lds, bool mesh, bool tree) {
     Shared sh;
     double* m = lds + a.ldsMeshOff;
     double* opt = lds + a.ldsOptOff;
@@ -153,6 +193,8 @@ __device__ __forceinline__ Shared stageTables(const Args& a, double* lds, bool m
     sh.sed = lds + a.ldsSedOff;
     const int nmesh = mesh ? (a.nx + a.ny + a.nz + 3) : 0;
     for (int q = threadIdx.x; q < nmesh; q += blockDim.x) m[q] = a.mesh[q];
+    const int ntree = tree ? 3 * (a.mapN + 1) : 0;
+    for (int q = threadIdx.x; q < ntree; q += blockDim.x) m[q] = a.treeT[q];
     const int nopt = 4 * a.ncomp * a.nlambda;
     for (int q = threadIdx.x; q < nopt; q += blockDim.x) opt[q] = a.optics[q];
     const int ninw = a.ninstr * (int)(sizeof(DevInstr) / sizeof(double));
@@ -181,8 +223,10 @@ struct Ray {
     double kext;           // kappa_ext at the ray's wavelength (one dust component)
     double param;          // see RayRec::param
     double f1, f2;         // FILL: exp(-tau), Lsca | WALK: tau and s at the previous segment end
-    double bx0, by0, bz0, bx1, by1, bz1;  // octree: box of the current node
-    int ci, cj, ck;        // Cartesian cell indices | octree node in ci
+    double bx0, by0, bz0, bx1, by1, bz1;  // octree walked through the node arrays: box of the node
+    double rho0;           // density (component 0) of the current cell
+    int ci, cj, ck;        // Cartesian cell indices | octree: node, cell number, leaf size in finest cells
+    int jx, jy, jz;        // octree leaf map: finest-level index of the current leaf's lower corner
     int idx, ell;
     unsigned flags, mode;
 };
@@ -252,9 +296,9 @@ struct Grid<SKIRT_GRID_CARTESIAN> {
             x += kx * d2; y += ky * d2; z = a.gz1 - 1e-8 * (zv[a.nz] - zv[a.nz - 1]);
         }
         if (x < a.gx0 || x > a.gx1 || y < a.gy0 || y > a.gy1 || z < a.gz0 || z > a.gz1) return false;
-        if (d0 > 0) seg(-1, d0);
-        if (d1 > 0) seg(-1, d1);
-        if (d2 > 0) seg(-1, d2);
+        if (d0 > 0) seg(-1, 0.0, d0);
+        if (d1 > 0) seg(-1, 0.0, d1);
+        if (d2 > 0) seg(-1, 0.0, d2);
         r.x = x; r.y = y; r.z = z;
         r.ci = locateClip(xv, a.nx + 1, x);
         r.cj = locateClip(yv, a.ny + 1, y);
@@ -270,6 +314,7 @@ struct Grid<SKIRT_GRID_CARTESIAN> {
         const double* zv = yv + a.ny + 1;
         const int i = r.ci, j = r.cj, k = r.ck;
         const int m = k + a.nz * j + a.nz * a.ny * i;
+        const double rho0 = a.rho[(size_t)m * a.ncomp];
         const double xE = (r.dx < 0.0) ? xv[i] : xv[i + 1];
         const double yE = (r.dy < 0.0) ? yv[j] : yv[j + 1];
         const double zE = (r.dz < 0.0) ? zv[k] : zv[k + 1];
@@ -277,17 +322,17 @@ struct Grid<SKIRT_GRID_CARTESIAN> {
         const double dsy = (r.iy != 0.0) ? (yE - r.y) * r.iy : kDblMax;
         const double dsz = (r.iz != 0.0) ? (zE - r.z) * r.iz : kDblMax;
         if (dsx <= dsy && dsx <= dsz) {
-            if (!seg(m, dsx)) return false;
+            if (!seg(m, rho0, dsx)) return false;
             const int ni = i + ((r.dx < 0.0) ? -1 : 1);
             if (ni >= a.nx || ni < 0) return false;
             r.ci = ni; r.x = xE; r.y += r.dy * dsx; r.z += r.dz * dsx;
         } else if (dsy < dsx && dsy <= dsz) {
-            if (!seg(m, dsy)) return false;
+            if (!seg(m, rho0, dsy)) return false;
             const int nj = j + ((r.dy < 0.0) ? -1 : 1);
             if (nj >= a.ny || nj < 0) return false;
             r.cj = nj; r.x += r.dx * dsy; r.y = yE; r.z += r.dz * dsy;
         } else if (dsz < dsx && dsz < dsy) {
-            if (!seg(m, dsz)) return false;
+            if (!seg(m, rho0, dsz)) return false;
             const int nk = k + ((r.dz < 0.0) ? -1 : 1);
             if (nk >= a.nz || nk < 0) return false;
             r.ck = nk; r.x += r.dx * dsz; r.y += r.dy * dsz; r.z = zE;
@@ -307,9 +352,11 @@ struct Grid<SKIRT_GRID_CARTESIAN> {
     }
 };
 
-// Octree grid: TreeDustGrid.cpp:390-521 (TopDown and Neighbor search), DustGridPath::moveInside
+// Octree grid walked through the node arrays: TreeDustGrid.cpp:390-521 (TopDown and Neighbor
+// search), DustGridPath::moveInside. Used for trees the leaf map cannot hold, and by the leaf-map
+// walk below for the rare steps whose exit point lies on a cell face.
 template <>
-struct Grid<SKIRT_GRID_OCTREE> {
+struct Grid<kOctreeNodes> {
     __device__ static __forceinline__ void loadBox(const Args& a, int l, double& x0, double& y0, double& z0,
                                                    double& x1, double& y1, double& z1) {
         const double2* b = reinterpret_cast<const double2*>(a.box + 6 * (size_t)l);
@@ -330,40 +377,77 @@ struct Grid<SKIRT_GRID_OCTREE> {
         return l;
     }
 
-    template <class SegFn>
-    __device__ static __forceinline__ bool begin(const Args& a, const Shared&, Ray& r, SegFn seg) {
-        const double kx = r.dx, ky = r.dy, kz = r.dz, eps = a.eps;
-        double rx = r.x, ry = r.y, rz = r.z, d0 = 0, d1 = 0, d2 = 0;
+    // the part of the path before the grid (TreeDustGrid.cpp:404-440): up to three segments outside the
+    // grid; on return (x,y,z) is the entry point. False for an empty path.
+    __device__ static __forceinline__ bool enterGrid(const Args& a, double& rx, double& ry, double& rz, double kx,
+                                                     double ky, double kz, double (&d)[3]) {
+        const double eps = a.eps;
+        d[0] = d[1] = d[2] = 0;
         if (rx <= a.gx0) {
             if (kx <= 0.0) return false;
-            d0 = (a.gx0 - rx) / kx; rx = a.gx0 + eps; ry += ky * d0; rz += kz * d0;
+            d[0] = (a.gx0 - rx) / kx; rx = a.gx0 + eps; ry += ky * d[0]; rz += kz * d[0];
         } else if (rx >= a.gx1) {
             if (kx >= 0.0) return false;
-            d0 = (a.gx1 - rx) / kx; rx = a.gx1 - eps; ry += ky * d0; rz += kz * d0;
+            d[0] = (a.gx1 - rx) / kx; rx = a.gx1 - eps; ry += ky * d[0]; rz += kz * d[0];
         }
         if (ry <= a.gy0) {
             if (ky <= 0.0) return false;
-            d1 = (a.gy0 - ry) / ky; rx += kx * d1; ry = a.gy0 + eps; rz += kz * d1;
+            d[1] = (a.gy0 - ry) / ky; rx += kx * d[1]; ry = a.gy0 + eps; rz += kz * d[1];
         } else if (ry >= a.gy1) {
             if (ky >= 0.0) return false;
-            d1 = (a.gy1 - ry) / ky; rx += kx * d1; ry = a.gy1 - eps; rz += kz * d1;
+            d[1] = (a.gy1 - ry) / ky; rx += kx * d[1]; ry = a.gy1 - eps; rz += kz * d[1];
         }
         if (rz <= a.gz0) {
             if (kz <= 0.0) return false;
-            d2 = (a.gz0 - rz) / kz; rx += kx * d2; ry += ky * d2; rz = a.gz0 + eps;
+            d[2] = (a.gz0 - rz) / kz; rx += kx * d[2]; ry += ky * d[2]; rz = a.gz0 + eps;
         } else if (rz >= a.gz1) {
             if (kz >= 0.0) return false;
-            d2 = (a.gz1 - rz) / kz; rx += kx * d2; ry += ky * d2; rz = a.gz1 - eps;
+            d[2] = (a.gz1 - rz) / kz; rx += kx * d[2]; ry += ky * d[2]; rz = a.gz1 - eps;
         }
+        return true;
+    }
+
+    template <class SegFn>
+    __device__ static __forceinline__ bool begin(const Args& a, const Shared&, Ray& r, SegFn seg) {
+        double rx = r.x, ry = r.y, rz = r.z, d[3];
+        if (!enterGrid(a, rx, ry, rz, r.dx, r.dy, r.dz, d)) return false;
         const int node = descend(a, rx, ry, rz);
         if (node < 0) return false;
-        if (d0 > 0) seg(-1, d0);
-        if (d1 > 0) seg(-1, d1);
-        if (d2 > 0) seg(-1, d2);
+        for (int q = 0; q < 3; q++)
+            if (d[q] > 0) seg(-1, 0.0, d[q]);
         r.x = rx; r.y = ry; r.z = rz;
         r.ci = node;
+        r.cj = a.cellnumber[node];
         loadBox(a, node, r.bx0, r.by0, r.bz0, r.bx1, r.by1, r.bz1);
         return true;
+    }
+
+    // the node after `node` for a ray leaving it through `wall` at (x,y,z) (already advanced by
+    // ds + eps): TreeNode::whichnode(wall, r) over the sorted neighbour list, else the descent from the
+    // root, with the reference's nextafter escape when the point has not left the node. May move
+    // (x,y,z). Returns -1 when the path leaves the grid.
+    __device__ static __forceinline__ int nextNode(const Args& a, int node, int wall, double& x, double& y, double& z,
+                                                   double kx, double ky, double kz) {
+        if (a.search == SKIRT_TREE_NEIGHBOR) {
+            const int q = 6 * node + wall;
+            const int nb = a.nbrOffset[q], ne = a.nbrOffset[q + 1];
+            for (int n = nb; n < ne; n++) {
+                const int c = a.nbrList[n];
+                double x0, y0, z0, x1, y1, z1;
+                loadBox(a, c, x0, y0, z0, x1, y1, z1);
+                if (x >= x0 && x <= x1 && y >= y0 && y <= y1 && z >= z0 && z <= z1) return c;
+            }
+        }
+        int next = descend(a, x, y, z);
+        if (next == node) {
+            // stuck: advance to the next representable coordinates (TreeDustGrid.cpp:502-519)
+            x = nextafter(x, (kx < 0.0) ? -kDblMax : kDblMax);
+            y = nextafter(y, (ky < 0.0) ? -kDblMax : kDblMax);
+            z = nextafter(z, (kz < 0.0) ? -kDblMax : kDblMax);
+            next = descend(a, x, y, z);
+            if (next == node) return -1;
+        }
+        return next;
     }
 
     template <class SegFn>
@@ -380,46 +464,138 @@ struct Grid<SKIRT_GRID_OCTREE> {
         if (dsx <= dsy && dsx <= dsz) { ds = dsx; wall = (r.dx < 0.0) ? 0 : 1; }
         else if (dsy <= dsx && dsy <= dsz) { ds = dsy; wall = (r.dy < 0.0) ? 2 : 3; }
         else { ds = dsz; wall = (r.dz < 0.0) ? 4 : 5; }
-        if (!seg(a.cellnumber[node], ds)) return false;
+        if (!seg(r.cj, a.rho[(size_t)r.cj * a.ncomp], ds)) return false;
         double x = r.x + (ds + a.eps) * r.dx;
         double y = r.y + (ds + a.eps) * r.dy;
         double z = r.z + (ds + a.eps) * r.dz;
-        int next = -1;
-        if (a.search == SKIRT_TREE_NEIGHBOR) {
-            // TreeNode::whichnode(wall, r): the first neighbour across the exit wall that contains r
-            const int q = 6 * node + wall;
-            const int nb = a.nbrOffset[q], ne = a.nbrOffset[q + 1];
-            for (int n = nb; n < ne; n++) {
-                const int c = a.nbrList[n];
-                double x0, y0, z0, x1, y1, z1;
-                loadBox(a, c, x0, y0, z0, x1, y1, z1);
-                if (x >= x0 && x <= x1 && y >= y0 && y <= y1 && z >= z0 && z <= z1) {
-                    next = c;
-                    r.bx0 = x0; r.by0 = y0; r.bz0 = z0; r.bx1 = x1; r.by1 = y1; r.bz1 = z1;
-                    break;
-                }
-            }
-        }
-        if (next < 0) {
-            next = descend(a, x, y, z);
-            if (next == node) {
-                // stuck: advance to the next representable coordinates (TreeDustGrid.cpp:502-519)
-                x = nextafter(x, (r.dx < 0.0) ? -kDblMax : kDblMax);
-                y = nextafter(y, (r.dy < 0.0) ? -kDblMax : kDblMax);
-                z = nextafter(z, (r.dz < 0.0) ? -kDblMax : kDblMax);
-                next = descend(a, x, y, z);
-                if (next == node) return false;
-            }
-            if (next >= 0) loadBox(a, next, r.bx0, r.by0, r.bz0, r.bx1, r.by1, r.bz1);
-        }
+        const int next = nextNode(a, node, wall, x, y, z, r.dx, r.dy, r.dz);
+        if (next < 0) return false;
+        loadBox(a, next, r.bx0, r.by0, r.bz0, r.bx1, r.by1, r.bz1);
         r.x = x; r.y = y; r.z = z;
         r.ci = next;
-        return next >= 0;
+        r.cj = a.cellnumber[next];
+        return true;
     }
 
     __device__ static __forceinline__ int whichcell(const Args& a, const Shared&, double x, double y, double z) {
         const int l = descend(a, x, y, z);
         return l < 0 ? -1 : a.cellnumber[l];
+    }
+};
+
+// Octree grid through the leaf map. An octree split at box centres (OctTreeNode::createchildren,
+// OctTreeNode.cpp:53-56, Box::center) has, per axis, one table of 2^L + 1 split coordinates T (L the
+// deepest level) such that a level-l node with integer coordinate i spans [T[i << (L-l)],
+// T[(i+1) << (L-l)]] -- bit for bit, since every split is 0.5*(lo+hi) of two table entries. So:
+//   - the box faces come from the T tables in LDS (no box gather);
+//   - the leaf containing a point is the leaf map entry of the finest-level cell holding it: one
+//     16-byte load instead of the neighbour-list walk. Locating by "T[j] <= x < T[j+1]" is exactly
+//     the reference's root descent (x < split -> lower child), so the only steps where it can differ
+//     from the inclusive-box neighbour search (TreeNode::whichnode(wall, r)) are those whose exit point
+//     lies exactly on a lower face of the leaf found, or that have not left the current leaf; those
+//     take the node-array search above. The walk is therefore the reference's, step for step.
+// The host builds the map only after checking every node box against the T tables.
+template <>
+struct Grid<SKIRT_GRID_OCTREE> {
+    using Nodes = Grid<kOctreeNodes>;
+
+    // finest-level index j with T[j] <= v < T[j+1] (the last cell also holds v == T[N]); v in [T[0], T[N]]
+    __device__ static __forceinline__ int finest(const double* T, int N, double inv, double v) {
+        int j = (int)((v - T[0]) * inv);
+        j = max(0, min(N - 1, j));
+        while (j > 0 && v < T[j]) j--;
+        while (j < N - 1 && v >= T[j + 1]) j++;
+        return j;
+    }
+
+    __device__ static __forceinline__ bool inside(const Args& a, double x, double y, double z) {
+        return x >= a.gx0 && x <= a.gx1 && y >= a.gy0 && y <= a.gy1 && z >= a.gz0 && z <= a.gz1;
+    }
+
+    // leaf map entry of the point (inside the grid); fx, fy, fz its finest-level indices
+    __device__ static __forceinline__ LeafEntry lookup(const Args& a, const Shared& sh, double x, double y, double z,
+                                                       int& fx, int& fy, int& fz) {
+        const int N = a.mapN;
+        const double* tx = sh.mesh;
+        fx = finest(tx, N, a.mapInvX, x);
+        fy = finest(tx + (N + 1), N, a.mapInvY, y);
+        fz = finest(tx + 2 * (N + 1), N, a.mapInvZ, z);
+        const int4 v = *reinterpret_cast<const int4*>(a.leafMap + morton3(fx, fy, fz));
+        LeafEntry e;
+        e.node = v.x;
+        e.cl = (unsigned)v.y;
+        const long long bits = ((long long)(unsigned)v.w << 32) | (unsigned)v.z;
+        e.rho0 = __longlong_as_double(bits);
+        return e;
+    }
+
+    __device__ static __forceinline__ void enter(const Args& a, Ray& r, int fx, int fy, int fz, const LeafEntry& e) {
+        const int sh = a.mapL - (int)(e.cl >> kLeafLevelShift);
+        r.ci = e.node;
+        r.cj = (int)(e.cl & kLeafCellMask);
+        r.ck = 1 << sh;
+        r.jx = (fx >> sh) << sh;
+        r.jy = (fy >> sh) << sh;
+        r.jz = (fz >> sh) << sh;
+        r.rho0 = e.rho0;
+    }
+
+    template <class SegFn>
+    __device__ static __forceinline__ bool begin(const Args& a, const Shared& sh, Ray& r, SegFn seg) {
+        double rx = r.x, ry = r.y, rz = r.z, d[3];
+        if (!Nodes::enterGrid(a, rx, ry, rz, r.dx, r.dy, r.dz, d)) return false;
+        if (!inside(a, rx, ry, rz)) return false;  // the root descent finds no node
+        for (int q = 0; q < 3; q++)
+            if (d[q] > 0) seg(-1, 0.0, d[q]);
+        int fx, fy, fz;
+        const LeafEntry e = lookup(a, sh, rx, ry, rz, fx, fy, fz);
+        r.x = rx; r.y = ry; r.z = rz;
+        enter(a, r, fx, fy, fz, e);
+        return true;
+    }
+
+    template <class SegFn>
+    __device__ static __forceinline__ bool step(const Args& a, const Shared& sh, Ray& r, SegFn seg) {
+        const int N1 = a.mapN + 1;
+        const double* tx = sh.mesh;
+        const double* ty = tx + N1;
+        const double* tz = ty + N1;
+        const int sz = r.ck;
+        const double xnext = tx[(r.dx < 0.0) ? r.jx : r.jx + sz];
+        const double ynext = ty[(r.dy < 0.0) ? r.jy : r.jy + sz];
+        const double znext = tz[(r.dz < 0.0) ? r.jz : r.jz + sz];
+        const double dsx = (r.ix != 0.0) ? (xnext - r.x) * r.ix : kDblMax;
+        const double dsy = (r.iy != 0.0) ? (ynext - r.y) * r.iy : kDblMax;
+        const double dsz = (r.iz != 0.0) ? (znext - r.z) * r.iz : kDblMax;
+        double ds;
+        int wall;
+        if (dsx <= dsy && dsx <= dsz) { ds = dsx; wall = (r.dx < 0.0) ? 0 : 1; }
+        else if (dsy <= dsx && dsy <= dsz) { ds = dsy; wall = (r.dy < 0.0) ? 2 : 3; }
+        else { ds = dsz; wall = (r.dz < 0.0) ? 4 : 5; }
+        if (!seg(r.cj, r.rho0, ds)) return false;
+        double x = r.x + (ds + a.eps) * r.dx;
+        double y = r.y + (ds + a.eps) * r.dy;
+        double z = r.z + (ds + a.eps) * r.dz;
+        if (!inside(a, x, y, z)) return false;  // no neighbour and no root descent contains it
+        int fx, fy, fz;
+        LeafEntry e = lookup(a, sh, x, y, z, fx, fy, fz);
+        const int lsh = a.mapL - (int)(e.cl >> kLeafLevelShift);
+        if (e.node == r.ci || x == tx[(fx >> lsh) << lsh] || y == ty[(fy >> lsh) << lsh] || z == tz[(fz >> lsh) << lsh]) {
+            // on a face, or not out of the current leaf: the reference's own search decides
+            const int next = Nodes::nextNode(a, r.ci, wall, x, y, z, r.dx, r.dy, r.dz);
+            if (next < 0) return false;
+            const double* b = a.box + 6 * (size_t)next;  // its lower corner is a finest cell of it
+            e = lookup(a, sh, b[0], b[1], b[2], fx, fy, fz);
+        }
+        r.x = x; r.y = y; r.z = z;
+        enter(a, r, fx, fy, fz, e);
+        return true;
+    }
+
+    __device__ static __forceinline__ int whichcell(const Args& a, const Shared& sh, double x, double y, double z) {
+        if (!inside(a, x, y, z)) return -1;
+        int fx, fy, fz;
+        return (int)(lookup(a, sh, x, y, z, fx, fy, fz).cl & kLeafCellMask);
     }
 };
 
@@ -433,12 +609,12 @@ struct Tracer {
     __device__ __forceinline__ double rho(int m, int h) const { return a.rho[(size_t)m * a.ncomp + h]; }
 
     // per-segment work; false stops the ray (a WALK reached its optical depth)
-    __device__ __forceinline__ bool segment(Ray& r, int m, double ds) {
+    __device__ __forceinline__ bool segment(Ray& r, int m, double rho0, double ds) {
         if (!(ds > 0)) return true;  // DustGridPath::addSegment skips ds <= 0
         r.s += ds;
         double kr = 0.0;  // KappaRho functor (DustSystem.cpp:465-491)
         if (m >= 0) {
-            if (ONECOMP) kr = r.kext * a.rho[m];
+            if (ONECOMP) kr = r.kext * rho0;
             else for (int h = 0; h < a.ncomp; h++) kr += sh.kext[h * a.nlambda + r.ell] * rho(m, h);
         }
         const double dtau = kr * ds;
@@ -493,7 +669,7 @@ struct Tracer {
         r.kext = sh.kext[r.ell];
         r.f1 = (r.mode == RAY_FILL) ? 1.0 : 0.0;
         r.f2 = 0;
-        return Grid<GRID>::begin(a, sh, r, [&](int m, double ds) { return segment(r, m, ds); });
+        return Grid<GRID>::begin(a, sh, r, [&](int m, double rho0, double ds) { return segment(r, m, rho0, ds); });
     }
 
     // the ray ended (grid edge, empty path or WALK target reached): deliver its result
@@ -544,10 +720,37 @@ struct Tracer {
     }
 };
 
+// fills the leaf map: one thread per finest-level cell descends the (checked) tree by its index bits
+__global__ void __launch_bounds__(kBlock) buildLeafMapKernel(LeafEntry* map, const int* firstChild, const int* cellnumber,
+                                                             const double* rho, int ncomp, int L) {
+    const unsigned long long n = 1ull << (3 * L);
+    for (unsigned long long q = blockIdx.x * (unsigned long long)blockDim.x + threadIdx.x; q < n;
+         q += (unsigned long long)gridDim.x * blockDim.x) {
+        unsigned fx = 0, fy = 0, fz = 0;
+        for (int b = 0; b < L; b++) {  // inverse Morton
+            fx |= (unsigned)((q >> (3 * b)) & 1u) << b;
+            fy |= (unsigned)((q >> (3 * b + 1)) & 1u) << b;
+            fz |= (unsigned)((q >> (3 * b + 2)) & 1u) << b;
+        }
+        int node = 0, level = 0;
+        while (firstChild[node] >= 0) {
+            const int bit = L - 1 - level;
+            node = firstChild[node] + (int)((fx >> bit) & 1u) + 2 * (int)((fy >> bit) & 1u) + 4 * (int)((fz >> bit) & 1u);
+            level++;
+        }
+        const int cell = cellnumber[node];
+        LeafEntry e;
+        e.node = node;
+        e.cl = (unsigned)cell | ((unsigned)level << kLeafLevelShift);
+        e.rho0 = rho[(size_t)cell * ncomp];
+        map[q] = e;
+    }
+}
+
 template <int GRID, bool ONECOMP>
-__global__ void __launch_bounds__(kBlock) traceKernel(const Args a) {
+__global__ void __launch_bounds__(kBlock) SKIRT_TRACE_ATTR traceKernel(const Args a) {
     extern __shared__ __attribute__((aligned(16))) double lds[];
-    Shared sh = stageTables(a, lds, GRID == SKIRT_GRID_CARTESIAN);
+    Shared sh = stageTables(a, lds, GRID == SKIRT_GRID_CARTESIAN, GRID == SKIRT_GRID_OCTREE);
     for (int q = threadIdx.x; q < a.nsed; q += blockDim.x) sh.sed[q] = 0.0;
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         // reset the counters the next event iteration appends to (nobody else uses them now)
@@ -592,7 +795,7 @@ __global__ void __launch_bounds__(kBlock) traceKernel(const Args a) {
 #pragma unroll 1
         for (int it = 0; it < 4; it++) {
             if (r.mode != RAY_NONE) {
-                if (!Grid<GRID>::step(a, sh, r, [&](int m, double ds) { return T.segment(r, m, ds); })) {
+                if (!Grid<GRID>::step(a, sh, r, [&](int m, double rho0, double ds) { return T.segment(r, m, rho0, ds); })) {
                     T.finish(r);
                     r.mode = RAY_NONE;
                 }
@@ -825,7 +1028,7 @@ enum PeelKind : int { PEEL_NONE = 0, PEEL_EMISSION = 1, PEEL_SCATTER = 2 };
 template <int GRID, bool ONECOMP>
 __global__ void __launch_bounds__(kBlock) eventKernel(const Args a) {
     extern __shared__ __attribute__((aligned(16))) double lds[];
-    Shared sh = stageTables(a, lds, GRID == SKIRT_GRID_CARTESIAN);
+    Shared sh = stageTables(a, lds, GRID == SKIRT_GRID_CARTESIAN, GRID == SKIRT_GRID_OCTREE);
     if (blockIdx.x == 0 && threadIdx.x == 0) a.ctr[4] = 0;  // the trace kernel's pull counter
     Events<GRID, ONECOMP> E{a, sh};
     const int lane = threadIdx.x & 63;
@@ -1001,6 +1204,12 @@ struct SkirtMcrt {
     double* dMesh = nullptr;
     double* dBox = nullptr;
     int *dFirstChild = nullptr, *dCellnumber = nullptr, *dNbrOffset = nullptr, *dNbrList = nullptr;
+    // octree leaf map (mapL < 0: walk the node arrays)
+    int mapL = -1, mapN = 0;
+    double mapInv[3] = {0, 0, 0};
+    double* dTreeT = nullptr;
+    LeafEntry* dLeafMap = nullptr;
+    bool mapReady = false;
     // media
     int ncomp = 0, nlambda = 0;
     double *dRho = nullptr, *dOptics = nullptr;
@@ -1079,6 +1288,75 @@ void carvePool(SkirtMcrt* c, Args& a) {
     takeU(a.splo); takeU(a.sphi); takeU(a.sblock); takeU(a.sw2); takeU(a.sw3); takeU(a.shave);
     takeI(a.act[0]); takeI(a.act[1]);
     a.nslots = c->nslots;
+}
+
+
+// Decides whether the octree can be walked through a leaf map (Grid<SKIRT_GRID_OCTREE>): every node
+// box must equal the box its level and integer coordinates give in the per-axis split tables, and the
+// tree must be at most kMaxMapLevel deep. Uploads the tables; the map itself is built at the first
+// phase (it caches the densities). SKIRT_AMD_LEAFMAP=0 forces the node-array walk.
+int planLeafMap(SkirtMcrt* c, const SkirtGridDesc* g) {
+    c->mapL = -1;
+    c->mapReady = false;
+    if (c->dLeafMap) { (void)hipFree(c->dLeafMap); c->dLeafMap = nullptr; }
+    const char* env = getenv("SKIRT_AMD_LEAFMAP");
+    if (env && env[0] == '0') return SKIRT_OK;
+    if (g->ncells >= (int)(1u << kLeafLevelShift)) return SKIRT_OK;
+    struct Item { int node, level, ix, iy, iz; };
+    std::vector<Item> stack{{0, 0, 0, 0, 0}};
+    std::vector<Item> nodes;
+    nodes.reserve(g->nnodes);
+    int L = 0;
+    while (!stack.empty()) {
+        const Item it = stack.back();
+        stack.pop_back();
+        nodes.push_back(it);
+        L = std::max(L, it.level);
+        if (L > kMaxMapLevel) return SKIRT_OK;
+        const int fc = g->first_child[it.node];
+        if (fc >= 0)
+            for (int k = 0; k < 8; k++)
+                stack.push_back({fc + k, it.level + 1, 2 * it.ix + (k & 1), 2 * it.iy + ((k >> 1) & 1), 2 * it.iz + ((k >> 2) & 1)});
+    }
+    if ((int)nodes.size() != g->nnodes) return SKIRT_OK;  // not a tree reachable from node 0
+    const int N = 1 << L;
+    std::vector<double> T(3 * (size_t)(N + 1));
+    for (int ax = 0; ax < 3; ax++) {
+        double* t = T.data() + ax * (N + 1);
+        t[0] = g->box[ax];
+        t[N] = g->box[3 + ax];
+        for (int w = N; w > 1; w >>= 1)  // Box::center of every node, coarse to fine
+            for (int lo = 0; lo < N; lo += w) t[lo + w / 2] = 0.5 * (t[lo] + t[lo + w]);
+        for (int j = 0; j < N; j++)
+            if (!(t[j] < t[j + 1])) return SKIRT_OK;
+    }
+    for (const Item& it : nodes) {
+        const int sh = L - it.level;
+        const int idx[3] = {it.ix, it.iy, it.iz};
+        const double* b = g->box + 6 * (size_t)it.node;
+        for (int ax = 0; ax < 3; ax++) {
+            const double* t = T.data() + ax * (N + 1);
+            if (b[ax] != t[idx[ax] << sh] || b[3 + ax] != t[(idx[ax] + 1) << sh]) return SKIRT_OK;
+        }
+    }
+    int rc = upload(c, c->dTreeT, T.data(), T.size());
+    if (rc) return rc;
+    c->mapL = L;
+    c->mapN = N;
+    for (int ax = 0; ax < 3; ax++) c->mapInv[ax] = N / (g->box[3 + ax] - g->box[ax]);
+    return SKIRT_OK;
+}
+
+int ensureLeafMap(SkirtMcrt* c) {
+    if (c->mapL < 0 || c->mapReady) return SKIRT_OK;
+    const size_t n = (size_t)1 << (3 * c->mapL);
+    if (!c->dLeafMap) HIPCHECK(c, hipMalloc(&c->dLeafMap, n * sizeof(LeafEntry)));
+    const int blocks = (int)std::min<size_t>((n + kBlock - 1) / kBlock, 65536);
+    hipLaunchKernelGGL(buildLeafMapKernel, dim3(blocks), dim3(kBlock), 0, c->stream, c->dLeafMap, c->dFirstChild,
+                       c->dCellnumber, c->dRho, std::max(1, c->ncomp), c->mapL);
+    HIPCHECK(c, hipGetLastError());
+    c->mapReady = true;
+    return SKIRT_OK;
 }
 
 }  // namespace
@@ -1177,6 +1455,7 @@ int skirt_mcrt_upload_grid(SkirtMcrt* c, const SkirtGridDesc* g) {
         if ((rc = upload(c, c->dNbrOffset, g->nbr_offset, 6 * (size_t)g->nnodes + 1))) return rc;
         std::vector<int> dummy(1, 0);
         if ((rc = upload(c, c->dNbrList, nnbr ? g->nbr_list : dummy.data(), nnbr ? (size_t)nnbr : 1))) return rc;
+        if ((rc = planLeafMap(c, g))) return rc;
     } else {
         return fail(c, SKIRT_ERR_UNSUPPORTED, "unsupported grid kind");
     }
@@ -1191,6 +1470,7 @@ int skirt_mcrt_upload_media(SkirtMcrt* c, const SkirtMediaDesc* m) {
         return fail(c, SKIRT_ERR_ARG, "media sizes do not match the grid (1 <= ncomp <= 8)");
     if (m->nlambda >= (1 << 14)) return fail(c, SKIRT_ERR_ARG, "at most 16383 wavelengths");
     HIPCHECK(c, hipSetDevice(c->device));
+    c->mapReady = false;  // the leaf map caches the densities
     c->ncomp = m->ncomp;
     c->nlambda = m->nlambda;
     const size_t nt = (size_t)m->ncomp * m->nlambda;
@@ -1348,6 +1628,12 @@ int skirt_mcrt_run_stellar(SkirtMcrt* c, uint64_t npp, uint64_t first, uint64_t 
     a.gx0 = c->gx0; a.gx1 = c->gx1; a.gy0 = c->gy0; a.gy1 = c->gy1; a.gz0 = c->gz0; a.gz1 = c->gz1;
     a.box = c->dBox; a.firstChild = c->dFirstChild; a.cellnumber = c->dCellnumber;
     a.nbrOffset = c->dNbrOffset; a.nbrList = c->dNbrList; a.eps = c->eps; a.search = c->search;
+    const bool leafMap = c->gridKind == SKIRT_GRID_OCTREE && c->mapL >= 0 && p->has_dust;
+    if (leafMap) {
+        if ((rc = ensureLeafMap(c))) return rc;
+        a.leafMap = c->dLeafMap; a.treeT = c->dTreeT; a.mapL = c->mapL; a.mapN = c->mapN;
+        a.mapInvX = c->mapInv[0]; a.mapInvY = c->mapInv[1]; a.mapInvZ = c->mapInv[2];
+    }
     a.ncomp = std::max(1, c->ncomp); a.nlambda = c->nlambda;
     a.rho = c->dRho;
     a.optics = c->dOptics;
@@ -1368,6 +1654,7 @@ int skirt_mcrt_run_stellar(SkirtMcrt* c, uint64_t npp, uint64_t first, uint64_t 
     int off = 0;
     a.ldsMeshOff = off;
     off += (c->gridKind == SKIRT_GRID_CARTESIAN && a.hasDust) ? (c->nx + c->ny + c->nz + 3) : 0;
+    off += leafMap ? 3 * (c->mapN + 1) : 0;
     off = (off + 1) & ~1;
     a.ldsOptOff = off;
     off += 4 * a.ncomp * a.nlambda;
@@ -1378,10 +1665,13 @@ int skirt_mcrt_run_stellar(SkirtMcrt* c, uint64_t npp, uint64_t first, uint64_t 
     off += c->nsed;
     const size_t lds = (size_t)off * sizeof(double);
     if (lds > 64 * 1024) return fail(c, SKIRT_ERR_UNSUPPORTED, "tables do not fit in LDS (" + std::to_string(lds) + " bytes)");
-    const bool octree = c->gridKind == SKIRT_GRID_OCTREE;
+    const int kind = c->gridKind == SKIRT_GRID_CARTESIAN ? SKIRT_GRID_CARTESIAN : (leafMap ? SKIRT_GRID_OCTREE : kOctreeNodes);
     const bool one = a.ncomp == 1;
-    auto traceFn = octree ? (one ? (const void*)traceKernel<SKIRT_GRID_OCTREE, true> : (const void*)traceKernel<SKIRT_GRID_OCTREE, false>)
-                          : (one ? (const void*)traceKernel<SKIRT_GRID_CARTESIAN, true> : (const void*)traceKernel<SKIRT_GRID_CARTESIAN, false>);
+    const void* traceFn = nullptr;
+    auto pick = [&](auto fn1, auto fnN) { traceFn = one ? (const void*)fn1 : (const void*)fnN; };
+    if (kind == SKIRT_GRID_CARTESIAN) pick(traceKernel<SKIRT_GRID_CARTESIAN, true>, traceKernel<SKIRT_GRID_CARTESIAN, false>);
+    else if (kind == SKIRT_GRID_OCTREE) pick(traceKernel<SKIRT_GRID_OCTREE, true>, traceKernel<SKIRT_GRID_OCTREE, false>);
+    else pick(traceKernel<kOctreeNodes, true>, traceKernel<kOctreeNodes, false>);
     int tgrid = c->traceGrid;
     if (tgrid <= 0) {
         int per = 0;
@@ -1394,22 +1684,18 @@ int skirt_mcrt_run_stellar(SkirtMcrt* c, uint64_t npp, uint64_t first, uint64_t 
     HIPCHECK(c, hipMemsetAsync(c->dCtr, 0, 8 * sizeof(unsigned int), c->stream));
     HIPCHECK(c, hipEventRecord(c->ev0, c->stream));
     auto launchEvent = [&](const Args& aa) {
-        if (octree) {
-            if (one) hipLaunchKernelGGL((eventKernel<SKIRT_GRID_OCTREE, true>), dim3(egrid), dim3(kBlock), lds, c->stream, aa);
-            else hipLaunchKernelGGL((eventKernel<SKIRT_GRID_OCTREE, false>), dim3(egrid), dim3(kBlock), lds, c->stream, aa);
-        } else {
-            if (one) hipLaunchKernelGGL((eventKernel<SKIRT_GRID_CARTESIAN, true>), dim3(egrid), dim3(kBlock), lds, c->stream, aa);
-            else hipLaunchKernelGGL((eventKernel<SKIRT_GRID_CARTESIAN, false>), dim3(egrid), dim3(kBlock), lds, c->stream, aa);
-        }
+#define SKIRT_EVENT(G, O) hipLaunchKernelGGL((eventKernel<G, O>), dim3(egrid), dim3(kBlock), lds, c->stream, aa)
+        if (kind == SKIRT_GRID_CARTESIAN) { if (one) SKIRT_EVENT(SKIRT_GRID_CARTESIAN, true); else SKIRT_EVENT(SKIRT_GRID_CARTESIAN, false); }
+        else if (kind == SKIRT_GRID_OCTREE) { if (one) SKIRT_EVENT(SKIRT_GRID_OCTREE, true); else SKIRT_EVENT(SKIRT_GRID_OCTREE, false); }
+        else { if (one) SKIRT_EVENT(kOctreeNodes, true); else SKIRT_EVENT(kOctreeNodes, false); }
+#undef SKIRT_EVENT
     };
     auto launchTrace = [&](const Args& aa) {
-        if (octree) {
-            if (one) hipLaunchKernelGGL((traceKernel<SKIRT_GRID_OCTREE, true>), dim3(tgrid), dim3(kBlock), lds, c->stream, aa);
-            else hipLaunchKernelGGL((traceKernel<SKIRT_GRID_OCTREE, false>), dim3(tgrid), dim3(kBlock), lds, c->stream, aa);
-        } else {
-            if (one) hipLaunchKernelGGL((traceKernel<SKIRT_GRID_CARTESIAN, true>), dim3(tgrid), dim3(kBlock), lds, c->stream, aa);
-            else hipLaunchKernelGGL((traceKernel<SKIRT_GRID_CARTESIAN, false>), dim3(tgrid), dim3(kBlock), lds, c->stream, aa);
-        }
+#define SKIRT_TRACE(G, O) hipLaunchKernelGGL((traceKernel<G, O>), dim3(tgrid), dim3(kBlock), lds, c->stream, aa)
+        if (kind == SKIRT_GRID_CARTESIAN) { if (one) SKIRT_TRACE(SKIRT_GRID_CARTESIAN, true); else SKIRT_TRACE(SKIRT_GRID_CARTESIAN, false); }
+        else if (kind == SKIRT_GRID_OCTREE) { if (one) SKIRT_TRACE(SKIRT_GRID_OCTREE, true); else SKIRT_TRACE(SKIRT_GRID_OCTREE, false); }
+        else { if (one) SKIRT_TRACE(kOctreeNodes, true); else SKIRT_TRACE(kOctreeNodes, false); }
+#undef SKIRT_TRACE
     };
     // iteration it (parity q = it & 1): the event kernel consumes active list ctr[2+q] and queues rays
     // into ctr[q] and the next active list into ctr[2+1-q]; the trace kernel walks the ctr[q] rays and
@@ -1491,7 +1777,8 @@ void skirt_mcrt_destroy(SkirtMcrt* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    void* bufs[] = {c->dMesh, c->dBox, c->dFirstChild, c->dCellnumber, c->dNbrOffset, c->dNbrList, c->dRho,
+    void* bufs[] = {c->dMesh, c->dBox, c->dFirstChild, c->dCellnumber, c->dNbrOffset, c->dNbrList, c->dTreeT,
+                    c->dLeafMap, c->dRho,
                     c->dOptics, c->dGeomParam, c->dLum, c->dLumtot, c->dCdf, c->dInstr,
                     c->dClaim, c->dStats, c->dError, c->dCtr, c->dPool};
     for (void* b : bufs)

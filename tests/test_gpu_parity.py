@@ -62,6 +62,32 @@ def test_engine_matches_oracle_same_streams(name, packages):
             assert close_fraction(frames, orc.frames[i], 1e-9) > 0.999
 
 
+@pytest.mark.parametrize("path,packages", [(os.path.join("tests", "golden", "ski", "pan_oct.ski"), 3000),
+                                           (os.path.join("benchmarks", "c3_oct128.ski"), 40)])
+def test_leaf_map_walk_equals_node_walk(path, packages, monkeypatch):
+    """The octree leaf-map walk takes exactly the reference's steps: the same segment, absorption and
+    detection counts as the node-array walk (TreeNode neighbour search), and the same tallies up to the
+    order of the f64 atomic additions."""
+    full = os.path.join(os.path.dirname(GOLD), "..", path)
+    runs = []
+    for leafmap in ("1", "0"):
+        monkeypatch.setenv("SKIRT_AMD_LEAFMAP", leafmap)
+        sim = S.Simulation(full, packages=packages)
+        sim.attach(0)
+        sim.run_stellar()
+        sim.fetch()
+        runs.append(sim)
+    a, b = runs
+    sa, sb = a.stats(), b.stats()
+    for k in ("packets", "segments_fill", "segments_walk", "segments_peel", "detects", "absorb_adds"):
+        assert sa[k] == sb[k], (k, sa[k], sb[k])
+    np.testing.assert_allclose(a.labs(), b.labs(), rtol=1e-10, atol=1e-300)
+    fa, da = a.instrument(0)
+    fb, db = b.instrument(0)
+    np.testing.assert_allclose(da, db, rtol=1e-10, atol=1e-300)
+    np.testing.assert_allclose(fa, fb, rtol=1e-10, atol=1e-300)
+
+
 def test_sharded_packet_ranges_sum_to_the_whole():
     """Two disjoint packet ranges (as two GPUs would run) add up to the full run exactly."""
     name = "pan_cart16"
