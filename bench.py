@@ -127,7 +127,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    delta = {k: s1[k] - s0[k] for k in s1 if k != "kernel_ms"}
+    delta = {k: s1[k] - s0[k] for k in s1 if k not in ("kernel_ms", "iterations")}
     packets_all = share * world * args.steps
     value = packets_all / elapsed
     avg_kernel_s = sum(kernel_ms) / len(kernel_ms) / 1e3
@@ -157,6 +157,10 @@ def main():
             "packets_per_step_per_gpu": share,
             "parallelism": "dp%d (packet sharding, RCCL all-reduce of Labs + instrument tallies per phase)" % world,
             "segments_per_packet": segs / max(1, delta["packets"]),
+            "lane_use": (delta["segments_fill"] + delta["segments_walk"] + delta["segments_peel"]) / max(1, delta["lane_slots"]),
+            "iterations": s1["iterations"],
+            "per_packet": {k: delta[k] / max(1, delta["packets"]) for k in
+                           ("segments_fill", "segments_walk", "segments_peel", "absorb_adds", "detects")},
         },
         "roofline": {
             "bound": "hbm",
@@ -165,7 +169,7 @@ def main():
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
             "traffic": None,
-            "kernel": "stellarKernel<octree>" if info.grid_kind == 1 else "stellarKernel<cartesian>",
+            "kernel": "traceKernel<octree leaf map>" if info.grid_kind == 1 else "traceKernel<cartesian>",
             "kernel_ms_avg": avg_kernel_s * 1e3,
             "algorithmic_bytes_per_launch": bytes_per_launch,
         },

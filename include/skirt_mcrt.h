@@ -119,6 +119,8 @@ typedef struct {
     uint64_t segments_peel;     /* segments walked by peel-off optical depth passes */
     uint64_t detects;           /* peel-off detections */
     uint64_t absorb_adds;       /* Labs atomic updates */
+    uint64_t lane_slots;        /* trace kernel: 64 x wave steps (segments / lane_slots = SIMD lane use) */
+    uint64_t iterations;        /* event/trace iterations of the last run call */
     double kernel_ms;           /* device time of the last run call (HIP events on the engine stream) */
 } SkirtStats;
 
@@ -144,8 +146,9 @@ int skirt_mcrt_synchronize(SkirtMcrt* ctx);
 /* Copies tallies to host (Labs converted to row-major cell x wavelength); either pointer may be NULL. */
 int skirt_mcrt_download(SkirtMcrt* ctx, double* labs, double* instr);
 int skirt_mcrt_stats(SkirtMcrt* ctx, SkirtStats* out);
-/* kernel configuration knobs (0 = default): threads per block, blocks, event batching threshold */
-int skirt_mcrt_configure(SkirtMcrt* ctx, int block, int grid, int event_threshold);
+/* engine knobs (0 = default): packet slots in flight, trace-kernel workgroups, and the number of idle
+ * lanes at which a trace wave pulls new rays (1..64) */
+int skirt_mcrt_configure(SkirtMcrt* ctx, int slots, int grid, int pull_threshold);
 const char* skirt_mcrt_last_error(SkirtMcrt* ctx);
 void skirt_mcrt_destroy(SkirtMcrt* ctx);
 

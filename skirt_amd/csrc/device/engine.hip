@@ -41,6 +41,8 @@ namespace {
 
 constexpr double kDblMax = 1.7976931348623157e308;
 constexpr int kBlock = 256;
+constexpr int kLabsBuf = 8;        // buffered Labs adds per trace lane (LDS)
+constexpr int kStepsPerPull = 4;   // grid steps between two ray pulls of a trace wave
 // occupancy attribute of the trace kernel (a build knob for tuning variants, tools/build_variant.sh)
 #ifndef SKIRT_TRACE_ATTR
 #define SKIRT_TRACE_ATTR
@@ -61,13 +63,21 @@ enum State : int { S_NEW = 0, S_FILL = 2, S_WALK = 3 };
 // peel-off categories (which FullInstrument arrays a detection adds to, FullInstrument.cpp:115-171)
 enum PeelCat : unsigned { CAT_STAR_DIRECT = 0, CAT_STAR_SCATTERED = 1, CAT_DUST_DIRECT = 2, CAT_DUST_SCATTERED = 3 };
 
-// one queued ray, 64 bytes
-struct RayRec {
-    double x, y, z, dx, dy, dz;
-    double param;    // FILL: packet luminosity L; WALK: optical depth to reach; PEEL: peel-off luminosity
-    int idx;         // FILL/WALK: slot; PEEL: frame pixel (-1: none)
-    unsigned flags;  // mode | cat << 2 | instrument << 4 | scattering level << 10 | ell << 18
+// one queued ray, 128 bytes = 8 x 16-byte chunks. The event kernel writes it already entered into the
+// grid (the part of the path before the grid, the first cell and the reciprocal direction computed), so
+// the trace kernel starts stepping at once.
+struct __attribute__((aligned(16))) RayRec {
+    double x, y, z;        // c0-c1: entry point (inside the grid)
+    double dx, dy, dz;     // c1-c2: direction
+    double ix, iy, iz;     // c3-c4: 1/direction (0 where |k| <= 1e-15: that axis is never crossed)
+    double s0;             // c4: path length before the entry point; a finished PEEL ray: optical depth
+    double rho0;           // c5: density (component 0) of the entry cell
+    double param;          // c5: FILL: packet luminosity L; WALK: optical depth to reach; PEEL: peel-off L
+    int idx;               // c6: FILL/WALK: slot; PEEL: frame pixel (-1: none)
+    unsigned flags;        // c6: mode | cat << 2 | instrument << 4 | scattering level << 10 | ell << 18
+    int ci, cj, ck, jx, jy, jz;  // c6-c7: grid position of the entry cell (see Ray)
 };
+static_assert(sizeof(RayRec) == 128, "ray record layout");
 __device__ __forceinline__ unsigned rayMode(unsigned f) { return f & 3u; }
 __device__ __forceinline__ unsigned rayCat(unsigned f) { return (f >> 2) & 3u; }
 __device__ __forceinline__ int rayInstr(unsigned f) { return (int)((f >> 4) & 63u); }
@@ -122,7 +132,7 @@ struct Args {
     double* labs;                // [nlambda][ncells]
     double* tally;
     unsigned int* error;
-    unsigned long long* stats;   // packets, seg_fill, seg_walk, seg_peel, detects, absorbs
+    unsigned long long* stats;   // packets, seg_fill, seg_walk, seg_peel, detects, absorbs, lane slots
     // slot pool (structure of arrays) and queues
     int nslots;
     double *srx, *sry, *srz, *skx, *sky, *skz, *sL, *sLth;
@@ -179,7 +189,9 @@ struct Shared {
     double* sed;
 };
 
-__device__ __forceinline__ Shared stageTables(const Args& a, double* lds, bool mesh, bool tree) {
+enum StageParts : int { STAGE_MESH = 1, STAGE_TREE = 2, STAGE_OPTICS = 4, STAGE_INSTR = 8 };
+
+__device__ __forceinline__ Shared stageTables(const Args& a, double* lds, int parts) {
     Shared sh;
     double* m = lds + a.ldsMeshOff;
     double* opt = lds + a.ldsOptOff;
@@ -191,23 +203,28 @@ __device__ __forceinline__ Shared stageTables(const Args& a, double* lds, bool m
     sh.g = opt + 3 * a.ncomp * a.nlambda;
     sh.instr = reinterpret_cast<const DevInstr*>(idst);
     sh.sed = lds + a.ldsSedOff;
-    const int nmesh = mesh ? (a.nx + a.ny + a.nz + 3) : 0;
+    const int nmesh = (parts & STAGE_MESH) ? (a.nx + a.ny + a.nz + 3) : 0;
     for (int q = threadIdx.x; q < nmesh; q += blockDim.x) m[q] = a.mesh[q];
-    const int ntree = tree ? 3 * (a.mapN + 1) : 0;
+    const int ntree = (parts & STAGE_TREE) ? 3 * (a.mapN + 1) : 0;
     for (int q = threadIdx.x; q < ntree; q += blockDim.x) m[q] = a.treeT[q];
-    const int nopt = 4 * a.ncomp * a.nlambda;
+    const int nopt = (parts & STAGE_OPTICS) ? 4 * a.ncomp * a.nlambda : 0;
     for (int q = threadIdx.x; q < nopt; q += blockDim.x) opt[q] = a.optics[q];
-    const int ninw = a.ninstr * (int)(sizeof(DevInstr) / sizeof(double));
+    const int ninw = (parts & STAGE_INSTR) ? a.ninstr * (int)(sizeof(DevInstr) / sizeof(double)) : 0;
     const double* isrc = reinterpret_cast<const double*>(a.instr);
     for (int q = threadIdx.x; q < ninw; q += blockDim.x) idst[q] = isrc[q];
     __syncthreads();
     return sh;
 }
 
-__device__ __forceinline__ void flushStats(const Args& a, const unsigned long long (&vals)[6]) {
+template <int GRID>
+__device__ __forceinline__ constexpr int gridParts() {
+    return GRID == SKIRT_GRID_CARTESIAN ? STAGE_MESH : (GRID == SKIRT_GRID_OCTREE ? STAGE_TREE : 0);
+}
+
+__device__ __forceinline__ void flushStats(const Args& a, const unsigned long long (&vals)[7]) {
     const int lane = threadIdx.x & 63;
 #pragma unroll
-    for (int q = 0; q < 6; q++) {
+    for (int q = 0; q < 7; q++) {
         unsigned long long v = vals[q];
         for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
         if (lane == 0 && v) atomicAdd(a.stats + q, v);
@@ -229,6 +246,7 @@ struct Ray {
     int jx, jy, jz;        // octree leaf map: finest-level index of the current leaf's lower corner
     int idx, ell;
     unsigned flags, mode;
+    unsigned id;           // queue index of the ray (a PEEL ray writes its optical depth back there)
 };
 
 // ------------------------------------------------------------------ grids
@@ -341,6 +359,8 @@ struct Grid<SKIRT_GRID_CARTESIAN> {
         }
         return true;
     }
+
+    __device__ static __forceinline__ void resume(const Args&, Ray&) {}
 
     __device__ static __forceinline__ int whichcell(const Args& a, const Shared& sh, double x, double y, double z) {
         const double* xv = sh.mesh;
@@ -477,6 +497,10 @@ struct Grid<kOctreeNodes> {
         return true;
     }
 
+    __device__ static __forceinline__ void resume(const Args& a, Ray& r) {
+        loadBox(a, r.ci, r.bx0, r.by0, r.bz0, r.bx1, r.by1, r.bz1);
+    }
+
     __device__ static __forceinline__ int whichcell(const Args& a, const Shared&, double x, double y, double z) {
         const int l = descend(a, x, y, z);
         return l < 0 ? -1 : a.cellnumber[l];
@@ -499,12 +523,17 @@ template <>
 struct Grid<SKIRT_GRID_OCTREE> {
     using Nodes = Grid<kOctreeNodes>;
 
-    // finest-level index j with T[j] <= v < T[j+1] (the last cell also holds v == T[N]); v in [T[0], T[N]]
+    // finest-level index j with T[j] <= v < T[j+1] (the last cell also holds v == T[N]); v in [T[0], T[N]].
+    // The split coordinates are uniform to rounding, so the estimate is off by one at most near a
+    // split; the loops only run for that rare lane.
     __device__ static __forceinline__ int finest(const double* T, int N, double inv, double v) {
-        int j = (int)((v - T[0]) * inv);
-        j = max(0, min(N - 1, j));
-        while (j > 0 && v < T[j]) j--;
-        while (j < N - 1 && v >= T[j + 1]) j++;
+        int j = max(0, min(N - 1, (int)((v - T[0]) * inv)));
+        const double lo = T[j], hi = T[j + 1];
+        if (v < lo) {
+            do j--; while (j > 0 && v < T[j]);
+        } else if (v >= hi && j < N - 1) {
+            do j++; while (j < N - 1 && v >= T[j + 1]);
+        }
         return j;
     }
 
@@ -520,7 +549,9 @@ struct Grid<SKIRT_GRID_OCTREE> {
         fx = finest(tx, N, a.mapInvX, x);
         fy = finest(tx + (N + 1), N, a.mapInvY, y);
         fz = finest(tx + 2 * (N + 1), N, a.mapInvZ, z);
-        const int4 v = *reinterpret_cast<const int4*>(a.leafMap + morton3(fx, fy, fz));
+        int4 v = *reinterpret_cast<const int4*>(a.leafMap + morton3(fx, fy, fz));
+        // one 16-byte load: keep the compiler from splitting off the density into a later second load
+        asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w));
         LeafEntry e;
         e.node = v.x;
         e.cl = (unsigned)v.y;
@@ -592,6 +623,8 @@ struct Grid<SKIRT_GRID_OCTREE> {
         return true;
     }
 
+    __device__ static __forceinline__ void resume(const Args&, Ray&) {}
+
     __device__ static __forceinline__ int whichcell(const Args& a, const Shared& sh, double x, double y, double z) {
         if (!inside(a, x, y, z)) return -1;
         int fx, fy, fz;
@@ -604,7 +637,20 @@ template <int GRID, bool ONECOMP>
 struct Tracer {
     const Args& a;
     const Shared& sh;
-    unsigned int segFill = 0, segWalk = 0, segPeel = 0, detects = 0, absorbs = 0;
+    unsigned int segFill = 0, segWalk = 0, segPeel = 0, absorbs = 0, laneSlots = 0;
+    // Labs adds of this lane not yet issued: scattered f64 atomics run memory-side at a fixed chip-wide
+    // rate and every one stays in the wave's in-order vmcnt, so a wave that issued one per step would
+    // wait for its acknowledgement at every step. Buffered in LDS (kLabsBuf per lane) and issued in
+    // bursts, a wave waits for one round trip per burst.
+    double* pendVal;
+    unsigned* pendIdx;
+    int npend = 0;
+
+    __device__ __forceinline__ void drain() {
+        for (int j = 0; j < kLabsBuf; j++)
+            if (j < npend) atomicAddF64(a.labs + pendIdx[j * kBlock], pendVal[j * kBlock]);
+        npend = 0;
+    }
 
     __device__ __forceinline__ double rho(int m, int h) const { return a.rho[(size_t)m * a.ncomp + h]; }
 
@@ -638,7 +684,9 @@ struct Tracer {
                     r.f2 += albedo * Lintm;
                 }
                 if (a.store) {
-                    atomicAddF64(a.labs + (size_t)r.ell * a.ncells + m, (1.0 - albedo) * Lintm);
+                    pendVal[npend * kBlock] = (1.0 - albedo) * Lintm;
+                    pendIdx[npend * kBlock] = (unsigned)r.ell * (unsigned)a.ncells + (unsigned)m;
+                    npend++;
                     absorbs++;
                 }
             }
@@ -653,56 +701,37 @@ struct Tracer {
         return true;
     }
 
-    // load a queued ray and walk its entry part; false for an empty path
-    __device__ __forceinline__ bool start(Ray& r, const RayRec& q) {
-        r.x = q.x; r.y = q.y; r.z = q.z;
-        r.dx = q.dx; r.dy = q.dy; r.dz = q.dz;
-        r.param = q.param;
-        r.idx = q.idx;
-        r.flags = q.flags;
-        r.mode = rayMode(q.flags);
-        r.ell = rayEll(q.flags);
-        r.ix = (fabs(r.dx) > 1e-15) ? 1.0 / r.dx : 0.0;
-        r.iy = (fabs(r.dy) > 1e-15) ? 1.0 / r.dy : 0.0;
-        r.iz = (fabs(r.dz) > 1e-15) ? 1.0 / r.dz : 0.0;
-        r.tau = 0; r.s = 0;
+    // load queued ray `id` (already entered into the grid by the event kernel)
+    __device__ __forceinline__ void load(Ray& r, unsigned id) {
+        const double2* c = reinterpret_cast<const double2*>(a.rays + id);
+        const double2 c0 = c[0], c1 = c[1], c2 = c[2], c3 = c[3], c4 = c[4], c5 = c[5];
+        const int4 c6 = reinterpret_cast<const int4*>(c)[6];
+        const int4 c7 = reinterpret_cast<const int4*>(c)[7];
+        r.id = id;
+        r.x = c0.x; r.y = c0.y; r.z = c1.x;
+        r.dx = c1.y; r.dy = c2.x; r.dz = c2.y;
+        r.ix = c3.x; r.iy = c3.y; r.iz = c4.x;
+        r.rho0 = c5.x;
+        r.param = c5.y;
+        r.idx = c6.x;
+        r.flags = (unsigned)c6.y;
+        r.ci = c6.z; r.cj = c6.w; r.ck = c7.x;
+        r.jx = c7.y; r.jy = c7.z; r.jz = c7.w;
+        r.mode = rayMode(r.flags);
+        r.ell = rayEll(r.flags);
+        r.tau = 0;
+        r.s = c4.y;
         r.kext = sh.kext[r.ell];
+        // FILL: f1 = exp(-tau) = 1, f2 = scattered luminosity; WALK: tau and s at the last segment end
         r.f1 = (r.mode == RAY_FILL) ? 1.0 : 0.0;
-        r.f2 = 0;
-        return Grid<GRID>::begin(a, sh, r, [&](int m, double rho0, double ds) { return segment(r, m, rho0, ds); });
+        r.f2 = (r.mode == RAY_WALK) ? c4.y : 0.0;
+        if (r.mode != RAY_NONE) Grid<GRID>::resume(a, r);
     }
 
-    // the ray ended (grid edge, empty path or WALK target reached): deliver its result
+    // the ray ended (grid edge or WALK target reached): deliver its result
     __device__ __forceinline__ void finish(const Ray& r) {
         if (r.mode == RAY_PEEL) {
-            // Instrument::detect (FullInstrument.cpp:107-174 and the Simple/SED/Frame variants)
-            const DevInstr& ins = sh.instr[rayInstr(r.flags)];
-            const double Lp = r.param;
-            const double Lextf = Lp * exp(-r.tau);
-            const int l = r.idx;
-            const int nl = a.nlambda;
-            const long long nframe = (long long)ins.nx * ins.ny;
-            detects++;
-            auto add = [&](int slot, double v) {
-                if (ins.kind != SKIRT_INSTR_FRAME) atomicAdd(&sh.sed[ins.sedOff + slot * nl + r.ell], v);
-                if (l >= 0 && ins.kind != SKIRT_INSTR_SED)
-                    atomicAddF64(a.tally + ins.frameBase + ((long long)slot * nl + r.ell) * nframe + l, v);
-            };
-            if (ins.kind != SKIRT_INSTR_FULL) { add(0, Lextf); return; }
-            switch (rayCat(r.flags)) {
-            case CAT_STAR_DIRECT:
-                add(0, Lp);
-                add(1, Lextf);
-                break;
-            case CAT_STAR_SCATTERED: {
-                add(2, Lextf);
-                const int lev = rayLevel(r.flags);
-                if (lev >= 1 && lev <= ins.levels) add(5 + lev - 1, Lextf);
-                break;
-            }
-            case CAT_DUST_DIRECT: add(3, Lextf); break;
-            default: add(4, Lextf); break;
-            }
+            a.rays[r.id].s0 = r.tau;  // detectKernel turns it into a detection
         } else if (r.mode == RAY_FILL) {
             a.resA[r.idx] = r.tau;
             if (!ONECOMP) a.resB[r.idx] = r.f2;
@@ -719,6 +748,40 @@ struct Tracer {
         }
     }
 };
+
+// Instrument::detect of one peel-off ray with optical depth tau (FullInstrument.cpp:107-174 and the
+// Simple/SED/Frame variants): SEDs into `sed` (LDS sums of the workgroup) or, when null, the global
+// tally; frames with f64 atomics
+__device__ __forceinline__ void detectPeel(const Args& a, const DevInstr& ins, unsigned flags, int l, double Lp,
+                                           double tau, double* sed) {
+    const double Lextf = Lp * exp(-tau);
+    const int nl = a.nlambda;
+    const int ell = rayEll(flags);
+    const long long nframe = (long long)ins.nx * ins.ny;
+    auto add = [&](int slot, double v) {
+        if (ins.kind != SKIRT_INSTR_FRAME) {
+            if (sed) atomicAdd(&sed[ins.sedOff + slot * nl + ell], v);
+            else atomicAddF64(a.tally + ins.sedBase + slot * nl + ell, v);
+        }
+        if (l >= 0 && ins.kind != SKIRT_INSTR_SED)
+            atomicAddF64(a.tally + ins.frameBase + ((long long)slot * nl + ell) * nframe + l, v);
+    };
+    if (ins.kind != SKIRT_INSTR_FULL) { add(0, Lextf); return; }
+    switch (rayCat(flags)) {
+    case CAT_STAR_DIRECT:
+        add(0, Lp);
+        add(1, Lextf);
+        break;
+    case CAT_STAR_SCATTERED: {
+        add(2, Lextf);
+        const int lev = rayLevel(flags);
+        if (lev >= 1 && lev <= ins.levels) add(5 + lev - 1, Lextf);
+        break;
+    }
+    case CAT_DUST_DIRECT: add(3, Lextf); break;
+    default: add(4, Lextf); break;
+    }
+}
 
 // fills the leaf map: one thread per finest-level cell descends the (checked) tree by its index bits
 __global__ void __launch_bounds__(kBlock) buildLeafMapKernel(LeafEntry* map, const int* firstChild, const int* cellnumber,
@@ -750,16 +813,16 @@ __global__ void __launch_bounds__(kBlock) buildLeafMapKernel(LeafEntry* map, con
 template <int GRID, bool ONECOMP>
 __global__ void __launch_bounds__(kBlock) SKIRT_TRACE_ATTR traceKernel(const Args a) {
     extern __shared__ __attribute__((aligned(16))) double lds[];
-    Shared sh = stageTables(a, lds, GRID == SKIRT_GRID_CARTESIAN, GRID == SKIRT_GRID_OCTREE);
-    for (int q = threadIdx.x; q < a.nsed; q += blockDim.x) sh.sed[q] = 0.0;
+    Shared sh = stageTables(a, lds, gridParts<GRID>() | STAGE_OPTICS);
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         // reset the counters the next event iteration appends to (nobody else uses them now)
         a.ctr[1 - a.parity] = 0;  // ray count of the next iteration
         a.ctr[2 + a.parity] = 0;  // active list just consumed by the event kernel
     }
-    __syncthreads();
 
     Tracer<GRID, ONECOMP> T{a, sh};
+    T.pendVal = lds + a.ldsInstrOff + threadIdx.x;  // after the grid and optics tables
+    T.pendIdx = reinterpret_cast<unsigned*>(lds + a.ldsInstrOff + kLabsBuf * kBlock) + threadIdx.x;
     const int lane = threadIdx.x & 63;
     const unsigned int nrays = a.ctr[a.parity];
     Ray r;
@@ -779,21 +842,14 @@ __global__ void __launch_bounds__(kBlock) SKIRT_TRACE_ATTR traceKernel(const Arg
             if (idle) {
                 const unsigned int id = base + (unsigned int)__popcll(imask & ((1ull << lane) - 1ull));
                 if (id >= nrays) done = true;
-                else {
-                    const double2* src = reinterpret_cast<const double2*>(a.rays + id);
-                    const double2 p0 = src[0], p1 = src[1], p2 = src[2], p3 = src[3];
-                    RayRec q;
-                    q.x = p0.x; q.y = p0.y; q.z = p1.x; q.dx = p1.y; q.dy = p2.x; q.dz = p2.y; q.param = p3.x;
-                    int2 tail;
-                    memcpy(&tail, &p3.y, 8);
-                    q.idx = tail.x;
-                    q.flags = (unsigned)tail.y;
-                    if (!T.start(r, q)) { T.finish(r); r.mode = RAY_NONE; }
-                }
+                else T.load(r, id);  // a RAY_NONE record (empty path) leaves the lane idle
             }
         }
+        if (__ballot(T.npend > kLabsBuf - kStepsPerPull)) T.drain();  // room for the next steps' adds
 #pragma unroll 1
-        for (int it = 0; it < 4; it++) {
+        for (int it = 0; it < kStepsPerPull; it++) {
+            if (__ballot(r.mode != RAY_NONE) == 0) break;
+            T.laneSlots++;
             if (r.mode != RAY_NONE) {
                 if (!Grid<GRID>::step(a, sh, r, [&](int m, double rho0, double ds) { return T.segment(r, m, rho0, ds); })) {
                     T.finish(r);
@@ -802,7 +858,29 @@ __global__ void __launch_bounds__(kBlock) SKIRT_TRACE_ATTR traceKernel(const Arg
             }
         }
     }
-    // flush the per-workgroup SED sums and the statistics
+    T.drain();
+    const unsigned long long vals[7] = {0, T.segFill, T.segWalk, T.segPeel, 0, T.absorbs, T.laneSlots};
+    flushStats(a, vals);
+}
+
+// the detections of this iteration's peel-off rays (their optical depths are in the queue now)
+__global__ void __launch_bounds__(kBlock) detectKernel(const Args a) {
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    Shared sh = stageTables(a, lds, STAGE_INSTR);
+    for (int q = threadIdx.x; q < a.nsed; q += blockDim.x) sh.sed[q] = 0.0;
+    __syncthreads();
+    const unsigned int nrays = a.ctr[a.parity];
+    unsigned int detects = 0;
+    for (unsigned int id = blockIdx.x * blockDim.x + threadIdx.x; id < nrays; id += gridDim.x * blockDim.x) {
+        const int4 c6 = reinterpret_cast<const int4*>(a.rays + id)[6];
+        const unsigned flags = (unsigned)c6.y;
+        if (rayMode(flags) != RAY_PEEL) continue;
+        const double2 c4 = reinterpret_cast<const double2*>(a.rays + id)[4];
+        const double2 c5 = reinterpret_cast<const double2*>(a.rays + id)[5];
+        detectPeel(a, sh.instr[rayInstr(flags)], flags, c6.x, c5.y, c4.y, sh.sed);
+        detects++;
+    }
+    // flush the per-workgroup SED sums
     __syncthreads();
     for (int q = threadIdx.x; q < a.nsed; q += blockDim.x) {
         const double v = sh.sed[q];
@@ -812,7 +890,7 @@ __global__ void __launch_bounds__(kBlock) SKIRT_TRACE_ATTR traceKernel(const Arg
             atomicAddF64(a.tally + sh.instr[ii].sedBase + (q - sh.instr[ii].sedOff), v);
         }
     }
-    const unsigned long long vals[6] = {0, T.segFill, T.segWalk, T.segPeel, T.detects, T.absorbs};
+    const unsigned long long vals[7] = {0, 0, 0, 0, detects, 0, 0};
     flushStats(a, vals);
 }
 
@@ -827,9 +905,54 @@ template <int GRID, bool ONECOMP>
 struct Events {
     const Args& a;
     const Shared& sh;
-    unsigned int packets = 0, detects = 0;
+    unsigned int packets = 0, detects = 0, segFill = 0, segWalk = 0, segPeel = 0;
 
     __device__ __forceinline__ double rho(int m, int h) const { return a.rho[(size_t)m * a.ncomp + h]; }
+
+    // queues ray `pos`: walks the part of the path before the grid (DustGrid::path up to the first
+    // cell) and stores the entered ray; an empty path is finished here and queued as RAY_NONE
+    __device__ __forceinline__ void emitRay(unsigned pos, const Packet& p, double dx, double dy, double dz, double prm,
+                                            int idx, unsigned flags) {
+        Ray r;
+        r.x = p.rx; r.y = p.ry; r.z = p.rz;
+        r.dx = dx; r.dy = dy; r.dz = dz;
+        r.ix = (fabs(dx) > 1e-15) ? 1.0 / dx : 0.0;
+        r.iy = (fabs(dy) > 1e-15) ? 1.0 / dy : 0.0;
+        r.iz = (fabs(dz) > 1e-15) ? 1.0 / dz : 0.0;
+        r.s = 0;
+        r.rho0 = 0;
+        r.ci = r.cj = r.ck = r.jx = r.jy = r.jz = 0;
+        const unsigned mode = rayMode(flags);
+        unsigned nseg = 0;
+        const bool entered = a.hasDust && Grid<GRID>::begin(a, sh, r, [&](int, double, double ds) {
+            if (ds > 0) { r.s += ds; nseg++; }  // outside the grid: no optical depth
+            return true;
+        });
+        if (mode == RAY_FILL) segFill += nseg;
+        else if (mode == RAY_WALK) segWalk += nseg;
+        else segPeel += nseg;
+        int4* dst = reinterpret_cast<int4*>(a.rays + pos);
+        if (!entered) {
+            if (mode == RAY_PEEL) {
+                detectPeel(a, sh.instr[rayInstr(flags)], flags, idx, prm, 0.0, nullptr);
+                detects++;
+            } else {
+                a.resA[idx] = 0.0;  // FILL: tau = 0 (and no scattered luminosity); WALK: s = 0
+                if (!ONECOMP) a.resB[idx] = 0.0;
+            }
+            dst[6] = make_int4(idx, (int)RAY_NONE, 0, 0);
+            return;
+        }
+        double2* d2 = reinterpret_cast<double2*>(dst);
+        d2[0] = make_double2(r.x, r.y);
+        d2[1] = make_double2(r.z, dx);
+        d2[2] = make_double2(dy, dz);
+        d2[3] = make_double2(r.ix, r.iy);
+        d2[4] = make_double2(r.iz, r.s);
+        d2[5] = make_double2(r.rho0, prm);
+        dst[6] = make_int4(idx, (int)flags, r.ci, r.cj);
+        dst[7] = make_int4(r.ck, r.jx, r.jy, r.jz);
+    }
 
     __device__ __forceinline__ void load(int s, Packet& p) const {
         p.rx = a.srx[s]; p.ry = a.sry[s]; p.rz = a.srz[s];
@@ -1028,7 +1151,7 @@ enum PeelKind : int { PEEL_NONE = 0, PEEL_EMISSION = 1, PEEL_SCATTER = 2 };
 template <int GRID, bool ONECOMP>
 __global__ void __launch_bounds__(kBlock) eventKernel(const Args a) {
     extern __shared__ __attribute__((aligned(16))) double lds[];
-    Shared sh = stageTables(a, lds, GRID == SKIRT_GRID_CARTESIAN, GRID == SKIRT_GRID_OCTREE);
+    Shared sh = stageTables(a, lds, gridParts<GRID>() | STAGE_OPTICS | STAGE_INSTR);
     if (blockIdx.x == 0 && threadIdx.x == 0) a.ctr[4] = 0;  // the trace kernel's pull counter
     Events<GRID, ONECOMP> E{a, sh};
     const int lane = threadIdx.x & 63;
@@ -1140,23 +1263,22 @@ __global__ void __launch_bounds__(kBlock) eventKernel(const Args a) {
             qbase = __shfl(qbase, 63);
         }
         unsigned int pos = qbase + (unsigned)(incl - nray);
-        auto emit = [&](double dx, double dy, double dz, double param, int idx, unsigned flags) {
-            double2* dst = reinterpret_cast<double2*>(a.rays + pos);
-            int2 tail = make_int2(idx, (int)flags);
-            double tailv;
-            memcpy(&tailv, &tail, 8);
-            dst[0] = make_double2(p.rx, p.ry);
-            dst[1] = make_double2(p.rz, dx);
-            dst[2] = make_double2(dy, dz);
-            dst[3] = make_double2(param, tailv);
-            pos++;
-        };
-        if (peel != PEEL_NONE) {
-            const unsigned ellBits = (unsigned)p.ell << 18;
-            for (int i = 0; i < a.ninstr; i++) {
+        const int npeel = nray - (mainMode != RAY_NONE ? 1 : 0);
+        int inext = 0;  // next instrument to consider for a peel-off
+        for (int k = 0; k < nray; k++) {
+            double dx, dy, dz, prm;
+            int idx;
+            unsigned flags;
+            if (k < npeel) {
+                int i = inext, l;
+                while (true) {  // the next instrument that receives this peel-off
+                    const DevInstr& ins = sh.instr[i];
+                    l = ins.kind == SKIRT_INSTR_SED ? -1 : E.pixel(ins, p);
+                    if (ins.kind == SKIRT_INSTR_FRAME && l < 0) { i++; continue; }
+                    break;
+                }
+                inext = i + 1;
                 const DevInstr& ins = sh.instr[i];
-                const int l = ins.kind == SKIRT_INSTR_SED ? -1 : E.pixel(ins, p);
-                if (ins.kind == SKIRT_INSTR_FRAME && l < 0) continue;
                 double Lp = p.L;
                 unsigned cat, level = 0;
                 if (peel == PEEL_EMISSION) {
@@ -1168,11 +1290,18 @@ __global__ void __launch_bounds__(kBlock) eventKernel(const Args a) {
                     cat = p.stellar >= 0 ? CAT_STAR_SCATTERED : CAT_DUST_SCATTERED;
                     level = (unsigned)min(p.nscatt, 255);  // nscatt already counts this scattering
                 }
-                emit(ins.kobs[0], ins.kobs[1], ins.kobs[2], Lp, l,
-                     RAY_PEEL | (cat << 2) | ((unsigned)i << 4) | (level << 10) | ellBits);
+                dx = ins.kobs[0]; dy = ins.kobs[1]; dz = ins.kobs[2];
+                prm = Lp;
+                idx = l;
+                flags = RAY_PEEL | (cat << 2) | ((unsigned)i << 4) | (level << 10) | ((unsigned)p.ell << 18);
+            } else {
+                dx = p.kx; dy = p.ky; dz = p.kz;
+                prm = mainParam;
+                idx = slot;
+                flags = mainMode | ((unsigned)p.ell << 18);
             }
+            E.emitRay(pos++, p, dx, dy, dz, prm, idx, flags);
         }
-        if (mainMode != RAY_NONE) emit(p.kx, p.ky, p.kz, mainParam, slot, mainMode | ((unsigned)p.ell << 18));
         // the slot stays active while it has a FILL/WALK ray in flight
         const bool active = mainMode != RAY_NONE;
         const unsigned long long am = __ballot(active);
@@ -1185,7 +1314,7 @@ __global__ void __launch_bounds__(kBlock) eventKernel(const Args a) {
         }
         if (valid) E.store(slot, p);
     }
-    const unsigned long long vals[6] = {E.packets, 0, 0, 0, E.detects, 0};
+    const unsigned long long vals[7] = {E.packets, E.segFill, E.segWalk, E.segPeel, E.detects, 0, 0};
     flushStats(a, vals);
 }
 
@@ -1645,6 +1774,7 @@ int skirt_mcrt_run_stellar(SkirtMcrt* c, uint64_t npp, uint64_t first, uint64_t 
     a.store = p->store_absorption ? 1 : 0;
     a.hasDust = p->has_dust ? 1 : 0;
     if (a.store && !c->dLabs) return fail(c, SKIRT_ERR_STATE, "no Labs buffer");
+    if ((uint64_t)c->ncells * (uint64_t)c->nlambda >= (1ull << 32)) return fail(c, SKIRT_ERR_UNSUPPORTED, "Labs table exceeds 2^32 entries");
     a.labs = c->dLabs; a.tally = c->dTally;
     a.error = c->dError; a.stats = c->dStats;
     a.claim = c->dClaim; a.ctr = c->dCtr;
@@ -1663,7 +1793,10 @@ int skirt_mcrt_run_stellar(SkirtMcrt* c, uint64_t npp, uint64_t first, uint64_t 
     off += a.ninstr * (int)(sizeof(DevInstr) / sizeof(double));
     a.ldsSedOff = off;
     off += c->nsed;
-    const size_t lds = (size_t)off * sizeof(double);
+    const size_t lds = (size_t)off * sizeof(double);                       // detect kernel: everything
+    const size_t ldsTrace = (size_t)a.ldsInstrOff * sizeof(double)          // grid tables + optics
+                            + (size_t)kLabsBuf * kBlock * (sizeof(double) + sizeof(unsigned));  // + Labs buffers
+    const size_t ldsEvent = (size_t)a.ldsSedOff * sizeof(double);           // + instruments
     if (lds > 64 * 1024) return fail(c, SKIRT_ERR_UNSUPPORTED, "tables do not fit in LDS (" + std::to_string(lds) + " bytes)");
     const int kind = c->gridKind == SKIRT_GRID_CARTESIAN ? SKIRT_GRID_CARTESIAN : (leafMap ? SKIRT_GRID_OCTREE : kOctreeNodes);
     const bool one = a.ncomp == 1;
@@ -1675,23 +1808,24 @@ int skirt_mcrt_run_stellar(SkirtMcrt* c, uint64_t npp, uint64_t first, uint64_t 
     int tgrid = c->traceGrid;
     if (tgrid <= 0) {
         int per = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, traceFn, kBlock, lds) != hipSuccess || per < 1) per = 2;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, traceFn, kBlock, ldsTrace) != hipSuccess || per < 1) per = 2;
         tgrid = std::max(1, c->numCUs) * per;
     }
     const int egrid = std::max(1, std::min((slots + kBlock - 1) / kBlock, std::max(1, c->numCUs) * 8));
+    const int dgrid = std::max(1, std::max(1, c->numCUs) * 4);
 
     HIPCHECK(c, hipMemsetAsync(c->dClaim, 0, sizeof(unsigned long long), c->stream));
     HIPCHECK(c, hipMemsetAsync(c->dCtr, 0, 8 * sizeof(unsigned int), c->stream));
     HIPCHECK(c, hipEventRecord(c->ev0, c->stream));
     auto launchEvent = [&](const Args& aa) {
-#define SKIRT_EVENT(G, O) hipLaunchKernelGGL((eventKernel<G, O>), dim3(egrid), dim3(kBlock), lds, c->stream, aa)
+#define SKIRT_EVENT(G, O) hipLaunchKernelGGL((eventKernel<G, O>), dim3(egrid), dim3(kBlock), ldsEvent, c->stream, aa)
         if (kind == SKIRT_GRID_CARTESIAN) { if (one) SKIRT_EVENT(SKIRT_GRID_CARTESIAN, true); else SKIRT_EVENT(SKIRT_GRID_CARTESIAN, false); }
         else if (kind == SKIRT_GRID_OCTREE) { if (one) SKIRT_EVENT(SKIRT_GRID_OCTREE, true); else SKIRT_EVENT(SKIRT_GRID_OCTREE, false); }
         else { if (one) SKIRT_EVENT(kOctreeNodes, true); else SKIRT_EVENT(kOctreeNodes, false); }
 #undef SKIRT_EVENT
     };
     auto launchTrace = [&](const Args& aa) {
-#define SKIRT_TRACE(G, O) hipLaunchKernelGGL((traceKernel<G, O>), dim3(tgrid), dim3(kBlock), lds, c->stream, aa)
+#define SKIRT_TRACE(G, O) hipLaunchKernelGGL((traceKernel<G, O>), dim3(tgrid), dim3(kBlock), ldsTrace, c->stream, aa)
         if (kind == SKIRT_GRID_CARTESIAN) { if (one) SKIRT_TRACE(SKIRT_GRID_CARTESIAN, true); else SKIRT_TRACE(SKIRT_GRID_CARTESIAN, false); }
         else if (kind == SKIRT_GRID_OCTREE) { if (one) SKIRT_TRACE(SKIRT_GRID_OCTREE, true); else SKIRT_TRACE(SKIRT_GRID_OCTREE, false); }
         else { if (one) SKIRT_TRACE(kOctreeNodes, true); else SKIRT_TRACE(kOctreeNodes, false); }
@@ -1711,6 +1845,10 @@ int skirt_mcrt_run_stellar(SkirtMcrt* c, uint64_t npp, uint64_t first, uint64_t 
         if (!a.hasDust) { it++; break; }  // without dust every packet completes inside the event kernel
         launchTrace(a);
         HIPCHECK(c, hipGetLastError());
+        if (a.ninstr > 0) {
+            hipLaunchKernelGGL(detectKernel, dim3(dgrid), dim3(kBlock), lds, c->stream, a);
+            HIPCHECK(c, hipGetLastError());
+        }
         it++;
         if (it % pollEvery == 0) {
             HIPCHECK(c, hipMemcpyAsync(c->hCtr, c->dCtr, 8 * sizeof(unsigned int), hipMemcpyDeviceToHost, c->stream));
@@ -1767,6 +1905,8 @@ int skirt_mcrt_stats(SkirtMcrt* c, SkirtStats* out) {
     out->segments_peel = v[3];
     out->detects = v[4];
     out->absorb_adds = v[5];
+    out->lane_slots = v[6];
+    out->iterations = (uint64_t)c->lastIterations;
     out->kernel_ms = c->lastMs;
     return SKIRT_OK;
 }
