@@ -26,6 +26,18 @@ CONFIGS = {
     "c2": ("benchmarks/c2_cart64.ski", 1000000, 0, "C2 Cartesian 64^3, 10 lambda, peel-off"),
 }
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip-level parameters (spec)
+ATOMIC_PEAK_ADDS = 2.36e10  # scattered 8-byte atomic adds per second, measured (profiles/r01_atomic_bench.txt)
+
+
+def pmc_traffic(config):
+    """HBM bytes per trace-kernel launch from the committed rocprofv3 PMC passes of this same bench
+    command (tools/pmc_traffic.py writes profiles/pmc_<config>.json); None when absent."""
+    path = os.path.join(REPO, "profiles", "pmc_%s.json" % config)
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        d = json.load(f)
+    return {"bytes_per_launch": d["traffic_bytes_per_launch"], "source": d["source"]}
 
 
 def algorithmic_bytes(stats, geom_bytes, ncomp):
@@ -36,7 +48,7 @@ def algorithmic_bytes(stats, geom_bytes, ncomp):
     return segs * (geom_bytes + 8 * ncomp) + stats["absorb_adds"] * 16 + stats["detects"] * 16
 
 
-def cpu_baseline(ski, target_seconds=15.0):
+def cpu_baseline(ski, target_seconds=20.0):
     """The CPU oracle (a C++ restatement of the reference's photon loop, std::thread over packets with
     lock-free tallies like the reference's Parallel + LockFree::add) on this host's cores, on a bounded
     sample of the same workload: fewer packets per wavelength, all wavelengths. A short probe sizes the
@@ -78,14 +90,16 @@ def main():
     torch.cuda.set_device(local)
 
     import skirt_amd
+    from skirt_amd.sharding import allreduce_tallies, shard_range
 
     ski_rel, ppl_default, geom_bytes, desc = CONFIGS[args.config]
     ski = os.path.join(REPO, ski_rel)
     ppl = args.packets_per_lambda or ppl_default
     sim = skirt_amd.Simulation(ski, packages=float(ppl * world))
     info = sim.info
-    share = ppl * info.nlambda  # packets per rank per step
-    first = rank * share
+    # weak scaling: the phase has ppl packets per wavelength per rank; rank r shoots its contiguous
+    # slice of the global packet index space
+    first, share = shard_range(ppl * info.nlambda * world, rank, world)
     sim.attach(local)
     if args.threshold or args.slots or args.trace_grid:
         sim.configure(slots=args.slots, grid=args.trace_grid, threshold=args.threshold)
@@ -99,10 +113,8 @@ def main():
 
     def step():
         sim.run_stellar(first, share)
-        if world > 1:
-            # phase end: PanDustSystem::sumResults (Labs) and Instrument::sumResults, over RCCL/xGMI
-            dist.all_reduce(labs)
-            dist.all_reduce(instr)
+        # phase end: PanDustSystem::sumResults (Labs) and Instrument::sumResults, over RCCL/xGMI
+        allreduce_tallies(labs, instr)
 
     for _ in range(args.warmup):
         step()
@@ -111,12 +123,15 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     s0 = sim.stats()
-    kernel_ms = []
+    kernel_ms, trace_ms, trace_launches = [], 0.0, 0
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
         sim.synchronize()
-        kernel_ms.append(sim.stats()["kernel_ms"])
+        st = sim.stats()
+        kernel_ms.append(st["kernel_ms"])
+        trace_ms += st["trace_ms"]
+        trace_launches += st["trace_launches"]
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -127,13 +142,18 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    delta = {k: s1[k] - s0[k] for k in s1 if k not in ("kernel_ms", "iterations")}
+    delta = {k: s1[k] - s0[k] for k in s1 if k not in ("kernel_ms", "iterations", "trace_ms", "trace_launches")}
     packets_all = share * world * args.steps
     value = packets_all / elapsed
     avg_kernel_s = sum(kernel_ms) / len(kernel_ms) / 1e3
-    bytes_per_launch = algorithmic_bytes(delta, geom_bytes, info.ncomp) / args.steps
-    achieved = bytes_per_launch / avg_kernel_s / 1e9
     segs = delta["segments_fill"] + delta["segments_walk"] + delta["segments_peel"]
+    # the dominant kernel: traceKernel. Its algorithmic bytes per launch (without the
+    # detections, which the detect kernel performs) over its average launch time (HIP events)
+    trace_bytes = algorithmic_bytes(delta, geom_bytes, info.ncomp) - 16 * delta["detects"]
+    launch_s = trace_ms / max(1, trace_launches) / 1e3
+    bytes_per_launch = trace_bytes / max(1, trace_launches)
+    achieved = bytes_per_launch / launch_s / 1e9
+    traffic = pmc_traffic(args.config)
 
     result = {
         "metric": "photon packets/sec (whole node), 128^3 octree, 1/2/4/8 MI355X + HBM%",
@@ -168,11 +188,18 @@ def main():
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
-            "traffic": None,
+            "traffic": traffic["bytes_per_launch"] if traffic else None,
             "kernel": "traceKernel<octree leaf map>" if info.grid_kind == 1 else "traceKernel<cartesian>",
-            "kernel_ms_avg": avg_kernel_s * 1e3,
+            "launch_ms_avg": launch_s * 1e3,
+            "launches_per_step": trace_launches / args.steps,
             "algorithmic_bytes_per_launch": bytes_per_launch,
+            "traffic_source": traffic["source"] if traffic else None,
+            # what actually bounds the kernel: Labs adds are scattered f64 atomics, executed memory-side
+            # at a fixed chip-wide rate (tools/atomic_bench.hip, profiles/r01_atomic_bench.txt)
+            "labs_atomic_adds_per_s": delta["absorb_adds"] / max(1e-9, trace_ms / 1e3),
+            "labs_atomic_peak_measured": ATOMIC_PEAK_ADDS,
         },
+        "phase_ms_avg": avg_kernel_s * 1e3,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         v, cores, sample = cpu_baseline(ski)

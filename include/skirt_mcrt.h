@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define SKIRT_MCRT_ABI_VERSION 1
+#define SKIRT_MCRT_ABI_VERSION 2
 
 enum {
     SKIRT_OK = 0,
@@ -122,6 +122,8 @@ typedef struct {
     uint64_t lane_slots;        /* trace kernel: 64 x wave steps (segments / lane_slots = SIMD lane use) */
     uint64_t iterations;        /* event/trace iterations of the last run call */
     double kernel_ms;           /* device time of the last run call (HIP events on the engine stream) */
+    double trace_ms;            /* of which trace-kernel launches (HIP events around each launch) */
+    uint64_t trace_launches;    /* trace-kernel launches of the last run call */
 } SkirtStats;
 
 int skirt_mcrt_abi_version(void);

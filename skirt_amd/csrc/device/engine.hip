@@ -1363,6 +1363,9 @@ struct SkirtMcrt {
     // config
     int traceGrid = 0, threshold = 16, slotsWanted = 0;
     double lastMs = 0;
+    std::vector<hipEvent_t> traceEv;  // pairs around the trace launches of the last run call
+    int traceLaunches = 0;
+    double traceMs = 0;
     int numCUs = 0;
     int lastIterations = 0;
 };
@@ -1739,6 +1742,8 @@ int skirt_mcrt_run_stellar(SkirtMcrt* c, uint64_t npp, uint64_t first, uint64_t 
     if (rc) return rc;
     c->lastMs = 0;
     c->lastIterations = 0;
+    c->traceLaunches = 0;
+    c->traceMs = 0;
     if (count == 0) return SKIRT_OK;
     if (!c->dOptics) {  // a dust-free simulation still stages (zero) optical tables
         std::vector<double> z(4 * (size_t)c->nlambda, 0.0);
@@ -1843,8 +1848,18 @@ int skirt_mcrt_run_stellar(SkirtMcrt* c, uint64_t npp, uint64_t first, uint64_t 
         launchEvent(a);
         HIPCHECK(c, hipGetLastError());
         if (!a.hasDust) { it++; break; }  // without dust every packet completes inside the event kernel
+        if ((int)c->traceEv.size() < 2 * (c->traceLaunches + 1)) {
+            hipEvent_t e0, e1;
+            HIPCHECK(c, hipEventCreate(&e0));
+            HIPCHECK(c, hipEventCreate(&e1));
+            c->traceEv.push_back(e0);
+            c->traceEv.push_back(e1);
+        }
+        HIPCHECK(c, hipEventRecord(c->traceEv[2 * c->traceLaunches], c->stream));
         launchTrace(a);
         HIPCHECK(c, hipGetLastError());
+        HIPCHECK(c, hipEventRecord(c->traceEv[2 * c->traceLaunches + 1], c->stream));
+        c->traceLaunches++;
         if (a.ninstr > 0) {
             hipLaunchKernelGGL(detectKernel, dim3(dgrid), dim3(kBlock), lds, c->stream, a);
             HIPCHECK(c, hipGetLastError());
@@ -1868,6 +1883,10 @@ int skirt_mcrt_synchronize(SkirtMcrt* c) {
     HIPCHECK(c, hipStreamSynchronize(c->stream));
     float ms = 0;
     if (hipEventElapsedTime(&ms, c->ev0, c->ev1) == hipSuccess) c->lastMs = ms;
+    double tms = 0;
+    for (int k = 0; k < c->traceLaunches; k++)
+        if (hipEventElapsedTime(&ms, c->traceEv[2 * k], c->traceEv[2 * k + 1]) == hipSuccess) tms += ms;
+    c->traceMs = tms;
     unsigned int e = 0;
     HIPCHECK(c, hipMemcpy(&e, c->dError, sizeof e, hipMemcpyDeviceToHost));
     if (e) return fail(c, SKIRT_ERR_NUMERIC, "the optical depth along the path is not a positive number");
@@ -1908,6 +1927,8 @@ int skirt_mcrt_stats(SkirtMcrt* c, SkirtStats* out) {
     out->lane_slots = v[6];
     out->iterations = (uint64_t)c->lastIterations;
     out->kernel_ms = c->lastMs;
+    out->trace_ms = c->traceMs;
+    out->trace_launches = (uint64_t)c->traceLaunches;
     return SKIRT_OK;
 }
 
@@ -1926,6 +1947,7 @@ void skirt_mcrt_destroy(SkirtMcrt* c) {
     if (c->hCtr) (void)hipHostFree(c->hCtr);
     if (c->ownLabs && c->dLabs) (void)hipFree(c->dLabs);
     if (c->ownTally && c->dTally) (void)hipFree(c->dTally);
+    for (hipEvent_t e : c->traceEv) (void)hipEventDestroy(e);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->own) (void)hipStreamDestroy(c->own);
