@@ -638,17 +638,29 @@ struct Tracer {
     const Args& a;
     const Shared& sh;
     unsigned int segFill = 0, segWalk = 0, segPeel = 0, absorbs = 0, laneSlots = 0;
-    // Labs adds of this lane not yet issued: scattered f64 atomics run memory-side at a fixed chip-wide
-    // rate and every one stays in the wave's in-order vmcnt, so a wave that issued one per step would
-    // wait for its acknowledgement at every step. Buffered in LDS (kLabsBuf per lane) and issued in
-    // bursts, a wave waits for one round trip per burst.
-    double* pendVal;
-    unsigned* pendIdx;
+    // Labs adds of this lane not yet issued. f64 atomics execute memory-side at a fixed chip-wide rate
+    // of 64-byte requests; lanes of one wave instruction that hit the same 64-byte line share a
+    // request. A lane's consecutive adds are consecutive cells of one ray -- spatial neighbours, and
+    // with Morton-ordered device cell numbers mostly in the same or the next line -- so the adds wait
+    // in LDS (kLabsBuf per lane, [slot][thread]) and are issued transposed: each wave instruction
+    // carries the kLabsBuf consecutive adds of 64 / kLabsBuf lanes. A wave also waits for one
+    // atomic round trip per burst instead of one per step.
+    double* pendVal;    // LDS, [kLabsBuf][kBlock]
+    unsigned* pendIdx;  // LDS, [kLabsBuf][kBlock]
     int npend = 0;
 
     __device__ __forceinline__ void drain() {
-        for (int j = 0; j < kLabsBuf; j++)
-            if (j < npend) atomicAddF64(a.labs + pendIdx[j * kBlock], pendVal[j * kBlock]);
+        static_assert(kLabsBuf == 8, "the transposed drain covers 8 lanes x 8 adds per instruction");
+        const int lane = threadIdx.x & 63;
+        const int wbase = threadIdx.x - lane;
+        const int j = lane & 7;
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            const int src = 8 * i + (lane >> 3);
+            const int n = __shfl(npend, src);
+            const int q = j * kBlock + wbase + src;
+            if (j < n) atomicAddF64(a.labs + pendIdx[q], pendVal[q]);
+        }
         npend = 0;
     }
 
@@ -684,8 +696,8 @@ struct Tracer {
                     r.f2 += albedo * Lintm;
                 }
                 if (a.store) {
-                    pendVal[npend * kBlock] = (1.0 - albedo) * Lintm;
-                    pendIdx[npend * kBlock] = (unsigned)r.ell * (unsigned)a.ncells + (unsigned)m;
+                    pendVal[npend * kBlock + threadIdx.x] = (1.0 - albedo) * Lintm;
+                    pendIdx[npend * kBlock + threadIdx.x] = (unsigned)r.ell * (unsigned)a.ncells + (unsigned)m;
                     npend++;
                     absorbs++;
                 }
@@ -821,8 +833,8 @@ __global__ void __launch_bounds__(kBlock) SKIRT_TRACE_ATTR traceKernel(const Arg
     }
 
     Tracer<GRID, ONECOMP> T{a, sh};
-    T.pendVal = lds + a.ldsInstrOff + threadIdx.x;  // after the grid and optics tables
-    T.pendIdx = reinterpret_cast<unsigned*>(lds + a.ldsInstrOff + kLabsBuf * kBlock) + threadIdx.x;
+    T.pendVal = lds + a.ldsInstrOff;  // after the grid and optics tables
+    T.pendIdx = reinterpret_cast<unsigned*>(lds + a.ldsInstrOff + kLabsBuf * kBlock);
     const int lane = threadIdx.x & 63;
     const unsigned int nrays = a.ctr[a.parity];
     Ray r;
@@ -845,7 +857,6 @@ __global__ void __launch_bounds__(kBlock) SKIRT_TRACE_ATTR traceKernel(const Arg
                 else T.load(r, id);  // a RAY_NONE record (empty path) leaves the lane idle
             }
         }
-        if (__ballot(T.npend > kLabsBuf - kStepsPerPull)) T.drain();  // room for the next steps' adds
 #pragma unroll 1
         for (int it = 0; it < kStepsPerPull; it++) {
             if (__ballot(r.mode != RAY_NONE) == 0) break;
@@ -856,6 +867,7 @@ __global__ void __launch_bounds__(kBlock) SKIRT_TRACE_ATTR traceKernel(const Arg
                     r.mode = RAY_NONE;
                 }
             }
+            if (__ballot(T.npend == kLabsBuf)) T.drain();  // a full buffer: issue the wave's adds
         }
     }
     T.drain();
@@ -1339,6 +1351,10 @@ struct SkirtMcrt {
     double* dTreeT = nullptr;
     LeafEntry* dLeafMap = nullptr;
     bool mapReady = false;
+    // device cell numbering: devCell[reference cell] (empty = identity). Octree cells are renumbered in
+    // Morton (depth-first, children in octant order) order so that neighbouring cells share Labs lines;
+    // rho is uploaded and Labs downloaded through it.
+    std::vector<int> devCell;
     // media
     int ncomp = 0, nlambda = 0;
     double *dRho = nullptr, *dOptics = nullptr;
@@ -1540,6 +1556,7 @@ int skirt_mcrt_upload_grid(SkirtMcrt* c, const SkirtGridDesc* g) {
     if (!c || !g) return SKIRT_ERR_ARG;
     HIPCHECK(c, hipSetDevice(c->device));
     c->ncells = g->ncells;
+    c->devCell.clear();
     if (g->kind == SKIRT_GRID_CARTESIAN) {
         if (g->nx < 1 || g->ny < 1 || g->nz < 1 || !g->xv || !g->yv || !g->zv) return fail(c, SKIRT_ERR_ARG, "bad Cartesian grid");
         if ((long long)g->nx * g->ny * g->nz != g->ncells) return fail(c, SKIRT_ERR_ARG, "ncells != nx*ny*nz");
@@ -1583,7 +1600,28 @@ int skirt_mcrt_upload_grid(SkirtMcrt* c, const SkirtGridDesc* g) {
         int rc;
         if ((rc = upload(c, c->dBox, g->box, 6 * (size_t)g->nnodes))) return rc;
         if ((rc = upload(c, c->dFirstChild, g->first_child, (size_t)g->nnodes))) return rc;
-        if ((rc = upload(c, c->dCellnumber, g->cellnumber, (size_t)g->nnodes))) return rc;
+        // Morton order of the leaves: depth-first, children in octant order (x, y, z bits)
+        c->devCell.assign(g->ncells, -1);
+        {
+            std::vector<int> stack{0};
+            int next = 0;
+            while (!stack.empty()) {
+                const int l = stack.back();
+                stack.pop_back();
+                const int fc = g->first_child[l];
+                if (fc < 0) {
+                    if (c->devCell[g->cellnumber[l]] >= 0) return fail(c, SKIRT_ERR_ARG, "octree cell number used twice");
+                    c->devCell[g->cellnumber[l]] = next++;
+                } else {
+                    for (int k = 7; k >= 0; k--) stack.push_back(fc + k);
+                }
+            }
+            if (next != g->ncells) return fail(c, SKIRT_ERR_ARG, "octree leaves do not cover the cells");
+        }
+        std::vector<int> cn(g->cellnumber, g->cellnumber + g->nnodes);
+        for (int l = 0; l < g->nnodes; l++)
+            if (cn[l] >= 0) cn[l] = c->devCell[cn[l]];
+        if ((rc = upload(c, c->dCellnumber, cn.data(), (size_t)g->nnodes))) return rc;
         if ((rc = upload(c, c->dNbrOffset, g->nbr_offset, 6 * (size_t)g->nnodes + 1))) return rc;
         std::vector<int> dummy(1, 0);
         if ((rc = upload(c, c->dNbrList, nnbr ? g->nbr_list : dummy.data(), nnbr ? (size_t)nnbr : 1))) return rc;
@@ -1612,7 +1650,14 @@ int skirt_mcrt_upload_media(SkirtMcrt* c, const SkirtMediaDesc* m) {
     std::memcpy(opt.data() + 2 * nt, m->albedo, nt * sizeof(double));
     std::memcpy(opt.data() + 3 * nt, m->g, nt * sizeof(double));
     int rc;
-    if ((rc = upload(c, c->dRho, m->rho, (size_t)m->ncells * m->ncomp))) return rc;
+    if (c->devCell.empty()) {
+        if ((rc = upload(c, c->dRho, m->rho, (size_t)m->ncells * m->ncomp))) return rc;
+    } else {
+        std::vector<double> rho((size_t)m->ncells * m->ncomp);
+        for (int q = 0; q < m->ncells; q++)
+            for (int h = 0; h < m->ncomp; h++) rho[(size_t)c->devCell[q] * m->ncomp + h] = m->rho[(size_t)q * m->ncomp + h];
+        if ((rc = upload(c, c->dRho, rho.data(), rho.size()))) return rc;
+    }
     if ((rc = upload(c, c->dOptics, opt.data(), opt.size()))) return rc;
     return SKIRT_OK;
 }
@@ -1902,8 +1947,10 @@ int skirt_mcrt_download(SkirtMcrt* c, double* labs, double* instr) {
         if (!c->dLabs) return fail(c, SKIRT_ERR_STATE, "no Labs buffer");
         std::vector<double> t(nl);
         HIPCHECK(c, hipMemcpy(t.data(), c->dLabs, nl * sizeof(double), hipMemcpyDeviceToHost));
+        const bool perm = !c->devCell.empty();
         for (int ell = 0; ell < c->nlambda; ell++)
-            for (int m = 0; m < c->ncells; m++) labs[(size_t)m * c->nlambda + ell] = t[(size_t)ell * c->ncells + m];
+            for (int m = 0; m < c->ncells; m++)
+                labs[(size_t)m * c->nlambda + ell] = t[(size_t)ell * c->ncells + (perm ? c->devCell[m] : m)];
     }
     if (instr && c->nInstrTally) {
         if (!c->dTally) return fail(c, SKIRT_ERR_STATE, "no instrument buffer");
