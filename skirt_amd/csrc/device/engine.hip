@@ -41,8 +41,17 @@ namespace {
 
 constexpr double kDblMax = 1.7976931348623157e308;
 constexpr int kBlock = 256;
-constexpr int kLabsBuf = 8;        // buffered Labs adds per trace lane (LDS)
+#ifndef SKIRT_LABS_BUF
+#define SKIRT_LABS_BUF 16
+#endif
+constexpr int kLabsBuf = SKIRT_LABS_BUF;  // buffered Labs adds per trace lane (LDS)
 constexpr int kStepsPerPull = 4;   // grid steps between two ray pulls of a trace wave
+// The slot pool runs as kHalves independent pipelines on their own streams: while one half's trace
+// kernel drains its queue, the other half's event and detect kernels (and its trace kernel's first
+// waves) fill the CUs the finishing waves leave idle.
+constexpr int kHalves = 1;
+constexpr int kPollEvery = 1;      // iterations between two counter copies of a half
+constexpr int kPollRing = 3;       // copies in flight per half (the host reads each kPollRing copies late)
 // occupancy attribute of the trace kernel (a build knob for tuning variants, tools/build_variant.sh)
 #ifndef SKIRT_TRACE_ATTR
 #define SKIRT_TRACE_ATTR
@@ -650,13 +659,14 @@ struct Tracer {
     int npend = 0;
 
     __device__ __forceinline__ void drain() {
-        static_assert(kLabsBuf == 8, "the transposed drain covers 8 lanes x 8 adds per instruction");
+        static_assert(kLabsBuf >= 2 && kLabsBuf <= 64 && (kLabsBuf & (kLabsBuf - 1)) == 0, "kLabsBuf: power of 2");
+        constexpr int G = 64 / kLabsBuf;  // lanes per wave instruction
         const int lane = threadIdx.x & 63;
         const int wbase = threadIdx.x - lane;
-        const int j = lane & 7;
+        const int j = lane & (kLabsBuf - 1);
 #pragma unroll
-        for (int i = 0; i < 8; i++) {
-            const int src = 8 * i + (lane >> 3);
+        for (int i = 0; i < kLabsBuf; i++) {
+            const int src = G * i + lane / kLabsBuf;
             const int n = __shfl(npend, src);
             const int q = j * kBlock + wbase + src;
             if (j < n) atomicAddF64(a.labs + pendIdx[q], pendVal[q]);
@@ -825,12 +835,13 @@ __global__ void __launch_bounds__(kBlock) buildLeafMapKernel(LeafEntry* map, con
 template <int GRID, bool ONECOMP>
 __global__ void __launch_bounds__(kBlock) SKIRT_TRACE_ATTR traceKernel(const Args a) {
     extern __shared__ __attribute__((aligned(16))) double lds[];
-    Shared sh = stageTables(a, lds, gridParts<GRID>() | STAGE_OPTICS);
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         // reset the counters the next event iteration appends to (nobody else uses them now)
         a.ctr[1 - a.parity] = 0;  // ray count of the next iteration
         a.ctr[2 + a.parity] = 0;  // active list just consumed by the event kernel
     }
+    if (a.ctr[a.parity] == 0) return;  // an iteration after the end of the phase
+    Shared sh = stageTables(a, lds, gridParts<GRID>() | STAGE_OPTICS);
 
     Tracer<GRID, ONECOMP> T{a, sh};
     T.pendVal = lds + a.ldsInstrOff;  // after the grid and optics tables
@@ -878,6 +889,7 @@ __global__ void __launch_bounds__(kBlock) SKIRT_TRACE_ATTR traceKernel(const Arg
 // the detections of this iteration's peel-off rays (their optical depths are in the queue now)
 __global__ void __launch_bounds__(kBlock) detectKernel(const Args a) {
     extern __shared__ __attribute__((aligned(16))) double lds[];
+    if (a.ctr[a.parity] == 0) return;
     Shared sh = stageTables(a, lds, STAGE_INSTR);
     for (int q = threadIdx.x; q < a.nsed; q += blockDim.x) sh.sed[q] = 0.0;
     __syncthreads();
@@ -1163,8 +1175,9 @@ enum PeelKind : int { PEEL_NONE = 0, PEEL_EMISSION = 1, PEEL_SCATTER = 2 };
 template <int GRID, bool ONECOMP>
 __global__ void __launch_bounds__(kBlock) eventKernel(const Args a) {
     extern __shared__ __attribute__((aligned(16))) double lds[];
-    Shared sh = stageTables(a, lds, gridParts<GRID>() | STAGE_OPTICS | STAGE_INSTR);
     if (blockIdx.x == 0 && threadIdx.x == 0) a.ctr[4] = 0;  // the trace kernel's pull counter
+    if (!a.init && a.ctr[2 + a.parity] == 0) return;  // an iteration after the end of the phase
+    Shared sh = stageTables(a, lds, gridParts<GRID>() | STAGE_OPTICS | STAGE_INSTR);
     Events<GRID, ONECOMP> E{a, sh};
     const int lane = threadIdx.x & 63;
     const unsigned long long total = a.end - a.first;
@@ -1371,10 +1384,13 @@ struct SkirtMcrt {
     double *dLabs = nullptr, *dTally = nullptr;
     bool ownLabs = true, ownTally = true;
     unsigned long long *dClaim = nullptr, *dStats = nullptr;
-    unsigned int *dError = nullptr, *dCtr = nullptr, *hCtr = nullptr;
+    unsigned int *dError = nullptr, *dCtr = nullptr, *hCtr = nullptr;  // kHalves x 8 counters; hCtr: poll ring
+    hipStream_t aux = nullptr;           // the second pipeline half's stream
+    hipEvent_t evFork = nullptr, evJoin = nullptr;
+    std::vector<hipEvent_t> pollEv;      // kHalves x kPollRing events behind the counter copies
     // slot pool
     int nslots = 0, rayCap = 0;
-    void* dPool = nullptr;
+    void* dPool = nullptr;               // kHalves pools of nslots / kHalves slots each
     size_t poolBytes = 0;
     // config
     int traceGrid = 0, threshold = 16, slotsWanted = 0;
@@ -1409,21 +1425,22 @@ int upload(SkirtMcrt* c, T*& dst, const T* src, size_t n) {
     return SKIRT_OK;
 }
 
-// slot pool: the ray queue, the SoA packet state, per-slot results and two active lists
+// slot pool: kHalves independent pipelines, each with its ray queue, SoA packet state, per-slot
+// results and two active lists; nslots counts the slots of one half
 int ensurePool(SkirtMcrt* c, int nslots) {
     const int rayCap = nslots * (1 + (int)c->instr.size());
-    const size_t need = (size_t)rayCap * sizeof(RayRec) + (size_t)nslots * (10 * 8 + 4 * 4 + 6 * 4 + 2 * 4) + 4096;
+    const size_t half = (size_t)rayCap * sizeof(RayRec) + (size_t)nslots * (10 * 8 + 4 * 4 + 6 * 4 + 2 * 4) + 4096;
     if (c->dPool && c->nslots == nslots && c->rayCap == rayCap) return SKIRT_OK;
     if (c->dPool) { (void)hipFree(c->dPool); c->dPool = nullptr; }
-    HIPCHECK(c, hipMalloc(&c->dPool, need));
-    c->poolBytes = need;
+    HIPCHECK(c, hipMalloc(&c->dPool, kHalves * half));
+    c->poolBytes = half;
     c->nslots = nslots;
     c->rayCap = rayCap;
     return SKIRT_OK;
 }
 
-void carvePool(SkirtMcrt* c, Args& a) {
-    char* p = static_cast<char*>(c->dPool);
+void carvePool(SkirtMcrt* c, Args& a, int h) {
+    char* p = static_cast<char*>(c->dPool) + (size_t)h * c->poolBytes;
     const size_t n = (size_t)c->nslots;
     auto takeD = [&](double*& d) { d = reinterpret_cast<double*>(p); p += n * 8; };
     auto takeI = [&](int*& d) { d = reinterpret_cast<int*>(p); p += n * 4; };
@@ -1436,8 +1453,8 @@ void carvePool(SkirtMcrt* c, Args& a) {
     takeU(a.splo); takeU(a.sphi); takeU(a.sblock); takeU(a.sw2); takeU(a.sw3); takeU(a.shave);
     takeI(a.act[0]); takeI(a.act[1]);
     a.nslots = c->nslots;
+    a.ctr = c->dCtr + 8 * h;
 }
-
 
 // Decides whether the octree can be walked through a leaf map (Grid<SKIRT_GRID_OCTREE>): every node
 // box must equal the box its level and integer coordinates give in the per-axis split tables, and the
@@ -1523,8 +1540,11 @@ int skirt_mcrt_create(int device, SkirtMcrt** out) {
         hipMalloc(&c->dClaim, sizeof(unsigned long long)) != hipSuccess ||
         hipMalloc(&c->dStats, 8 * sizeof(unsigned long long)) != hipSuccess ||
         hipMalloc(&c->dError, sizeof(unsigned int)) != hipSuccess ||
-        hipMalloc(&c->dCtr, 8 * sizeof(unsigned int)) != hipSuccess ||
-        hipHostMalloc(&c->hCtr, 8 * sizeof(unsigned int)) != hipSuccess) {
+        hipMalloc(&c->dCtr, kHalves * 8 * sizeof(unsigned int)) != hipSuccess ||
+        hipHostMalloc(&c->hCtr, kHalves * kPollRing * 8 * sizeof(unsigned int)) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&c->evFork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->evJoin, hipEventDisableTiming) != hipSuccess) {
         delete c;
         return SKIRT_ERR_HIP;
     }
@@ -1797,7 +1817,7 @@ int skirt_mcrt_run_stellar(SkirtMcrt* c, uint64_t npp, uint64_t first, uint64_t 
     // slot pool: enough packets in flight to fill the chip many times over, bounded by the phase size
     int slots = c->slotsWanted > 0 ? c->slotsWanted : (1 << 21);
     if ((uint64_t)slots > count) slots = (int)count;
-    slots = std::max(slots, 64);
+    slots = std::max(slots, 64 * kHalves) / kHalves;  // per half
     if ((rc = ensurePool(c, slots))) return rc;
 
     Args a{};
@@ -1827,9 +1847,8 @@ int skirt_mcrt_run_stellar(SkirtMcrt* c, uint64_t npp, uint64_t first, uint64_t 
     if ((uint64_t)c->ncells * (uint64_t)c->nlambda >= (1ull << 32)) return fail(c, SKIRT_ERR_UNSUPPORTED, "Labs table exceeds 2^32 entries");
     a.labs = c->dLabs; a.tally = c->dTally;
     a.error = c->dError; a.stats = c->dStats;
-    a.claim = c->dClaim; a.ctr = c->dCtr;
+    a.claim = c->dClaim;
     a.threshold = c->threshold;
-    carvePool(c, a);
     // LDS layout (doubles): mesh | optics | instruments | SED sums
     int off = 0;
     a.ldsMeshOff = off;
@@ -1865,59 +1884,100 @@ int skirt_mcrt_run_stellar(SkirtMcrt* c, uint64_t npp, uint64_t first, uint64_t 
     const int dgrid = std::max(1, std::max(1, c->numCUs) * 4);
 
     HIPCHECK(c, hipMemsetAsync(c->dClaim, 0, sizeof(unsigned long long), c->stream));
-    HIPCHECK(c, hipMemsetAsync(c->dCtr, 0, 8 * sizeof(unsigned int), c->stream));
+    HIPCHECK(c, hipMemsetAsync(c->dCtr, 0, kHalves * 8 * sizeof(unsigned int), c->stream));
     HIPCHECK(c, hipEventRecord(c->ev0, c->stream));
-    auto launchEvent = [&](const Args& aa) {
-#define SKIRT_EVENT(G, O) hipLaunchKernelGGL((eventKernel<G, O>), dim3(egrid), dim3(kBlock), ldsEvent, c->stream, aa)
+    HIPCHECK(c, hipEventRecord(c->evFork, c->stream));
+    HIPCHECK(c, hipStreamWaitEvent(c->aux, c->evFork, 0));
+    hipStream_t streams[2] = {c->stream, c->aux};
+    auto launchEvent = [&](const Args& aa, hipStream_t st) {
+#define SKIRT_EVENT(G, O) hipLaunchKernelGGL((eventKernel<G, O>), dim3(egrid), dim3(kBlock), ldsEvent, st, aa)
         if (kind == SKIRT_GRID_CARTESIAN) { if (one) SKIRT_EVENT(SKIRT_GRID_CARTESIAN, true); else SKIRT_EVENT(SKIRT_GRID_CARTESIAN, false); }
         else if (kind == SKIRT_GRID_OCTREE) { if (one) SKIRT_EVENT(SKIRT_GRID_OCTREE, true); else SKIRT_EVENT(SKIRT_GRID_OCTREE, false); }
         else { if (one) SKIRT_EVENT(kOctreeNodes, true); else SKIRT_EVENT(kOctreeNodes, false); }
 #undef SKIRT_EVENT
     };
-    auto launchTrace = [&](const Args& aa) {
-#define SKIRT_TRACE(G, O) hipLaunchKernelGGL((traceKernel<G, O>), dim3(tgrid), dim3(kBlock), ldsTrace, c->stream, aa)
+    auto launchTrace = [&](const Args& aa, hipStream_t st) {
+#define SKIRT_TRACE(G, O) hipLaunchKernelGGL((traceKernel<G, O>), dim3(tgrid), dim3(kBlock), ldsTrace, st, aa)
         if (kind == SKIRT_GRID_CARTESIAN) { if (one) SKIRT_TRACE(SKIRT_GRID_CARTESIAN, true); else SKIRT_TRACE(SKIRT_GRID_CARTESIAN, false); }
         else if (kind == SKIRT_GRID_OCTREE) { if (one) SKIRT_TRACE(SKIRT_GRID_OCTREE, true); else SKIRT_TRACE(SKIRT_GRID_OCTREE, false); }
         else { if (one) SKIRT_TRACE(kOctreeNodes, true); else SKIRT_TRACE(kOctreeNodes, false); }
 #undef SKIRT_TRACE
     };
-    // iteration it (parity q = it & 1): the event kernel consumes active list ctr[2+q] and queues rays
-    // into ctr[q] and the next active list into ctr[2+1-q]; the trace kernel walks the ctr[q] rays and
-    // resets ctr[1-q] and ctr[2+q] for the next iteration. The host polls the active count every few
-    // iterations -- the only host synchronization of the phase.
-    int it = 0;
-    const int pollEvery = 4;
-    while (true) {
-        a.parity = it & 1;
-        a.init = (it == 0) ? 1 : 0;
-        launchEvent(a);
-        HIPCHECK(c, hipGetLastError());
-        if (!a.hasDust) { it++; break; }  // without dust every packet completes inside the event kernel
-        if ((int)c->traceEv.size() < 2 * (c->traceLaunches + 1)) {
-            hipEvent_t e0, e1;
-            HIPCHECK(c, hipEventCreate(&e0));
-            HIPCHECK(c, hipEventCreate(&e1));
-            c->traceEv.push_back(e0);
-            c->traceEv.push_back(e1);
+    if ((int)c->pollEv.size() < kHalves * kPollRing) {
+        while ((int)c->pollEv.size() < kHalves * kPollRing) {
+            hipEvent_t e;
+            HIPCHECK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            c->pollEv.push_back(e);
         }
-        HIPCHECK(c, hipEventRecord(c->traceEv[2 * c->traceLaunches], c->stream));
-        launchTrace(a);
-        HIPCHECK(c, hipGetLastError());
-        HIPCHECK(c, hipEventRecord(c->traceEv[2 * c->traceLaunches + 1], c->stream));
-        c->traceLaunches++;
-        if (a.ninstr > 0) {
-            hipLaunchKernelGGL(detectKernel, dim3(dgrid), dim3(kBlock), lds, c->stream, a);
-            HIPCHECK(c, hipGetLastError());
-        }
-        it++;
-        if (it % pollEvery == 0) {
-            HIPCHECK(c, hipMemcpyAsync(c->hCtr, c->dCtr, 8 * sizeof(unsigned int), hipMemcpyDeviceToHost, c->stream));
-            HIPCHECK(c, hipStreamSynchronize(c->stream));
-            if (c->hCtr[2 + (it & 1)] == 0) break;  // no slot has a ray in flight: the phase is over
-        }
-        if (it > 10000000) return fail(c, SKIRT_ERR_STATE, "photon phase did not terminate");
     }
+    // Per half, iteration it (parity q = it & 1): the event kernel consumes active list ctr[2+q] and
+    // queues rays into ctr[q] and the next active list into ctr[2+1-q]; the trace kernel walks the
+    // ctr[q] rays and resets ctr[1-q] and ctr[2+q] for the next iteration; the detect kernel turns the
+    // finished peel-off rays into detections. Every kPollEvery iterations the half's counters are
+    // copied to pinned memory behind an event; the host reads each copy kPollRing copies later (by
+    // then long complete), so it never drains a stream. A half whose active count was 0 is finished;
+    // the few iterations launched after that point find no work and exit at once.
+    Args ah[kHalves];
+    int its[kHalves] = {0}, polls[kHalves] = {0};
+    int pollIt[kHalves][kPollRing] = {};  // the iteration count each copy was taken at
+    bool done[kHalves] = {false};
+    for (int h = 0; h < kHalves; h++) {
+        ah[h] = a;
+        carvePool(c, ah[h], h);
+    }
+    int total = 0;
+    while (true) {
+        bool all = true;
+        for (int h = 0; h < kHalves; h++) {
+            if (done[h]) continue;
+            all = false;
+            Args& aa = ah[h];
+            hipStream_t st = streams[h];
+            aa.parity = its[h] & 1;
+            aa.init = (its[h] == 0) ? 1 : 0;
+            launchEvent(aa, st);
+            HIPCHECK(c, hipGetLastError());
+            if (!a.hasDust) { done[h] = true; its[h]++; continue; }  // every packet completes in the event kernel
+            if ((int)c->traceEv.size() < 2 * (c->traceLaunches + 1)) {
+                hipEvent_t e0, e1;
+                HIPCHECK(c, hipEventCreate(&e0));
+                HIPCHECK(c, hipEventCreate(&e1));
+                c->traceEv.push_back(e0);
+                c->traceEv.push_back(e1);
+            }
+            HIPCHECK(c, hipEventRecord(c->traceEv[2 * c->traceLaunches], st));
+            launchTrace(aa, st);
+            HIPCHECK(c, hipGetLastError());
+            HIPCHECK(c, hipEventRecord(c->traceEv[2 * c->traceLaunches + 1], st));
+            c->traceLaunches++;
+            if (a.ninstr > 0) {
+                hipLaunchKernelGGL(detectKernel, dim3(dgrid), dim3(kBlock), lds, st, aa);
+                HIPCHECK(c, hipGetLastError());
+            }
+            its[h]++;
+            total++;
+            if (its[h] % kPollEvery == 0) {
+                const int slot = polls[h] % kPollRing;
+                unsigned int* hc = c->hCtr + (h * kPollRing + slot) * 8;
+                hipEvent_t pe = c->pollEv[h * kPollRing + slot];
+                if (polls[h] >= kPollRing) {
+                    // the copy made kPollRing polls ago: is the half finished?
+                    HIPCHECK(c, hipEventSynchronize(pe));
+                    if (hc[2 + (pollIt[h][slot] & 1)] == 0) { done[h] = true; continue; }
+                }
+                HIPCHECK(c, hipMemcpyAsync(hc, aa.ctr, 8 * sizeof(unsigned int), hipMemcpyDeviceToHost, st));
+                HIPCHECK(c, hipEventRecord(pe, st));
+                pollIt[h][slot] = its[h];
+                polls[h]++;
+            }
+            if (its[h] > 10000000) return fail(c, SKIRT_ERR_STATE, "photon phase did not terminate");
+        }
+        if (all) break;
+    }
+    int it = total;
     c->lastIterations = it;
+    HIPCHECK(c, hipEventRecord(c->evJoin, c->aux));
+    HIPCHECK(c, hipStreamWaitEvent(c->stream, c->evJoin, 0));
     HIPCHECK(c, hipEventRecord(c->ev1, c->stream));
     return SKIRT_OK;
 }
@@ -1995,6 +2055,10 @@ void skirt_mcrt_destroy(SkirtMcrt* c) {
     if (c->ownLabs && c->dLabs) (void)hipFree(c->dLabs);
     if (c->ownTally && c->dTally) (void)hipFree(c->dTally);
     for (hipEvent_t e : c->traceEv) (void)hipEventDestroy(e);
+    for (hipEvent_t e : c->pollEv) (void)hipEventDestroy(e);
+    if (c->evFork) (void)hipEventDestroy(c->evFork);
+    if (c->evJoin) (void)hipEventDestroy(c->evJoin);
+    if (c->aux) (void)hipStreamDestroy(c->aux);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->own) (void)hipStreamDestroy(c->own);
