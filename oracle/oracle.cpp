@@ -13,6 +13,7 @@
 #include <thread>
 #include <vector>
 
+#include "../skirt_amd/csrc/host/dustemission.hpp"
 #include "../skirt_amd/csrc/host/model.hpp"
 #include "../skirt_amd/csrc/host/outputs.hpp"
 
@@ -596,6 +597,52 @@ public:
         Vec3 k = isotropic(rng);
         pp = Packet{Lw, ell, pos, k, 0, h};
     }
+
+    // the launch of dodustemissionchunk (biased cell choice, PanMonteCarloSimulation.cpp:296-325) and
+    // of dodustselfabsorptionchunk (natural cell choice, :207-216): cell, random position in the cell
+    // (Random::position(box), Random.cpp:226-234), isotropic direction; PhotonPackage::launch makes the
+    // packet a dust packet (stellar = -1, PhotonPackage.cpp)
+    void launchCell(Rng& rng, Packet& pp, int ell, const CellSources& src, double L, bool biased, double xi) const {
+        int N = M.ncells();
+        const double* Lv = &src.lv[(size_t)ell * N];
+        const double* Xv = &src.cdf[(size_t)ell * (N + 1)];
+        auto locateClip = [&](double x) {
+            if (x < Xv[0]) return 0;
+            int jl = -1, ju = N;
+            while (ju - jl > 1) { int jm = (ju + jl) >> 1; if (x < Xv[jm]) ju = jm; else jl = jm; }
+            return jl;
+        };
+        double X = rng.uniform();
+        int m;
+        double Lw = L;
+        if (biased) {
+            if (X < xi) m = std::max(0, std::min(N - 1, static_cast<int>(N * X / xi)));
+            else m = locateClip((X - xi) / (1 - xi));
+            double Lmean = src.ltot[ell] / N;
+            double weight = 1.0 / (1 - xi + xi * Lmean / Lv[m]);
+            Lw = L * weight;
+        } else {
+            m = locateClip(X);
+        }
+        double b[6];
+        M.grid.cellBox(m, b);
+        double x = rng.uniform();
+        double y = rng.uniform();
+        double z = rng.uniform();
+        Vec3 pos{b[0] + x * (b[3] - b[0]), b[1] + y * (b[4] - b[1]), b[2] + z * (b[5] - b[2])};
+        Vec3 k = isotropic(rng);
+        pp = Packet{Lw, ell, pos, k, 0, -1};
+    }
+};
+
+// one photon phase: which packets, where their absorption goes
+struct PhaseSpec {
+    int phase = ORACLE_PHASE_STELLAR;
+    uint32_t tag = 0;                // Philox counter word 1: phase | cycle << 2 (the engine's convention)
+    uint64_t Npp = 0;                // packets per wavelength (setChunkParams with one chunk)
+    const CellSources* src = nullptr;
+    std::vector<double>* labs = nullptr;
+    bool store = false;
 };
 
 }  // namespace
@@ -603,6 +650,7 @@ public:
 struct OracleRun {
     std::unique_ptr<Model> model;
     Tallies tal;
+    std::vector<double> labsDustTotals;  // Labsdusttot after every self-absorption cycle
     double seconds = 0;
     uint64_t packets = 0;
 };
@@ -625,52 +673,62 @@ OracleRun* oracle_run(const char* ski, const char* datadir, int rngKind, int nth
         Model& M = *run->model;
         M.seed = theSeed;
         if (packages > 0) M.packages = packages;
-        (void)phases;
+        if (phases == 0) phases = ORACLE_PHASES_ALL;
         Sim sim(M);
         sim.initTallies(run->tal);
-        int Nl = M.wl.n();
-        uint64_t Npp = (uint64_t)std::ceil(M.packages);  // setChunkParams with one chunk
-        uint64_t total = Npp * (uint64_t)Nl;
-        uint64_t pb = packet_begin, pe = packet_end ? std::min<uint64_t>(packet_end, total) : total;
-        bool store = M.hasDust && M.storeAbsorption;
+        const int Nl = M.wl.n();
         auto t0 = std::chrono::steady_clock::now();
+        MTRng mtr(&mt);
 
-        if (rngKind == ORACLE_RNG_MT) {
-            // dostellaremissionchunk for chunk index ell = 0 .. Nlambda-1, one chunk per wavelength
-            MTRng rng(&mt);
-            Path p, tmp;
-            p.v.reserve(1024);
-            tmp.v.reserve(1024);
-            for (int ell = 0; ell < Nl; ell++) {
-                double L = M.starLtot[ell] / Npp;
-                if (!(L > 0)) continue;
+        // shoots packet pk of a phase (global index: ell = pk / Npp, as in the engine)
+        auto shoot = [&](const PhaseSpec& ph, Tallies& tl, Rng& rng, uint64_t pk, Path& p, Path& tmp,
+                         uint64_t& count) {
+            int ell = (int)(pk / ph.Npp);
+            Sim::Packet pp;
+            if (ph.phase == ORACLE_PHASE_STELLAR) {
+                double L = M.starLtot[ell] / ph.Npp;
+                if (!(L > 0)) return;  // dostellaremissionchunk skips the wavelength
                 double Lthreshold = L / M.minWeightReduction;
-                for (uint64_t i = 0; i < Npp; i++) {
-                    Sim::Packet pp;
-                    sim.launchStellar(rng, pp, ell, L);
-                    run->packets++;
-                    if (pp.L > 0) {
-                        if (M.hasDust)
-                            sim.lifeCycle(run->tal, rng, pp, Lthreshold, true, store, &run->tal.labs, p, tmp);
-                        else
-                            for (size_t q = 0; q < M.instruments.size(); q++) sim.detect(run->tal, (int)q, pp, tmp);
-                    }
+                sim.launchStellar(rng, pp, ell, L);
+                count++;
+                if (pp.L > 0) {
+                    if (M.hasDust) sim.lifeCycle(tl, rng, pp, Lthreshold, true, ph.store, ph.labs, p, tmp);
+                    else
+                        for (size_t q = 0; q < M.instruments.size(); q++) sim.detect(tl, (int)q, pp, tmp);
                 }
+            } else {
+                double Ltot = ph.src->ltot[ell];
+                if (!(Ltot > 0)) return;
+                double L = Ltot / ph.Npp;  // Lem (dust emission) or L (self-absorption)
+                double Lthreshold = L / M.minWeightReduction;
+                bool emission = ph.phase == ORACLE_PHASE_DUST_EMISSION;
+                sim.launchCell(rng, pp, ell, *ph.src, L, emission, M.dustEmissionBias);
+                count++;
+                sim.lifeCycle(tl, rng, pp, Lthreshold, emission, ph.store, ph.labs, p, tmp);
             }
-        } else {
-            int T = std::max(1, nthreads);
+        };
+        // runs a phase over packets [pb, pe): MT mode in the reference's -t 1 order (chunk = wavelength,
+        // packets in order), Philox mode over threads with one stream per packet
+        auto runPhase = [&](const PhaseSpec& ph, uint64_t pb, uint64_t pe) {
             Tallies& tl = run->tal;
+            if (rngKind == ORACLE_RNG_MT) {
+                Path p, tmp;
+                p.v.reserve(1024);
+                tmp.v.reserve(1024);
+                for (uint64_t pk = pb; pk < pe; pk++) shoot(ph, tl, mtr, pk, p, tmp, run->packets);
+                return;
+            }
+            int T = std::max(1, nthreads);
             tl.shared = true;
             std::vector<std::thread> th;
             std::atomic<uint64_t> next{pb};
-            std::atomic<uint64_t> segs{0};
             const uint64_t grain = 64;
             std::vector<std::string> errs(T);
             std::vector<uint64_t> cnt(T, 0);
             for (int w = 0; w < T; w++) {
                 th.emplace_back([&, w] {
                     try {
-                        PhiloxRng rng(theSeed, 0);
+                        PhiloxRng rng(theSeed, ph.tag);
                         Path p, tmp;
                         p.v.reserve(1024);
                         tmp.v.reserve(1024);
@@ -679,20 +737,8 @@ OracleRun* oracle_run(const char* ski, const char* datadir, int rngKind, int nth
                             if (b >= pe) break;
                             uint64_t e = std::min(pe, b + grain);
                             for (uint64_t pk = b; pk < e; pk++) {
-                                int ell = (int)(pk / Npp);
-                                double L = M.starLtot[ell] / Npp;
-                                if (!(L > 0)) continue;
-                                double Lthreshold = L / M.minWeightReduction;
                                 rng.start(pk);
-                                Sim::Packet pp;
-                                sim.launchStellar(rng, pp, ell, L);
-                                cnt[w]++;
-                                if (pp.L > 0) {
-                                    if (M.hasDust)
-                                        sim.lifeCycle(tl, rng, pp, Lthreshold, true, store, &tl.labs, p, tmp);
-                                    else
-                                        for (size_t q = 0; q < M.instruments.size(); q++) sim.detect(tl, (int)q, pp, tmp);
-                                }
+                                shoot(ph, tl, rng, pk, p, tmp, cnt[w]);
                             }
                         }
                     } catch (std::exception& ex) {
@@ -701,14 +747,63 @@ OracleRun* oracle_run(const char* ski, const char* datadir, int rngKind, int nth
                 });
             }
             for (auto& x : th) x.join();
+            tl.shared = false;
             for (int w = 0; w < T; w++)
                 if (!errs[w].empty()) throw std::runtime_error(errs[w]);
             for (int w = 0; w < T; w++) run->packets += cnt[w];
-            tl.shared = false;
+        };
+
+        // ---- runstellaremission (MonteCarloSimulation.cpp:251-261)
+        if (phases & ORACLE_PHASES_STELLAR) {
+            PhaseSpec ph;
+            ph.Npp = (uint64_t)std::ceil(M.packages);
+            ph.store = M.hasDust && M.storeAbsorption;
+            ph.labs = &run->tal.labs;
+            uint64_t total = ph.Npp * (uint64_t)Nl;
+            uint64_t pb = packet_begin, pe = packet_end ? std::min<uint64_t>(packet_end, total) : total;
+            runPhase(ph, pb, pe);
+        }
+        // ---- rundustselfabsorption + rundustemission (PanMonteCarloSimulation::runSelf, .cpp:96-105)
+        if ((phases & ORACLE_PHASES_DUST) && M.hasDust && M.dustEmission) {
+            std::vector<PlanckTable> tables = planckTables(M);
+            std::vector<double> lum;
+            CellSources src;
+            uint32_t cycleIndex = 0;
+            if (M.selfAbsorption) {
+                run->tal.labsDust.assign(run->tal.labs.size(), 0.0);
+                SelfAbsorptionSchedule sched;
+                sched.fixedCycles = M.cycles;
+                while (sched.next()) {
+                    // calculatedustemission, then Labsbolv = Labs(m), then rebootLabsdust
+                    dustEmissionSpectra(M, tables, totalLabs(M, run->tal.labs, &run->tal.labsDust), lum);
+                    cellSources(M, run->tal.labs, &run->tal.labsDust, lum, src);
+                    std::fill(run->tal.labsDust.begin(), run->tal.labsDust.end(), 0.0);
+                    PhaseSpec ph;
+                    ph.phase = ORACLE_PHASE_DUST_SELFABS;
+                    ph.tag = ORACLE_PHASE_DUST_SELFABS | (cycleIndex++ << 2);
+                    ph.Npp = (uint64_t)std::ceil(M.packages * SelfAbsorptionSchedule::factor(sched.stage));
+                    ph.src = &src;
+                    ph.labs = &run->tal.labsDust;
+                    ph.store = true;
+                    runPhase(ph, 0, ph.Npp * (uint64_t)Nl);
+                    run->labsDustTotals.push_back(tableTotal(run->tal.labsDust));
+                    sched.finishCycle(run->labsDustTotals.back());
+                }
+            }
+            const std::vector<double>* dust = M.selfAbsorption ? &run->tal.labsDust : nullptr;
+            dustEmissionSpectra(M, tables, totalLabs(M, run->tal.labs, dust), lum);
+            cellSources(M, run->tal.labs, dust, lum, src);
+            PhaseSpec ph;
+            ph.phase = ORACLE_PHASE_DUST_EMISSION;
+            ph.tag = ORACLE_PHASE_DUST_EMISSION;
+            ph.Npp = (uint64_t)std::ceil(M.packages * M.emissionBoost);
+            ph.src = &src;
+            runPhase(ph, 0, ph.Npp * (uint64_t)Nl);
         }
         run->seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
         if (outprefix && *outprefix) {
-            writeOutputs(M, outprefix, run->tal.frames, run->tal.seds, run->tal.labs);
+            const std::vector<double>* dust = run->tal.labsDust.empty() ? nullptr : &run->tal.labsDust;
+            writeOutputs(M, outprefix, run->tal.frames, run->tal.seds, totalLabs(M, run->tal.labs, dust));
         }
         return run.release();
     } catch (std::exception& ex) {
@@ -735,6 +830,13 @@ int oracle_instrument(OracleRun* r, int i, const double** frames, const double**
     *nframe = ins.hasFrames() ? ins.nframe() : 0;
     *nlambda = r->model->wl.n();
     return 0;
+}
+
+const double* oracle_labs_dust(OracleRun* r) { return r->tal.labsDust.empty() ? nullptr : r->tal.labsDust.data(); }
+
+int oracle_selfabs_cycles(OracleRun* r, const double** totals) {
+    *totals = r->labsDustTotals.empty() ? nullptr : r->labsDustTotals.data();
+    return (int)r->labsDustTotals.size();
 }
 
 double oracle_seconds(OracleRun* r) { return r->seconds; }

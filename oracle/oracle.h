@@ -30,7 +30,10 @@ extern "C" {
 #endif
 
 enum { ORACLE_RNG_MT = 0, ORACLE_RNG_PHILOX = 1 };
-enum { ORACLE_PHASE_STELLAR = 0, ORACLE_PHASE_ALL = 1 };
+/* photon phases (the engine's SKIRT_PHASE_* values; Philox tag = phase | cycle << 2) */
+enum { ORACLE_PHASE_STELLAR = 0, ORACLE_PHASE_DUST_EMISSION = 1, ORACLE_PHASE_DUST_SELFABS = 2 };
+/* `phases` argument of oracle_run: which of the simulation's phases run (0 = all it has) */
+enum { ORACLE_PHASES_STELLAR = 1, ORACLE_PHASES_DUST = 2, ORACLE_PHASES_ALL = 3 };
 
 typedef struct OracleRun OracleRun;
 
@@ -39,8 +42,10 @@ typedef struct OracleRun OracleRun;
  *  nthreads     worker threads (Philox mode only; MT mode is single-threaded by definition)
  *  packages     if > 0, overrides the ski's packages (photon packets per wavelength)
  *  seed         if nonzero, overrides the ski's random seed
- *  packet_begin/packet_end  Philox mode only: restrict the stellar phase to this global packet range
- *               (end == 0 means all packets)
+ *  packet_begin/packet_end  restrict the stellar phase to this global packet range (end == 0: all)
+ *  phases       ORACLE_PHASES_* mask; 0 runs every phase of the simulation: stellar emission, then for
+ *               a Pan dust system with dust emission the self-absorption cycles (if enabled) and the
+ *               dust emission phase (PanMonteCarloSimulation::runSelf)
  *  outprefix    if non-NULL, writes SKIRT-format outputs (<prefix>_<instr>_sed.dat, FITS frames, ds_isrf)
  * Returns NULL on failure (see oracle_last_error()). */
 OracleRun* oracle_run(const char* ski, const char* datadir, int rng, int nthreads, double packages,
@@ -48,8 +53,12 @@ OracleRun* oracle_run(const char* ski, const char* datadir, int rng, int nthread
                       const char* outprefix);
 const char* oracle_last_error(void);
 
-/* Labs(m, ell) row-major, Ncells x Nlambda (stellar + dust), as DustSystem::Labs */
+/* stellar Labs(m, ell) row-major, Ncells x Nlambda (PanDustSystem::_Labsstelvv) */
 const double* oracle_labs(OracleRun* r, int* ncells, int* nlambda);
+/* dust Labs of the last self-absorption cycle (PanDustSystem::_Labsdustvv), or NULL */
+const double* oracle_labs_dust(OracleRun* r);
+/* Labsdusttot after every self-absorption cycle; returns the number of cycles */
+int oracle_selfabs_cycles(OracleRun* r, const double** totals);
 /* instrument accumulators before calibration: frames [nslots][nlambda][nframe], seds [nslots][nlambda] */
 int oracle_instrument(OracleRun* r, int i, const double** frames, const double** seds, int* nslots,
                       int* nframe, int* nlambda);

@@ -22,13 +22,19 @@ run() {  # run <ski> <seed> <tag>
       *) cp "$f" "$OUT/" ;;
     esac
   done
-  grep -h "Finished the stellar emission phase\|Total number of\|Total extinction" "$WORK/$tag"_log.txt > "$OUT/${tag}_log_excerpt.txt" || true
+  grep -h "Finished the stellar emission phase\|Total number of\|Total extinction\|absorbed dust luminosity\|absorbed stellar luminosity\|Convergence" "$WORK/$tag"_log.txt > "$OUT/${tag}_log_excerpt.txt" || true
 }
-run c1_oligo16 4357 c1_oligo16_s4357
-run c1_oligo16 777 c1_oligo16_s777
-run oligo_2comp 1234 oligo_2comp_s1234
-run pan_cart16 4357 pan_cart16_s4357
-run pan_oct 4357 pan_oct_s4357
-run pan_oct 99 pan_oct_s99
+all() {
+  run c1_oligo16 4357 c1_oligo16_s4357
+  run c1_oligo16 777 c1_oligo16_s777
+  run oligo_2comp 1234 oligo_2comp_s1234
+  run pan_cart16 4357 pan_cart16_s4357
+  run pan_oct 4357 pan_oct_s4357
+  run pan_oct 99 pan_oct_s99
+  run pan_cart16_sa 4357 pan_cart16_sa_s4357
+  run pan_cart16_sac 4357 pan_cart16_sac_s4357
+}
+# usage: make_fixtures.sh [ski seed tag]   (no arguments: every fixture)
+if [ $# -eq 3 ]; then run "$1" "$2" "$3"; else all; fi
 rm -rf "$WORK"
 ls -la "$OUT"

@@ -13,6 +13,7 @@ DATA_DIR = os.path.join(REPO, "skirt_amd", "data")
 
 RNG_MT = 0
 RNG_PHILOX = 1
+PHASES_STELLAR, PHASES_DUST, PHASES_ALL = 1, 2, 3  # oracle_run's phase mask (oracle.h)
 
 _lib = None
 
@@ -42,6 +43,9 @@ def lib():
         L.oracle_segments.restype = ctypes.c_uint64
         L.oracle_segments.argtypes = [ctypes.c_void_p]
         L.oracle_free.argtypes = [ctypes.c_void_p]
+        L.oracle_labs_dust.restype = ctypes.POINTER(ctypes.c_double)
+        L.oracle_labs_dust.argtypes = [ctypes.c_void_p]
+        L.oracle_selfabs_cycles.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.POINTER(ctypes.c_double))]
         L.oracle_philox4x32_10.argtypes = [ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32),
                                            ctypes.POINTER(ctypes.c_uint32)]
         _lib = L
@@ -66,15 +70,23 @@ class OracleResult:
             self.frames.append(np.ctypeslib.as_array(fp, shape=(ns.value, nlam.value, nf.value)).copy()
                                if fp else None)
             self.seds.append(np.ctypeslib.as_array(sp, shape=(ns.value, nlam.value)).copy() if sp else None)
+        pd = L.oracle_labs_dust(handle)
+        self.labs_dust = (np.ctypeslib.as_array(pd, shape=(self.ncells, self.nlambda)).copy() if pd else None)
+        tp = ctypes.POINTER(ctypes.c_double)()
+        n = L.oracle_selfabs_cycles(handle, ctypes.byref(tp))
+        self.labs_dust_totals = [tp[i] for i in range(n)] if n else []
         self.seconds = L.oracle_seconds(handle)
         self.packets = L.oracle_packets(handle)
         self.segments = L.oracle_segments(handle)
 
 
-def run(ski, rng=RNG_MT, threads=1, packages=0.0, seed=0, packet_begin=0, packet_end=0, outprefix=None):
+def run(ski, rng=RNG_MT, threads=1, packages=0.0, seed=0, packet_begin=0, packet_end=0, outprefix=None,
+        phases=PHASES_STELLAR):
+    """Runs the oracle; by default only the stellar emission phase (phases=PHASES_ALL adds the dust
+    self-absorption and dust emission phases of a Pan simulation with dust emission)."""
     L = lib()
     h = L.oracle_run(ski.encode(), DATA_DIR.encode(), rng, threads, float(packages), seed, packet_begin,
-                     packet_end, 0, outprefix.encode() if outprefix else None)
+                     packet_end, phases, outprefix.encode() if outprefix else None)
     if not h:
         raise RuntimeError("oracle failed: " + L.oracle_last_error().decode())
     try:

@@ -1,10 +1,11 @@
 """The CPU oracle against the reference's own outputs (`skirt -t 1`, tests/golden/ref).
 
 The oracle in MT mode restates the reference's photon life cycle and random-number consumption
-exactly, so every stellar-phase output must match the reference digit for digit (SED text at 9
-significant digits, FITS frames as float32 bit patterns, ds_isrf per-cell mean intensities at 6 digits,
-which pins Labs(cell, wavelength) for every cell). Outputs that depend on the dust-emission phase
-(dust columns, total frames of Pan runs) are out of this tier's scope and are not compared.
+exactly -- stellar emission, and for Pan simulations with dust emission the self-absorption cycles
+and the dust emission phase -- so every output must match the reference digit for digit (SED text at
+9 significant digits including the dust columns, FITS frames as float32 bit patterns including the
+dust and total frames, ds_isrf per-cell mean intensities at 6 digits, which pins Labs(cell,
+wavelength) for every cell).
 """
 import glob
 import os
@@ -16,8 +17,8 @@ import oracle_lib as O
 import skirt_files as F
 
 RUNS = [("c1_oligo16", 4357), ("c1_oligo16", 777), ("oligo_2comp", 1234), ("pan_cart16", 4357),
-        ("pan_oct", 4357), ("pan_oct", 99)]
-DUST_EMISSION_OUTPUTS = ("_dust.fits", "_dustscattered.fits")
+        ("pan_oct", 4357), ("pan_oct", 99), ("pan_cart16_sa", 4357), ("pan_cart16_sac", 4357)]
+LSUN = 3.839e26  # W (Units.cpp)
 
 
 def _compare_outputs(golden_dir, tag, outdir, pan):
@@ -27,18 +28,11 @@ def _compare_outputs(golden_dir, tag, outdir, pan):
         if "log_excerpt" in base or "ds_mix" in base:
             continue
         mine = os.path.join(outdir, base)
-        if pan and (base.endswith(DUST_EMISSION_OUTPUTS) or base.endswith("_total.fits")):
-            continue  # dust emission phase contributes (out of scope)
         assert os.path.exists(mine), base
         if base.endswith(".fits"):
             a, b = F.read_fits(ref), F.read_fits(mine)
             assert a.shape == b.shape, base
             assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), base
-        elif base.endswith("_sed.dat") and pan:
-            a, b = F.read_text_tokens(ref), F.read_text_tokens(mine)
-            # columns: lambda, total, direct, scattered, dust, dustscattered, transparent, levels...
-            keep = [0, 2, 3, 6] + list(range(7, len(a[0])))
-            assert [[r[k] for k in keep] for r in a] == [[r[k] for k in keep] for r in b], base
         elif base.endswith("_ds_cellprops.dat"):
             a, b = F.read_text_tokens(ref), F.read_text_tokens(mine)
             assert a[:len(b)] == b, base  # the reference appends statistics lines
@@ -52,9 +46,21 @@ def _compare_outputs(golden_dir, tag, outdir, pan):
 def test_oracle_matches_reference_bit_for_bit(golden_dir, tmp_path, ski, seed):
     tag = "%s_s%d" % (ski, seed)
     O.run(os.path.join(golden_dir, "ski", ski + ".ski"), rng=O.RNG_MT, seed=seed,
-          outprefix=str(tmp_path / tag))
+          outprefix=str(tmp_path / tag), phases=O.PHASES_ALL)
     n = _compare_outputs(golden_dir, tag, str(tmp_path), pan=ski.startswith("pan"))
     assert n >= 2
+
+
+@pytest.mark.parametrize("ski", ["pan_cart16_sa", "pan_cart16_sac"])
+def test_selfabsorption_cycles_match_the_reference_log(golden_dir, ski):
+    """Every self-absorption cycle's total absorbed dust luminosity, and the number of cycles the
+    convergence criteria run (PanMonteCarloSimulation.cpp:109-181), as the reference logged them."""
+    log = open(os.path.join(golden_dir, "ref", ski + "_s4357_log_excerpt.txt")).read().splitlines()
+    ref = [float(l.split(" is ")[1].split()[0]) for l in log if "total absorbed dust luminosity" in l]
+    r = O.run(os.path.join(golden_dir, "ski", ski + ".ski"), rng=O.RNG_MT, seed=4357, phases=O.PHASES_ALL)
+    mine = [t / LSUN for t in r.labs_dust_totals]
+    assert len(mine) == len(ref)
+    np.testing.assert_allclose(mine, ref, rtol=6e-6)
 
 
 def test_philox_known_answers():
