@@ -44,6 +44,16 @@ int skirt_sim_attach(SkirtSim* sim, int device);
 SkirtMcrt* skirt_sim_engine(SkirtSim* sim);
 /* stellar emission over global packets [first, first+count) (count 0 = all); asynchronous */
 int skirt_sim_run_stellar(SkirtSim* sim, uint64_t first, uint64_t count);
+/* PanMonteCarloSimulation::runSelf after the stellar phase (PanMonteCarloSimulation.cpp:96-105): for a
+ * Pan dust system with dust emission, the self-absorption cycles (if enabled; host-side grey-body
+ * spectra and cell sources between cycles, convergence as the reference) and the dust emission phase,
+ * whose detections add to the instrument tallies. Single process; fetches the stellar Labs first.
+ * Returns after launching the dust emission phase (asynchronous, like run_stellar). */
+int skirt_sim_run_dust(SkirtSim* sim);
+/* dust Labs of the last self-absorption cycle (row-major cell x wavelength), or NULL */
+const double* skirt_sim_labs_dust(SkirtSim* sim);
+/* Labsdusttot after every self-absorption cycle; returns the number of cycles */
+int skirt_sim_selfabs_totals(SkirtSim* sim, const double** totals);
 /* waits and copies the device tallies into the host accumulators */
 int skirt_sim_fetch(SkirtSim* sim);
 /* host accumulators after skirt_sim_fetch (same layouts as include/skirt_mcrt.h) */

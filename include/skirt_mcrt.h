@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define SKIRT_MCRT_ABI_VERSION 2
+#define SKIRT_MCRT_ABI_VERSION 3
 
 enum {
     SKIRT_OK = 0,
@@ -103,6 +103,18 @@ typedef struct {
     double xpmin, xpsiz, ypmin, ypsiz;
 } SkirtInstrDesc;
 
+/* Cell sources of a dust phase (the per-chunk cell distribution of PanMonteCarloSimulation.cpp:193-205
+ * and 273-294): per wavelength the luminosity Labsbol(m) * dustluminosity(m, ell) of every dust cell
+ * (reference cell order), its normalized cumulative distribution NR::cdf over the cells, and the total.
+ * emission_bias is PanDustSystem::emissionBias (used by the dust emission phase). */
+typedef struct {
+    int ncells, nlambda;
+    const double* lv;           /* nlambda x ncells */
+    const double* cdf;          /* nlambda x (ncells + 1) */
+    const double* ltot;         /* nlambda */
+    double emission_bias;
+} SkirtCellSourceDesc;
+
 /* MonteCarloSimulation properties used by the photon loop (MonteCarloSimulation.cpp:31-35). */
 typedef struct {
     double min_weight_reduction;
@@ -144,6 +156,22 @@ int skirt_mcrt_zero_tallies(SkirtMcrt* ctx);
  * per wavelength (packet p has wavelength index p / npp). Asynchronous. */
 int skirt_mcrt_run_stellar(SkirtMcrt* ctx, uint64_t npp, uint64_t first, uint64_t count, uint64_t seed,
                            const SkirtPhaseParams* params);
+/* One photon phase over global packets [first, first+count) of npp*nlambda (packet p has wavelength
+ * p / npp and its own random stream, selected by phase and cycle):
+ *   SKIRT_PHASE_STELLAR       as skirt_mcrt_run_stellar (cycle ignored)
+ *   SKIRT_PHASE_DUST_EMISSION dodustemissionchunk (PanMonteCarloSimulation.cpp:269-344): packets from the
+ *                             uploaded cell sources with the emission bias, peel-off on, no absorption stored
+ *   SKIRT_PHASE_DUST_SELFABS  dodustselfabsorptionchunk (:187-240): natural cell choice, no peel-off,
+ *                             absorption into the dust Labs tally; `cycle` numbers the self-absorption
+ *                             cycles of the simulation (0, 1, ...) */
+int skirt_mcrt_run_phase(SkirtMcrt* ctx, int phase, uint32_t cycle, uint64_t npp, uint64_t first, uint64_t count,
+                         uint64_t seed, const SkirtPhaseParams* params);
+int skirt_mcrt_upload_cell_sources(SkirtMcrt* ctx, const SkirtCellSourceDesc* src);
+/* the dust Labs tally (PanDustSystem::_Labsdustvv; device layout as Labs): bind caller memory (e.g. a torch
+ * tensor to all-reduce), zero it (rebootLabsdust) and copy it to host row-major (cell, wavelength) */
+int skirt_mcrt_bind_dust_labs(SkirtMcrt* ctx, double* d_labs_dust);
+int skirt_mcrt_zero_dust_labs(SkirtMcrt* ctx);
+int skirt_mcrt_download_dust_labs(SkirtMcrt* ctx, double* labs_dust);
 int skirt_mcrt_synchronize(SkirtMcrt* ctx);
 /* Copies tallies to host (Labs converted to row-major cell x wavelength); either pointer may be NULL. */
 int skirt_mcrt_download(SkirtMcrt* ctx, double* labs, double* instr);

@@ -54,10 +54,11 @@ ABI_SYMBOLS = [
     "skirt_mcrt_upload_media", "skirt_mcrt_upload_sources", "skirt_mcrt_set_instruments",
     "skirt_mcrt_tally_sizes", "skirt_mcrt_bind_tallies", "skirt_mcrt_zero_tallies", "skirt_mcrt_run_stellar",
     "skirt_mcrt_synchronize", "skirt_mcrt_download", "skirt_mcrt_stats", "skirt_mcrt_configure",
-    "skirt_mcrt_last_error", "skirt_mcrt_destroy",
+    "skirt_mcrt_last_error", "skirt_mcrt_destroy", "skirt_mcrt_run_phase", "skirt_mcrt_upload_cell_sources",
+    "skirt_mcrt_bind_dust_labs", "skirt_mcrt_zero_dust_labs", "skirt_mcrt_download_dust_labs",
     "skirt_sim_load", "skirt_sim_info", "skirt_sim_attach", "skirt_sim_engine", "skirt_sim_run_stellar",
     "skirt_sim_fetch", "skirt_sim_labs", "skirt_sim_instrument", "skirt_sim_set_tallies", "skirt_sim_write",
-    "skirt_sim_error", "skirt_sim_free",
+    "skirt_sim_error", "skirt_sim_free", "skirt_sim_run_dust", "skirt_sim_labs_dust", "skirt_sim_selfabs_totals",
 ]
 
 _lib = None
@@ -80,6 +81,10 @@ def lib():
         L.skirt_sim_engine.argtypes = [vp]
         L.skirt_sim_run_stellar.argtypes = [vp, c_u64, c_u64]
         L.skirt_sim_fetch.argtypes = [vp]
+        L.skirt_sim_run_dust.argtypes = [vp]
+        L.skirt_sim_labs_dust.restype = ctypes.POINTER(c_dbl)
+        L.skirt_sim_labs_dust.argtypes = [vp]
+        L.skirt_sim_selfabs_totals.argtypes = [vp, ctypes.POINTER(ctypes.POINTER(c_dbl))]
         L.skirt_sim_labs.restype = ctypes.POINTER(c_dbl)
         L.skirt_sim_labs.argtypes = [vp]
         L.skirt_sim_instrument.restype = ctypes.POINTER(c_dbl)
@@ -152,6 +157,21 @@ class Simulation:
 
     def run_stellar(self, first=0, count=0):
         self._check(lib().skirt_sim_run_stellar(self._h, first, count))
+
+    def run_dust(self):
+        """Self-absorption cycles (if enabled) and the dust emission phase (PanMonteCarloSimulation::runSelf)."""
+        self._check(lib().skirt_sim_run_dust(self._h))
+
+    def labs_dust(self):
+        p = lib().skirt_sim_labs_dust(self._h)
+        if not p:
+            return None
+        return np.ctypeslib.as_array(p, shape=(self.info.ncells, self.info.nlambda)).copy()
+
+    def selfabs_totals(self):
+        tp = ctypes.POINTER(ctypes.c_double)()
+        n = lib().skirt_sim_selfabs_totals(self._h, ctypes.byref(tp))
+        return [tp[i] for i in range(n)] if n > 0 else []
 
     def synchronize(self):
         self._check_engine(lib().skirt_mcrt_synchronize(self.engine))

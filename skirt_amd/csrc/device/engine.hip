@@ -126,6 +126,13 @@ struct Args {
     const double* lumtot;
     const double* cdf;
     double emissionBias;
+    // dust-phase cell sources (PanMonteCarloSimulation.cpp:193-205, 273-294), reference cell order
+    const double* cellLv;        // [nlambda][ncells]
+    const double* cellCdf;       // [nlambda][ncells + 1]
+    const double* cellLtot;      // [nlambda]
+    double cellBias;             // PanDustSystem::emissionBias (dust emission phase)
+    const int* cellNode;         // octree: the leaf node of every reference cell
+    int phase, peel;             // SKIRT_PHASE_*; peel-off on
     // instruments
     int ninstr;
     const DevInstr* instr;
@@ -1097,9 +1104,82 @@ struct Events {
         p.kx = nx; p.ky = ny; p.kz = nz;
     }
 
-    // StellarSystem::launch + GeometricStellarComp::launch + PlummerGeometry sampling; false when no
-    // packet results (wavelength without luminosity, or a selected component without luminosity)
+    // false when no packet results (wavelength without luminosity, or a selected component without
+    // luminosity)
     __device__ __forceinline__ bool launch(Packet& p, unsigned long long idx) {
+        return a.phase == SKIRT_PHASE_STELLAR ? launchStellar(p, idx) : launchCell(p, idx);
+    }
+
+    // the launch of dodustemissionchunk (biased cell choice, PanMonteCarloSimulation.cpp:296-325) and of
+    // dodustselfabsorptionchunk (natural choice, :207-216): a cell, a uniform position in its box
+    // (Random::position, Random.cpp:226-234), an isotropic direction; a dust packet (stellar = -1)
+    __device__ __forceinline__ bool launchCell(Packet& p, unsigned long long idx) {
+        const int ell = (int)(idx / a.npp);
+        const double Ltot = a.cellLtot[ell];
+        if (!(Ltot > 0)) return false;  // the chunk emits nothing at this wavelength
+        packets++;
+        const double L0 = Ltot / (double)a.npp;
+        p.Lth = L0 / a.minWeightReduction;
+        p.rng.start(a.seed, a.tag, idx);
+        p.ell = ell;
+        const int N = a.ncells;
+        const double* cdf = a.cellCdf + (size_t)ell * (N + 1);
+        const double X = p.rng.uniform();
+        int m;
+        double L = L0;
+        if (a.phase == SKIRT_PHASE_DUST_EMISSION) {
+            const double xi = a.cellBias;
+            if (X < xi) m = max(0, min(N - 1, static_cast<int>(N * X / xi)));
+            else m = locateClipGlobal(cdf, N + 1, (X - xi) / (1 - xi));
+            const double Lmean = Ltot / N;
+            const double weight = 1.0 / (1 - xi + xi * Lmean / a.cellLv[(size_t)ell * N + m]);
+            L = L0 * weight;
+        } else {
+            m = locateClipGlobal(cdf, N + 1, X);
+        }
+        double b[6];
+        cellBox(m, b);
+        const double x = p.rng.uniform();
+        const double y = p.rng.uniform();
+        const double z = p.rng.uniform();
+        p.rx = b[0] + x * (b[3] - b[0]);
+        p.ry = b[1] + y * (b[4] - b[1]);
+        p.rz = b[2] + z * (b[5] - b[2]);
+        isotropic(p.rng, p.kx, p.ky, p.kz);
+        p.L = L;
+        p.nscatt = 0;
+        p.stellar = -1;
+        return true;
+    }
+
+    // NR::locate_clip over a table in global memory
+    __device__ static __forceinline__ int locateClipGlobal(const double* v, int n, double q) {
+        if (q < v[0]) return 0;
+        int jl = -1, ju = n - 1;
+        while (ju - jl > 1) {
+            const int jm = (ju + jl) >> 1;
+            if (q < v[jm]) ju = jm;
+            else jl = jm;
+        }
+        return jl;
+    }
+
+    // the box of reference cell m (CartesianDustGrid::box, TreeDustGrid::getnode(m)->extent())
+    __device__ __forceinline__ void cellBox(int m, double (&b)[6]) const {
+        if (GRID == SKIRT_GRID_CARTESIAN) {
+            const double* xv = sh.mesh;
+            const double* yv = xv + a.nx + 1;
+            const double* zv = yv + a.ny + 1;
+            const int i = m / (a.nz * a.ny), j = (m / a.nz) % a.ny, k = m % a.nz;
+            b[0] = xv[i]; b[1] = yv[j]; b[2] = zv[k]; b[3] = xv[i + 1]; b[4] = yv[j + 1]; b[5] = zv[k + 1];
+        } else {
+            const double* bx = a.box + 6 * (size_t)a.cellNode[m];
+            for (int q = 0; q < 6; q++) b[q] = bx[q];
+        }
+    }
+
+    // StellarSystem::launch + GeometricStellarComp::launch + PlummerGeometry sampling (see below)
+    __device__ __forceinline__ bool launchStellar(Packet& p, unsigned long long idx) {
         const int ell = (int)(idx / a.npp);
         const double L0 = a.lumtot[ell] / (double)a.npp;
         if (!(L0 > 0)) return false;  // dostellaremissionchunk skips such wavelengths
@@ -1225,7 +1305,7 @@ __global__ void __launch_bounds__(kBlock) eventKernel(const Args a) {
                 p.rx = p.rx + s * p.kx;
                 p.ry = p.ry + s * p.ky;
                 p.rz = p.rz + s * p.kz;
-                bool ok = a.ninstr > 0;
+                bool ok = a.ninstr > 0 && a.peel;
                 if (ok && !ONECOMP) { double I; ok = E.peelWeight(sh.instr[0], p, p.kx, p.ky, p.kz, I); }
                 if (ok) { peel = PEEL_SCATTER; ox = p.kx; oy = p.ky; oz = p.kz; }
                 E.scatter(p);
@@ -1246,8 +1326,11 @@ __global__ void __launch_bounds__(kBlock) eventKernel(const Args a) {
                 const unsigned long long idx = base + __popcll(nmask & ((1ull << lane) - 1ull));
                 if (idx >= total) need = false;  // exhausted: the slot retires
                 else if (E.launch(p, a.first + idx)) {
-                    if (a.hasDust) {
-                        peel = a.ninstr > 0 ? PEEL_EMISSION : PEEL_NONE;
+                    if (!(p.L > 0)) {
+                        // a zero-weight dust packet (a cell without emission drawn uniformly): every
+                        // tally it would touch receives 0, so it ends here
+                    } else if (a.hasDust) {
+                        peel = (a.ninstr > 0 && a.peel) ? PEEL_EMISSION : PEEL_NONE;
                         mainMode = RAY_FILL;
                         mainParam = p.L;
                         p.state = S_FILL;
@@ -1375,6 +1458,12 @@ struct SkirtMcrt {
     int nstar = 0;
     double *dGeomParam = nullptr, *dLum = nullptr, *dLumtot = nullptr, *dCdf = nullptr;
     double emissionBias = 0.5;
+    // dust-phase cell sources and the dust Labs tally
+    double *dCellLv = nullptr, *dCellCdf = nullptr, *dCellLtot = nullptr;
+    double cellBias = 0.5;
+    int* dCellNode = nullptr;
+    double* dLabsDust = nullptr;
+    bool ownLabsDust = true;
     // instruments
     std::vector<DevInstr> instr;
     DevInstr* dInstr = nullptr;
@@ -1638,6 +1727,10 @@ int skirt_mcrt_upload_grid(SkirtMcrt* c, const SkirtGridDesc* g) {
             }
             if (next != g->ncells) return fail(c, SKIRT_ERR_ARG, "octree leaves do not cover the cells");
         }
+        std::vector<int> cellNode(g->ncells, 0);
+        for (int l = 0; l < g->nnodes; l++)
+            if (g->first_child[l] < 0) cellNode[g->cellnumber[l]] = l;
+        if ((rc = upload(c, c->dCellNode, cellNode.data(), cellNode.size()))) return rc;
         std::vector<int> cn(g->cellnumber, g->cellnumber + g->nnodes);
         for (int l = 0; l < g->nnodes; l++)
             if (cn[l] >= 0) cn[l] = c->devCell[cn[l]];
@@ -1795,9 +1888,77 @@ int skirt_mcrt_zero_tallies(SkirtMcrt* c) {
 
 int skirt_mcrt_run_stellar(SkirtMcrt* c, uint64_t npp, uint64_t first, uint64_t count, uint64_t seed,
                            const SkirtPhaseParams* p) {
+    return skirt_mcrt_run_phase(c, SKIRT_PHASE_STELLAR, 0, npp, first, count, seed, p);
+}
+
+int skirt_mcrt_upload_cell_sources(SkirtMcrt* c, const SkirtCellSourceDesc* src) {
+    if (!c || !src) return SKIRT_ERR_ARG;
+    if (c->gridKind < 0) return fail(c, SKIRT_ERR_STATE, "upload the grid before cell sources");
+    if (src->ncells != c->ncells || src->nlambda != c->nlambda || !src->lv || !src->cdf || !src->ltot)
+        return fail(c, SKIRT_ERR_ARG, "cell sources do not match the grid and wavelengths");
+    if (!(src->emission_bias >= 0 && src->emission_bias < 1)) return fail(c, SKIRT_ERR_ARG, "emission bias outside [0,1)");
+    HIPCHECK(c, hipSetDevice(c->device));
+    const size_t nl = (size_t)c->nlambda, nc = (size_t)c->ncells;
+    int rc;
+    if ((rc = upload(c, c->dCellLv, src->lv, nl * nc))) return rc;
+    if ((rc = upload(c, c->dCellCdf, src->cdf, nl * (nc + 1)))) return rc;
+    if ((rc = upload(c, c->dCellLtot, src->ltot, nl))) return rc;
+    c->cellBias = src->emission_bias;
+    return SKIRT_OK;
+}
+
+static int ensureDustLabs(SkirtMcrt* c) {
+    const size_t nl = (size_t)c->ncells * c->nlambda;
+    if (!c->dLabsDust && nl) {
+        HIPCHECK(c, hipMalloc(&c->dLabsDust, nl * sizeof(double)));
+        HIPCHECK(c, hipMemsetAsync(c->dLabsDust, 0, nl * sizeof(double), c->stream));
+        c->ownLabsDust = true;
+    }
+    return SKIRT_OK;
+}
+
+int skirt_mcrt_bind_dust_labs(SkirtMcrt* c, double* d) {
+    if (!c || !d) return SKIRT_ERR_ARG;
+    if (c->ownLabsDust && c->dLabsDust) (void)hipFree(c->dLabsDust);
+    c->dLabsDust = d;
+    c->ownLabsDust = false;
+    return SKIRT_OK;
+}
+
+int skirt_mcrt_zero_dust_labs(SkirtMcrt* c) {
+    if (!c) return SKIRT_ERR_ARG;
+    HIPCHECK(c, hipSetDevice(c->device));
+    int rc = ensureDustLabs(c);
+    if (rc) return rc;
+    const size_t nl = (size_t)c->ncells * c->nlambda;
+    if (nl) HIPCHECK(c, hipMemsetAsync(c->dLabsDust, 0, nl * sizeof(double), c->stream));
+    return SKIRT_OK;
+}
+
+int skirt_mcrt_download_dust_labs(SkirtMcrt* c, double* labs) {
+    if (!c || !labs) return SKIRT_ERR_ARG;
+    int rc = skirt_mcrt_synchronize(c);
+    if (rc) return rc;
+    const size_t nl = (size_t)c->ncells * c->nlambda;
+    if (!c->dLabsDust) { std::fill(labs, labs + nl, 0.0); return SKIRT_OK; }
+    std::vector<double> t(nl);
+    HIPCHECK(c, hipMemcpy(t.data(), c->dLabsDust, nl * sizeof(double), hipMemcpyDeviceToHost));
+    const bool perm = !c->devCell.empty();
+    for (int ell = 0; ell < c->nlambda; ell++)
+        for (int m = 0; m < c->ncells; m++)
+            labs[(size_t)m * c->nlambda + ell] = t[(size_t)ell * c->ncells + (perm ? c->devCell[m] : m)];
+    return SKIRT_OK;
+}
+
+int skirt_mcrt_run_phase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, uint64_t first, uint64_t count,
+                         uint64_t seed, const SkirtPhaseParams* p) {
     if (!c || !p) return SKIRT_ERR_ARG;
+    if (phase < SKIRT_PHASE_STELLAR || phase > SKIRT_PHASE_DUST_SELFABS) return fail(c, SKIRT_ERR_ARG, "unknown phase");
+    if (cycle >= (1u << 30)) return fail(c, SKIRT_ERR_ARG, "cycle number too large");
+    const bool cellPhase = phase != SKIRT_PHASE_STELLAR;
+    if (cellPhase && (!c->dCellLtot || !p->has_dust)) return fail(c, SKIRT_ERR_STATE, "a dust phase needs a dust system and uploaded cell sources");
     if (c->gridKind < 0 && p->has_dust) return fail(c, SKIRT_ERR_STATE, "no grid uploaded");
-    if (!c->dLumtot) return fail(c, SKIRT_ERR_STATE, "no sources uploaded");
+    if (!cellPhase && !c->dLumtot) return fail(c, SKIRT_ERR_STATE, "no sources uploaded");
     if (p->has_dust && !c->dRho) return fail(c, SKIRT_ERR_STATE, "no media uploaded");
     if (npp == 0) return fail(c, SKIRT_ERR_ARG, "npp must be positive");
     if (first + count > npp * (uint64_t)c->nlambda) return fail(c, SKIRT_ERR_ARG, "packet range exceeds npp*nlambda");
@@ -1805,6 +1966,7 @@ int skirt_mcrt_run_stellar(SkirtMcrt* c, uint64_t npp, uint64_t first, uint64_t 
     HIPCHECK(c, hipSetDevice(c->device));
     int rc = ensureTallies(c);
     if (rc) return rc;
+    if (phase == SKIRT_PHASE_DUST_SELFABS && (rc = ensureDustLabs(c))) return rc;
     c->lastMs = 0;
     c->lastIterations = 0;
     c->traceLaunches = 0;
@@ -1839,13 +2001,21 @@ int skirt_mcrt_run_stellar(SkirtMcrt* c, uint64_t npp, uint64_t first, uint64_t 
     a.nstar = c->nstar; a.geomParam = c->dGeomParam; a.lum = c->dLum;
     a.lumtot = c->dLumtot; a.cdf = c->dCdf; a.emissionBias = c->emissionBias;
     a.ninstr = (int)c->instr.size(); a.instr = c->dInstr; a.nsed = c->nsed;
-    a.npp = npp; a.first = first; a.end = first + count; a.seed = seed; a.tag = SKIRT_PHASE_STELLAR;
+    a.npp = npp; a.first = first; a.end = first + count; a.seed = seed;
+    a.tag = (unsigned)phase | (cycle << 2);  // Philox counter word 1: streams differ per phase and cycle
+    a.phase = phase;
+    a.peel = phase != SKIRT_PHASE_DUST_SELFABS;
+    a.cellLv = c->dCellLv; a.cellCdf = c->dCellCdf; a.cellLtot = c->dCellLtot; a.cellBias = c->cellBias;
+    a.cellNode = c->dCellNode;
     a.minWeightReduction = p->min_weight_reduction; a.minScatt = p->min_scatt_events; a.xi = p->scatt_bias;
-    a.store = p->store_absorption ? 1 : 0;
+    // absorption: the stellar phase as its parameters say (into Labs), self-absorption always (into the
+    // dust Labs), dust emission never (MonteCarloSimulation.cpp:287, PanMonteCarloSimulation.cpp:223, 331)
+    a.store = phase == SKIRT_PHASE_STELLAR ? (p->store_absorption ? 1 : 0) : (phase == SKIRT_PHASE_DUST_SELFABS ? 1 : 0);
     a.hasDust = p->has_dust ? 1 : 0;
     if (a.store && !c->dLabs) return fail(c, SKIRT_ERR_STATE, "no Labs buffer");
     if ((uint64_t)c->ncells * (uint64_t)c->nlambda >= (1ull << 32)) return fail(c, SKIRT_ERR_UNSUPPORTED, "Labs table exceeds 2^32 entries");
-    a.labs = c->dLabs; a.tally = c->dTally;
+    a.labs = phase == SKIRT_PHASE_DUST_SELFABS ? c->dLabsDust : c->dLabs;
+    a.tally = c->dTally;
     a.error = c->dError; a.stats = c->dStats;
     a.claim = c->dClaim;
     a.threshold = c->threshold;
@@ -2046,7 +2216,7 @@ void skirt_mcrt_destroy(SkirtMcrt* c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     void* bufs[] = {c->dMesh, c->dBox, c->dFirstChild, c->dCellnumber, c->dNbrOffset, c->dNbrList, c->dTreeT,
-                    c->dLeafMap, c->dRho,
+                    c->dLeafMap, c->dCellLv, c->dCellCdf, c->dCellLtot, c->dCellNode, c->dRho,
                     c->dOptics, c->dGeomParam, c->dLum, c->dLumtot, c->dCdf, c->dInstr,
                     c->dClaim, c->dStats, c->dError, c->dCtr, c->dPool};
     for (void* b : bufs)
@@ -2054,6 +2224,7 @@ void skirt_mcrt_destroy(SkirtMcrt* c) {
     if (c->hCtr) (void)hipHostFree(c->hCtr);
     if (c->ownLabs && c->dLabs) (void)hipFree(c->dLabs);
     if (c->ownTally && c->dTally) (void)hipFree(c->dTally);
+    if (c->ownLabsDust && c->dLabsDust) (void)hipFree(c->dLabsDust);
     for (hipEvent_t e : c->traceEv) (void)hipEventDestroy(e);
     for (hipEvent_t e : c->pollEv) (void)hipEventDestroy(e);
     if (c->evFork) (void)hipEventDestroy(c->evFork);

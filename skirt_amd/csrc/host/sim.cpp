@@ -7,6 +7,7 @@
 #include <vector>
 
 #include "../../../include/skirt_host.h"
+#include "dustemission.hpp"
 #include "model.hpp"
 #include "outputs.hpp"
 
@@ -21,7 +22,9 @@ struct SkirtSim {
     double setupSeconds = 0;
     uint64_t npp = 0;
     SkirtMcrt* eng = nullptr;
-    std::vector<double> labs;                 // Ncells x Nlambda
+    std::vector<double> labs;                 // Ncells x Nlambda (stellar)
+    std::vector<double> labsDust;             // Ncells x Nlambda (last self-absorption cycle)
+    std::vector<double> dustTotals;           // Labsdusttot after every self-absorption cycle
     std::vector<double> instrAll;             // concatenated device layout
     std::vector<size_t> instrOff;             // per instrument offset into instrAll
     std::vector<std::vector<double>> frames, seds;
@@ -184,6 +187,66 @@ int skirt_sim_run_stellar(SkirtSim* s, uint64_t first, uint64_t count) {
     return check(s, skirt_mcrt_run_stellar(s->eng, s->npp, first, count, s->m.seed, &p));
 }
 
+int skirt_sim_run_dust(SkirtSim* s) {
+    if (!s || !s->eng) { g_err = "no engine attached"; return SKIRT_ERR_STATE; }
+    const Model& m = s->m;
+    if (!(m.hasDust && m.pan && m.dustEmission)) return SKIRT_OK;  // no dust emission: nothing to do
+    try {
+        int rc = skirt_sim_fetch(s);  // the stellar phase's Labs on the host
+        if (rc) return rc;
+        const int Nl = m.wl.n();
+        const std::vector<PlanckTable> tables = planckTables(m);
+        std::vector<double> lum;
+        CellSources src;
+        SkirtPhaseParams p{m.minWeightReduction, m.minScattEvents, m.scattBias, 0, 1};
+        auto upload = [&]() {
+            SkirtCellSourceDesc d{src.ncells, src.nlambda, src.lv.data(), src.cdf.data(), src.ltot.data(),
+                                  m.dustEmissionBias};
+            return check(s, skirt_mcrt_upload_cell_sources(s->eng, &d));
+        };
+        s->dustTotals.clear();
+        if (m.selfAbsorption) {
+            // PanMonteCarloSimulation::rundustselfabsorption (PanMonteCarloSimulation.cpp:109-181)
+            s->labsDust.assign(s->labs.size(), 0.0);
+            SelfAbsorptionSchedule sched;
+            sched.fixedCycles = m.cycles;
+            uint32_t cycle = 0;
+            while (sched.next()) {
+                dustEmissionSpectra(m, tables, totalLabs(m, s->labs, &s->labsDust), lum);
+                cellSources(m, s->labs, &s->labsDust, lum, src);
+                if ((rc = upload())) return rc;
+                if ((rc = check(s, skirt_mcrt_zero_dust_labs(s->eng)))) return rc;  // rebootLabsdust
+                uint64_t npp = (uint64_t)std::ceil(m.packages * SelfAbsorptionSchedule::factor(sched.stage));
+                if ((rc = check(s, skirt_mcrt_run_phase(s->eng, SKIRT_PHASE_DUST_SELFABS, cycle++, npp, 0,
+                                                        npp * (uint64_t)Nl, m.seed, &p))))
+                    return rc;
+                if ((rc = check(s, skirt_mcrt_download_dust_labs(s->eng, s->labsDust.data())))) return rc;
+                s->dustTotals.push_back(tableTotal(s->labsDust));
+                sched.finishCycle(s->dustTotals.back());
+            }
+        }
+        // PanMonteCarloSimulation::rundustemission (PanMonteCarloSimulation.cpp:245-264)
+        const std::vector<double>* dust = m.selfAbsorption ? &s->labsDust : nullptr;
+        dustEmissionSpectra(m, tables, totalLabs(m, s->labs, dust), lum);
+        cellSources(m, s->labs, dust, lum, src);
+        if ((rc = upload())) return rc;
+        uint64_t npp = (uint64_t)std::ceil(m.packages * m.emissionBoost);
+        return check(s, skirt_mcrt_run_phase(s->eng, SKIRT_PHASE_DUST_EMISSION, 0, npp, 0, npp * (uint64_t)Nl,
+                                             m.seed, &p));
+    } catch (std::exception& e) {
+        g_err = e.what();
+        return SKIRT_ERR_ARG;
+    }
+}
+
+const double* skirt_sim_labs_dust(SkirtSim* s) { return s && !s->labsDust.empty() ? s->labsDust.data() : nullptr; }
+
+int skirt_sim_selfabs_totals(SkirtSim* s, const double** totals) {
+    if (!s || !totals) return -1;
+    *totals = s->dustTotals.empty() ? nullptr : s->dustTotals.data();
+    return (int)s->dustTotals.size();
+}
+
 int skirt_sim_fetch(SkirtSim* s) {
     if (!s || !s->eng) { g_err = "no engine attached"; return SKIRT_ERR_STATE; }
     int rc = check(s, skirt_mcrt_download(s->eng, s->labs.empty() ? nullptr : s->labs.data(),
@@ -222,7 +285,8 @@ int skirt_sim_set_tallies(SkirtSim* s, const double* labs, const double* instr) 
 int skirt_sim_write(SkirtSim* s, const char* prefix) {
     if (!s || !prefix) return SKIRT_ERR_ARG;
     try {
-        writeOutputs(s->m, prefix, s->frames, s->seds, s->labs);
+        writeOutputs(s->m, prefix, s->frames, s->seds,
+                     totalLabs(s->m, s->labs, s->labsDust.empty() ? nullptr : &s->labsDust));
     } catch (std::exception& e) {
         g_err = e.what();
         return SKIRT_ERR_ARG;
