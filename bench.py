@@ -24,7 +24,10 @@ CONFIGS = {
     # name: (ski, packets per wavelength per rank, segment geometry bytes, description)
     "c3": ("benchmarks/c3_oct128.ski", 400000, 56, "C3 octree 128^3 (levels 3-7, mass fraction 1e-6), 25 lambda, peel-off"),
     "c2": ("benchmarks/c2_cart64.ski", 1000000, 0, "C2 Cartesian 64^3, 10 lambda, peel-off"),
+    "c5": ("benchmarks/c5_oct128_sa.ski", 400000, 56,
+           "C5 = C3 + dust self-absorption (3 cycles) + dust emission, all phases per step"),
 }
+DUST_CONFIGS = ("c5",)
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip-level parameters (spec)
 ATOMIC_PEAK_ADDS = 2.36e10  # scattered 8-byte atomic adds per second, measured (profiles/r01_atomic_bench.txt)
 
@@ -109,12 +112,25 @@ def main():
     labs = torch.zeros(max(1, n_labs), dtype=torch.float64, device="cuda")
     instr = torch.zeros(max(1, n_instr), dtype=torch.float64, device="cuda")
     sim.bind_tallies(labs.data_ptr(), instr.data_ptr())
+    dust_phases = args.config in DUST_CONFIGS
+    if dust_phases:
+        dust = torch.zeros(max(1, n_labs), dtype=torch.float64, device="cuda")
+        sim.bind_dust_labs(dust.data_ptr())
     sim.zero_tallies()
 
     def step():
+        if not dust_phases:
+            sim.run_stellar(first, share)
+            # phase end: PanDustSystem::sumResults (Labs) and Instrument::sumResults, over RCCL/xGMI
+            allreduce_tallies(labs, instr)
+            return
+        # the whole simulation (PanMonteCarloSimulation::runSelf): stellar emission, the Labs summed over
+        # ranks, the self-absorption cycles (dust Labs summed after each), dust emission, instruments
+        sim.zero_tallies()
         sim.run_stellar(first, share)
-        # phase end: PanDustSystem::sumResults (Labs) and Instrument::sumResults, over RCCL/xGMI
-        allreduce_tallies(labs, instr)
+        allreduce_tallies(labs)
+        sim.run_dust(rank, world, lambda: allreduce_tallies(dust))
+        allreduce_tallies(instr)
 
     for _ in range(args.warmup):
         step()
@@ -123,15 +139,15 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     s0 = sim.stats()
-    kernel_ms, trace_ms, trace_launches = [], 0.0, 0
+    kernel_ms = []
+    per_step = []  # dust configs zero the tallies (and counters) every step: collect each step's counters
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
         sim.synchronize()
         st = sim.stats()
         kernel_ms.append(st["kernel_ms"])
-        trace_ms += st["trace_ms"]
-        trace_launches += st["trace_launches"]
+        per_step.append(st)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -142,8 +158,18 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    delta = {k: s1[k] - s0[k] for k in s1 if k not in ("kernel_ms", "iterations", "trace_ms", "trace_launches")}
+    delta = {k: s1[k] - s0[k] for k in s1 if k not in ("kernel_ms", "iterations")}
+    if dust_phases:
+        for k in ("packets", "segments_fill", "segments_walk", "segments_peel", "detects", "absorb_adds", "lane_slots"):
+            delta[k] = sum(st[k] for st in per_step)
+    trace_ms, trace_launches = delta["trace_ms"], delta["trace_launches"]
     packets_all = share * world * args.steps
+    if dust_phases:
+        # every phase's launched packets (stellar, self-absorption cycles, dust emission), all ranks
+        n = torch.tensor([float(delta["packets"])], dtype=torch.float64, device="cuda")
+        if world > 1:
+            dist.all_reduce(n)
+        packets_all = float(n.item())
     value = packets_all / elapsed
     avg_kernel_s = sum(kernel_ms) / len(kernel_ms) / 1e3
     segs = delta["segments_fill"] + delta["segments_walk"] + delta["segments_peel"]

@@ -50,6 +50,15 @@ int skirt_sim_run_stellar(SkirtSim* sim, uint64_t first, uint64_t count);
  * whose detections add to the instrument tallies. Single process; fetches the stellar Labs first.
  * Returns after launching the dust emission phase (asynchronous, like run_stellar). */
 int skirt_sim_run_dust(SkirtSim* sim);
+/* The same, one rank of `world` processes (one per GPU): every phase shoots this rank's contiguous slice
+ * of its packets, and after each self-absorption cycle `reduce(user, SKIRT_REDUCE_DUST_LABS)` must sum
+ * the engine's dust Labs device buffer over all ranks in place (e.g. an RCCL all-reduce of the tensor
+ * bound with skirt_mcrt_bind_dust_labs, on the engine's stream), as PanDustSystem::Labsdusttot and
+ * the next cycle's spectra need the whole simulation's absorption. The stellar Labs on the device must
+ * already be summed over ranks. Returns nonzero if `reduce` does. */
+enum { SKIRT_REDUCE_DUST_LABS = 0 };
+typedef int (*SkirtReduceFn)(void* user, int what);
+int skirt_sim_run_dust_sharded(SkirtSim* sim, int rank, int world, SkirtReduceFn reduce, void* user);
 /* dust Labs of the last self-absorption cycle (row-major cell x wavelength), or NULL */
 const double* skirt_sim_labs_dust(SkirtSim* sim);
 /* Labsdusttot after every self-absorption cycle; returns the number of cycles */

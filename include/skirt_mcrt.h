@@ -115,6 +115,23 @@ typedef struct {
     double emission_bias;
 } SkirtCellSourceDesc;
 
+/* Grey-body dust emissivity for the device-side dust emission sources (GreyBodyDustEmissivity with
+ * AllCellsDustLib): cell volumes (reference order), per component kappa_abs and the population's
+ * sigma_abs per wavelength, mu, the DustMix temperature grid and Planck-integrated absorption table
+ * (DustMix.cpp:238-263), the wavelength grid. */
+typedef struct {
+    int ncells, nlambda, ncomp, ntemp;
+    const double* volume;       /* ncells */
+    const double* kabs;         /* ncomp x nlambda */
+    const double* sigmaabs;     /* ncomp x nlambda */
+    const double* mu;           /* ncomp */
+    const double* tv;           /* ntemp */
+    const double* planckabs;    /* ncomp x ntemp */
+    const double* lambda;       /* nlambda */
+    const double* dlambda;      /* nlambda */
+    double emission_bias;       /* PanDustSystem::emissionBias */
+} SkirtEmissivityDesc;
+
 /* MonteCarloSimulation properties used by the photon loop (MonteCarloSimulation.cpp:31-35). */
 typedef struct {
     double min_weight_reduction;
@@ -134,8 +151,8 @@ typedef struct {
     uint64_t lane_slots;        /* trace kernel: 64 x wave steps (segments / lane_slots = SIMD lane use) */
     uint64_t iterations;        /* event/trace iterations of the last run call */
     double kernel_ms;           /* device time of the last run call (HIP events on the engine stream) */
-    double trace_ms;            /* of which trace-kernel launches (HIP events around each launch) */
-    uint64_t trace_launches;    /* trace-kernel launches of the last run call */
+    double trace_ms;            /* trace-kernel time (HIP events around each launch), cumulative */
+    uint64_t trace_launches;    /* trace-kernel launches timed so far, cumulative */
 } SkirtStats;
 
 int skirt_mcrt_abi_version(void);
@@ -167,6 +184,13 @@ int skirt_mcrt_run_stellar(SkirtMcrt* ctx, uint64_t npp, uint64_t first, uint64_
 int skirt_mcrt_run_phase(SkirtMcrt* ctx, int phase, uint32_t cycle, uint64_t npp, uint64_t first, uint64_t count,
                          uint64_t seed, const SkirtPhaseParams* params);
 int skirt_mcrt_upload_cell_sources(SkirtMcrt* ctx, const SkirtCellSourceDesc* src);
+/* The same cell sources computed on the device from the current Labs tally (plus the dust Labs when
+ * include_dust): grey-body spectra at the cells' equilibrium temperatures, cell luminosities and their
+ * per-wavelength cumulative distribution (at most 64 wavelengths). Asynchronous on the engine stream. */
+int skirt_mcrt_upload_emissivity(SkirtMcrt* ctx, const SkirtEmissivityDesc* emis);
+int skirt_mcrt_compute_cell_sources(SkirtMcrt* ctx, int include_dust);
+/* PanDustSystem::Labsdusttot of the device dust Labs (waits for the engine stream) */
+int skirt_mcrt_dust_labs_total(SkirtMcrt* ctx, double* total);
 /* the dust Labs tally (PanDustSystem::_Labsdustvv; device layout as Labs): bind caller memory (e.g. a torch
  * tensor to all-reduce), zero it (rebootLabsdust) and copy it to host row-major (cell, wavelength) */
 int skirt_mcrt_bind_dust_labs(SkirtMcrt* ctx, double* d_labs_dust);

@@ -56,12 +56,15 @@ ABI_SYMBOLS = [
     "skirt_mcrt_synchronize", "skirt_mcrt_download", "skirt_mcrt_stats", "skirt_mcrt_configure",
     "skirt_mcrt_last_error", "skirt_mcrt_destroy", "skirt_mcrt_run_phase", "skirt_mcrt_upload_cell_sources",
     "skirt_mcrt_bind_dust_labs", "skirt_mcrt_zero_dust_labs", "skirt_mcrt_download_dust_labs",
+    "skirt_mcrt_upload_emissivity", "skirt_mcrt_compute_cell_sources", "skirt_mcrt_dust_labs_total",
     "skirt_sim_load", "skirt_sim_info", "skirt_sim_attach", "skirt_sim_engine", "skirt_sim_run_stellar",
     "skirt_sim_fetch", "skirt_sim_labs", "skirt_sim_instrument", "skirt_sim_set_tallies", "skirt_sim_write",
-    "skirt_sim_error", "skirt_sim_free", "skirt_sim_run_dust", "skirt_sim_labs_dust", "skirt_sim_selfabs_totals",
+    "skirt_sim_error", "skirt_sim_free", "skirt_sim_run_dust", "skirt_sim_run_dust_sharded", "skirt_sim_labs_dust", "skirt_sim_selfabs_totals",
 ]
 
 _lib = None
+# int (*)(void* user, int what): the reduction callback of skirt_sim_run_dust_sharded
+REDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int)
 
 
 def lib():
@@ -82,6 +85,8 @@ def lib():
         L.skirt_sim_run_stellar.argtypes = [vp, c_u64, c_u64]
         L.skirt_sim_fetch.argtypes = [vp]
         L.skirt_sim_run_dust.argtypes = [vp]
+        L.skirt_sim_run_dust_sharded.argtypes = [vp, c_int, c_int, REDUCE_FN, vp]
+        L.skirt_mcrt_bind_dust_labs.argtypes = [vp, vp]
         L.skirt_sim_labs_dust.restype = ctypes.POINTER(c_dbl)
         L.skirt_sim_labs_dust.argtypes = [vp]
         L.skirt_sim_selfabs_totals.argtypes = [vp, ctypes.POINTER(ctypes.POINTER(c_dbl))]
@@ -158,9 +163,27 @@ class Simulation:
     def run_stellar(self, first=0, count=0):
         self._check(lib().skirt_sim_run_stellar(self._h, first, count))
 
-    def run_dust(self):
-        """Self-absorption cycles (if enabled) and the dust emission phase (PanMonteCarloSimulation::runSelf)."""
-        self._check(lib().skirt_sim_run_dust(self._h))
+    def run_dust(self, rank=0, world=1, reduce_dust_labs=None):
+        """Self-absorption cycles (if enabled) and the dust emission phase (PanMonteCarloSimulation::runSelf).
+        With world > 1 this rank shoots its slice of every phase and reduce_dust_labs() must sum the
+        bound dust Labs tensor over the ranks (it is called after every self-absorption cycle)."""
+        if world == 1:
+            self._check(lib().skirt_sim_run_dust(self._h))
+            return
+
+        def cb(_user, _what):
+            try:
+                reduce_dust_labs()
+                return 0
+            except Exception:  # noqa: BLE001 -- reported to the C side as a failed reduction
+                return 1
+
+        fn = REDUCE_FN(cb)
+        self._check(lib().skirt_sim_run_dust_sharded(self._h, rank, world, fn, None))
+
+    def bind_dust_labs(self, ptr):
+        """Make the engine accumulate the dust Labs in caller device memory (ncells*nlambda doubles)."""
+        self._check_engine(lib().skirt_mcrt_bind_dust_labs(self.engine, ctypes.c_void_p(ptr)))
 
     def labs_dust(self):
         p = lib().skirt_sim_labs_dust(self._h)

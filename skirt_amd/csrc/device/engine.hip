@@ -812,6 +812,144 @@ __device__ __forceinline__ void detectPeel(const Args& a, const DevInstr& ins, u
     }
 }
 
+// ================================================================== dust emission sources on the device
+// The grey-body emission spectrum of every cell and the per-wavelength cell distribution of the dust
+// phases (DustLib::calculate with AllCellsDustLib + GreyBodyDustEmissivity, DustLib.cpp:60-185,
+// GreyBodyDustEmissivity.cpp:19-43, DustMix::equilibrium DustMix.cpp:689-712; cell luminosities and
+// NR::cdf of PanMonteCarloSimulation.cpp:193-205, 273-294), computed from the device tallies so the
+// self-absorption cycles never leave the GPU. Reference cell order, like the host restatement
+// (host/dustemission.cpp), which the tests compare against.
+constexpr int kMaxEmisLambda = 64;
+
+struct EmisArgs {
+    int ncells, nlambda, ncomp, ntemp;
+    const int* devCell;          // reference cell -> device cell (null: identity)
+    const double* labs;          // [nlambda][device cell]
+    const double* labsDust;      // same, or null
+    const double* rho;           // [device cell][ncomp]
+    const double* volume;        // [reference cell]
+    const double* kabs;          // [ncomp][nlambda]
+    const double* sigmaabs;      // [ncomp][nlambda]
+    const double* mu;            // [ncomp]
+    const double* Tv;            // [ntemp]
+    const double* planckabs;     // [ncomp][ntemp]
+    const double* lambda;        // [nlambda]
+    const double* dlambda;       // [nlambda]
+    double* lv;                  // out [nlambda][ncells]
+    double* cdf;                 // out [nlambda][ncells + 1]
+    double* ltot;                // out [nlambda]
+    double* blockSums;           // scratch [nlambda][nblocks]
+    int nblocks;
+};
+
+__device__ __forceinline__ double planckB(double T, double lambda) {  // PlanckFunction
+    const double h = 6.62606957e-34, c = 2.99792458e8, k = 1.3806488e-23;
+    const double x = h * c / (lambda * k * T);
+    return 2.0 * h * c * c / pow(lambda, 5) / (exp(x) - 1.0);
+}
+
+__global__ void __launch_bounds__(kBlock) cellSpectraKernel(const EmisArgs e) {
+    const int m = blockIdx.x * blockDim.x + threadIdx.x;
+    if (m >= e.ncells) return;
+    const int N = e.ncells, Nl = e.nlambda;
+    const int dm = e.devCell ? e.devCell[m] : m;
+    // PanDustSystem::Labs(m): stellar sum, continued by the dust sum
+    double Labsbol = 0;
+    for (int ell = 0; ell < Nl; ell++) Labsbol += e.labs[(size_t)ell * N + dm];
+    if (e.labsDust)
+        for (int ell = 0; ell < Nl; ell++) Labsbol += e.labsDust[(size_t)ell * N + dm];
+    double Jv[kMaxEmisLambda], Lv[kMaxEmisLambda];
+    const double fac = 4.0 * M_PI * e.volume[m];
+    for (int ell = 0; ell < Nl; ell++) {  // DustSystem::meanintensityv
+        double L = 0;
+        L += e.labs[(size_t)ell * N + dm];
+        if (e.labsDust) L += e.labsDust[(size_t)ell * N + dm];
+        double kr = 0.0;
+        for (int h = 0; h < e.ncomp; h++) kr += e.kabs[h * Nl + ell] * e.rho[(size_t)dm * e.ncomp + h];
+        const double J = L / (kr * fac) / e.dlambda[ell];
+        Jv[ell] = isfinite(J) ? J : 0.0;
+        Lv[ell] = 0.0;
+    }
+    for (int h = 0; h < e.ncomp; h++) {
+        // DustMix::equilibrium -> invplanckabs (NR::locate_clip + linear interpolation)
+        const double* sa = e.sigmaabs + h * Nl;
+        double pa = 0.0;
+        for (int ell = 0; ell < Nl; ell++) pa += sa[ell] * Jv[ell] * e.dlambda[ell];
+        const double* tab = e.planckabs + (size_t)h * e.ntemp;
+        int p;
+        if (pa < tab[0]) p = 0;
+        else {
+            int jl = -1, ju = e.ntemp - 1;
+            while (ju - jl > 1) { const int jm = (ju + jl) >> 1; if (pa < tab[jm]) ju = jm; else jl = jm; }
+            p = jl;
+        }
+        const double T = e.Tv[p] + ((pa - tab[p]) / (tab[p + 1] - tab[p])) * (e.Tv[p + 1] - e.Tv[p]);
+        const double w = e.ncomp > 1 ? e.rho[(size_t)dm * e.ncomp + h] : 1.0;
+        for (int ell = 0; ell < Nl; ell++) {
+            double ev = 0.0;
+            ev += sa[ell] * planckB(T, e.lambda[ell]);
+            ev /= e.mu[h];
+            if (e.ncomp > 1) Lv[ell] += ev * w;
+            else Lv[ell] = ev;
+        }
+    }
+    double total = 0.0;
+    for (int ell = 0; ell < Nl; ell++) {
+        Lv[ell] *= e.dlambda[ell];
+        total += Lv[ell];
+    }
+    for (int ell = 0; ell < Nl; ell++) {
+        const double lum = total > 0 ? Lv[ell] / total : Lv[ell];
+        e.lv[(size_t)ell * N + m] = Labsbol > 0.0 ? Labsbol * lum : 0.0;
+    }
+}
+
+// per wavelength: sums of kBlock consecutive cells
+__global__ void __launch_bounds__(kBlock) cellBlockSumKernel(const EmisArgs e) {
+    __shared__ double red[kBlock];
+    const int ell = blockIdx.y, b = blockIdx.x, m = b * kBlock + threadIdx.x;
+    red[threadIdx.x] = m < e.ncells ? e.lv[(size_t)ell * e.ncells + m] : 0.0;
+    __syncthreads();
+    for (int w = kBlock / 2; w > 0; w >>= 1) {
+        if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) e.blockSums[(size_t)ell * e.nblocks + b] = red[0];
+}
+
+// per wavelength (one block each): exclusive scan of the block sums and the total
+__global__ void __launch_bounds__(kBlock) cellScanBlocksKernel(const EmisArgs e) {
+    const int ell = blockIdx.x;
+    if (threadIdx.x != 0) return;
+    double run = 0;
+    double* bs = e.blockSums + (size_t)ell * e.nblocks;
+    for (int b = 0; b < e.nblocks; b++) {
+        const double v = bs[b];
+        bs[b] = run;
+        run += v;
+    }
+    e.ltot[ell] = run;
+}
+
+// the normalized cumulative distribution: X[0] = 0, X[m+1] = (sum of Lv[0..m]) / Ltot
+__global__ void __launch_bounds__(kBlock) cellCdfKernel(const EmisArgs e) {
+    __shared__ double sc[kBlock];
+    const int ell = blockIdx.y, b = blockIdx.x, m = b * kBlock + threadIdx.x;
+    const int N = e.ncells;
+    sc[threadIdx.x] = m < N ? e.lv[(size_t)ell * N + m] : 0.0;
+    __syncthreads();
+    for (int off = 1; off < kBlock; off <<= 1) {  // inclusive Hillis-Steele scan
+        const double v = threadIdx.x >= off ? sc[threadIdx.x - off] : 0.0;
+        __syncthreads();
+        sc[threadIdx.x] += v;
+        __syncthreads();
+    }
+    const double total = e.ltot[ell];
+    double* X = e.cdf + (size_t)ell * (N + 1);
+    if (m < N) X[m + 1] = total > 0 ? (e.blockSums[(size_t)ell * e.nblocks + b] + sc[threadIdx.x]) / total : 0.0;
+    if (m == 0) X[0] = 0.0;
+}
+
 // fills the leaf map: one thread per finest-level cell descends the (checked) tree by its index bits
 __global__ void __launch_bounds__(kBlock) buildLeafMapKernel(LeafEntry* map, const int* firstChild, const int* cellnumber,
                                                              const double* rho, int ncomp, int L) {
@@ -1464,6 +1602,11 @@ struct SkirtMcrt {
     int* dCellNode = nullptr;
     double* dLabsDust = nullptr;
     bool ownLabsDust = true;
+    // grey-body emissivity tables for the device-side dust emission sources
+    int emisNtemp = 0;
+    double *dEmisVolume = nullptr, *dEmisKabs = nullptr, *dEmisSigma = nullptr, *dEmisMu = nullptr, *dEmisTv = nullptr,
+           *dEmisPlanck = nullptr, *dEmisLambda = nullptr, *dEmisDlambda = nullptr, *dEmisScratch = nullptr;
+    int* dDevCell = nullptr;
     // instruments
     std::vector<DevInstr> instr;
     DevInstr* dInstr = nullptr;
@@ -1484,9 +1627,10 @@ struct SkirtMcrt {
     // config
     int traceGrid = 0, threshold = 16, slotsWanted = 0;
     double lastMs = 0;
-    std::vector<hipEvent_t> traceEv;  // pairs around the trace launches of the last run call
+    std::vector<hipEvent_t> traceEv;  // pairs around the trace launches not yet timed
     int traceLaunches = 0;
-    double traceMs = 0;
+    double traceMs = 0;               // all timed trace launches since the context was created
+    uint64_t traceLaunchesTotal = 0;
     int numCUs = 0;
     int lastIterations = 0;
 };
@@ -1907,6 +2051,95 @@ int skirt_mcrt_upload_cell_sources(SkirtMcrt* c, const SkirtCellSourceDesc* src)
     return SKIRT_OK;
 }
 
+static int ensureDustLabs(SkirtMcrt* c);
+
+// scratch of the cell-source scans and the dust Labs sum: block sums of every wavelength (or of the
+// whole dust table) plus two result slots
+static int ensureEmisScratch(SkirtMcrt* c) {
+    if (c->dEmisScratch) return SKIRT_OK;
+    const size_t nb = (size_t)c->nlambda * (((size_t)c->ncells + kBlock - 1) / kBlock);
+    const size_t nbAll = ((size_t)c->ncells * c->nlambda + kBlock - 1) / kBlock;
+    HIPCHECK(c, hipMalloc(&c->dEmisScratch, (std::max(nb, nbAll) + 2) * sizeof(double)));
+    return SKIRT_OK;
+}
+
+int skirt_mcrt_upload_emissivity(SkirtMcrt* c, const SkirtEmissivityDesc* d) {
+    if (!c || !d) return SKIRT_ERR_ARG;
+    if (c->gridKind < 0 || !c->dRho) return fail(c, SKIRT_ERR_STATE, "upload the grid and media before the emissivity");
+    if (d->ncells != c->ncells || d->nlambda != c->nlambda || d->ncomp != c->ncomp || d->ntemp < 2)
+        return fail(c, SKIRT_ERR_ARG, "emissivity tables do not match the grid, wavelengths and media");
+    if (d->nlambda > kMaxEmisLambda) return fail(c, SKIRT_ERR_UNSUPPORTED, "device dust emission supports at most 64 wavelengths");
+    HIPCHECK(c, hipSetDevice(c->device));
+    const size_t nl = (size_t)d->nlambda, nh = (size_t)d->ncomp;
+    int rc;
+    if ((rc = upload(c, c->dEmisVolume, d->volume, (size_t)d->ncells))) return rc;
+    if ((rc = upload(c, c->dEmisKabs, d->kabs, nh * nl))) return rc;
+    if ((rc = upload(c, c->dEmisSigma, d->sigmaabs, nh * nl))) return rc;
+    if ((rc = upload(c, c->dEmisMu, d->mu, nh))) return rc;
+    if ((rc = upload(c, c->dEmisTv, d->tv, (size_t)d->ntemp))) return rc;
+    if ((rc = upload(c, c->dEmisPlanck, d->planckabs, nh * d->ntemp))) return rc;
+    if ((rc = upload(c, c->dEmisLambda, d->lambda, nl))) return rc;
+    if ((rc = upload(c, c->dEmisDlambda, d->dlambda, nl))) return rc;
+    if (!c->devCell.empty() && (rc = upload(c, c->dDevCell, c->devCell.data(), c->devCell.size()))) return rc;
+    c->emisNtemp = d->ntemp;
+    c->cellBias = d->emission_bias;
+    return SKIRT_OK;
+}
+
+int skirt_mcrt_compute_cell_sources(SkirtMcrt* c, int include_dust) {
+    if (!c) return SKIRT_ERR_ARG;
+    if (!c->emisNtemp) return fail(c, SKIRT_ERR_STATE, "no emissivity uploaded");
+    if (!c->dLabs) return fail(c, SKIRT_ERR_STATE, "no Labs tally");
+    HIPCHECK(c, hipSetDevice(c->device));
+    if (include_dust) {
+        int rc = ensureDustLabs(c);
+        if (rc) return rc;
+    }
+    const int N = c->ncells, Nl = c->nlambda;
+    const int nblocks = (N + kBlock - 1) / kBlock;
+    auto alloc = [&](double*& p, size_t n) -> int {
+        if (!p) HIPCHECK(c, hipMalloc(&p, n * sizeof(double)));
+        return SKIRT_OK;
+    };
+    int rc;
+    if ((rc = alloc(c->dCellLv, (size_t)Nl * N)) || (rc = alloc(c->dCellCdf, (size_t)Nl * (N + 1))) ||
+        (rc = alloc(c->dCellLtot, (size_t)Nl)) || (rc = ensureEmisScratch(c)))
+        return rc;
+    EmisArgs e{};
+    e.ncells = N; e.nlambda = Nl; e.ncomp = c->ncomp; e.ntemp = c->emisNtemp;
+    e.devCell = c->devCell.empty() ? nullptr : c->dDevCell;
+    e.labs = c->dLabs; e.labsDust = include_dust ? c->dLabsDust : nullptr;
+    e.rho = c->dRho; e.volume = c->dEmisVolume; e.kabs = c->dEmisKabs; e.sigmaabs = c->dEmisSigma; e.mu = c->dEmisMu;
+    e.Tv = c->dEmisTv; e.planckabs = c->dEmisPlanck; e.lambda = c->dEmisLambda; e.dlambda = c->dEmisDlambda;
+    e.lv = c->dCellLv; e.cdf = c->dCellCdf; e.ltot = c->dCellLtot; e.blockSums = c->dEmisScratch; e.nblocks = nblocks;
+    hipLaunchKernelGGL(cellSpectraKernel, dim3(nblocks), dim3(kBlock), 0, c->stream, e);
+    hipLaunchKernelGGL(cellBlockSumKernel, dim3(nblocks, Nl), dim3(kBlock), 0, c->stream, e);
+    hipLaunchKernelGGL(cellScanBlocksKernel, dim3(Nl), dim3(64), 0, c->stream, e);
+    hipLaunchKernelGGL(cellCdfKernel, dim3(nblocks, Nl), dim3(kBlock), 0, c->stream, e);
+    HIPCHECK(c, hipGetLastError());
+    return SKIRT_OK;
+}
+
+int skirt_mcrt_dust_labs_total(SkirtMcrt* c, double* total) {
+    if (!c || !total) return SKIRT_ERR_ARG;
+    HIPCHECK(c, hipSetDevice(c->device));
+    int rc = ensureDustLabs(c);
+    if (rc) return rc;
+    const size_t n = (size_t)c->ncells * c->nlambda;
+    if ((rc = ensureEmisScratch(c))) return rc;
+    // reuse the cell-sum kernels on the dust table viewed as one "wavelength" of n cells
+    EmisArgs e{};
+    e.ncells = (int)n; e.nlambda = 1; e.lv = c->dLabsDust; e.blockSums = c->dEmisScratch;
+    e.nblocks = (int)((n + kBlock - 1) / kBlock);
+    e.ltot = c->dEmisScratch + e.nblocks;  // one slot past the block sums
+    hipLaunchKernelGGL(cellBlockSumKernel, dim3(e.nblocks, 1), dim3(kBlock), 0, c->stream, e);
+    hipLaunchKernelGGL(cellScanBlocksKernel, dim3(1), dim3(64), 0, c->stream, e);
+    HIPCHECK(c, hipGetLastError());
+    HIPCHECK(c, hipMemcpyAsync(total, e.ltot, sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    HIPCHECK(c, hipStreamSynchronize(c->stream));
+    return SKIRT_OK;
+}
+
 static int ensureDustLabs(SkirtMcrt* c) {
     const size_t nl = (size_t)c->ncells * c->nlambda;
     if (!c->dLabsDust && nl) {
@@ -1969,8 +2202,14 @@ int skirt_mcrt_run_phase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, 
     if (phase == SKIRT_PHASE_DUST_SELFABS && (rc = ensureDustLabs(c))) return rc;
     c->lastMs = 0;
     c->lastIterations = 0;
-    c->traceLaunches = 0;
-    c->traceMs = 0;
+    if (c->traceLaunches) {  // time the previous call's launches before their events are reused
+        HIPCHECK(c, hipStreamSynchronize(c->stream));
+        float ms = 0;
+        for (int k = 0; k < c->traceLaunches; k++)
+            if (hipEventElapsedTime(&ms, c->traceEv[2 * k], c->traceEv[2 * k + 1]) == hipSuccess) c->traceMs += ms;
+        c->traceLaunchesTotal += (uint64_t)c->traceLaunches;
+        c->traceLaunches = 0;
+    }
     if (count == 0) return SKIRT_OK;
     if (!c->dOptics) {  // a dust-free simulation still stages (zero) optical tables
         std::vector<double> z(4 * (size_t)c->nlambda, 0.0);
@@ -2158,10 +2397,10 @@ int skirt_mcrt_synchronize(SkirtMcrt* c) {
     HIPCHECK(c, hipStreamSynchronize(c->stream));
     float ms = 0;
     if (hipEventElapsedTime(&ms, c->ev0, c->ev1) == hipSuccess) c->lastMs = ms;
-    double tms = 0;
     for (int k = 0; k < c->traceLaunches; k++)
-        if (hipEventElapsedTime(&ms, c->traceEv[2 * k], c->traceEv[2 * k + 1]) == hipSuccess) tms += ms;
-    c->traceMs = tms;
+        if (hipEventElapsedTime(&ms, c->traceEv[2 * k], c->traceEv[2 * k + 1]) == hipSuccess) c->traceMs += ms;
+    c->traceLaunchesTotal += (uint64_t)c->traceLaunches;
+    c->traceLaunches = 0;  // timed: the event pairs can be reused
     unsigned int e = 0;
     HIPCHECK(c, hipMemcpy(&e, c->dError, sizeof e, hipMemcpyDeviceToHost));
     if (e) return fail(c, SKIRT_ERR_NUMERIC, "the optical depth along the path is not a positive number");
@@ -2205,7 +2444,7 @@ int skirt_mcrt_stats(SkirtMcrt* c, SkirtStats* out) {
     out->iterations = (uint64_t)c->lastIterations;
     out->kernel_ms = c->lastMs;
     out->trace_ms = c->traceMs;
-    out->trace_launches = (uint64_t)c->traceLaunches;
+    out->trace_launches = c->traceLaunchesTotal;
     return SKIRT_OK;
 }
 
@@ -2216,7 +2455,9 @@ void skirt_mcrt_destroy(SkirtMcrt* c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     void* bufs[] = {c->dMesh, c->dBox, c->dFirstChild, c->dCellnumber, c->dNbrOffset, c->dNbrList, c->dTreeT,
-                    c->dLeafMap, c->dCellLv, c->dCellCdf, c->dCellLtot, c->dCellNode, c->dRho,
+                    c->dLeafMap, c->dCellLv, c->dCellCdf, c->dCellLtot, c->dCellNode, c->dEmisVolume, c->dEmisKabs,
+                    c->dEmisSigma, c->dEmisMu, c->dEmisTv, c->dEmisPlanck, c->dEmisLambda, c->dEmisDlambda,
+                    c->dEmisScratch, c->dDevCell, c->dRho,
                     c->dOptics, c->dGeomParam, c->dLum, c->dLumtot, c->dCdf, c->dInstr,
                     c->dClaim, c->dStats, c->dError, c->dCtr, c->dPool};
     for (void* b : bufs)

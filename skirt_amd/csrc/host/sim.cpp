@@ -1,5 +1,6 @@
 // Host driver: .ski -> Model -> device engine -> outputs (include/skirt_host.h).
 #include <chrono>
+#include <cstdlib>
 #include <cmath>
 #include <memory>
 #include <stdexcept>
@@ -187,19 +188,53 @@ int skirt_sim_run_stellar(SkirtSim* s, uint64_t first, uint64_t count) {
     return check(s, skirt_mcrt_run_stellar(s->eng, s->npp, first, count, s->m.seed, &p));
 }
 
-int skirt_sim_run_dust(SkirtSim* s) {
+int skirt_sim_run_dust(SkirtSim* s) { return skirt_sim_run_dust_sharded(s, 0, 1, nullptr, nullptr); }
+
+int skirt_sim_run_dust_sharded(SkirtSim* s, int rank, int world, SkirtReduceFn reduce, void* user) {
     if (!s || !s->eng) { g_err = "no engine attached"; return SKIRT_ERR_STATE; }
+    if (world < 1 || rank < 0 || rank >= world || (world > 1 && !reduce)) {
+        g_err = "bad shard (rank, world) or missing reduction";
+        return SKIRT_ERR_ARG;
+    }
+    // this rank's contiguous slice of a phase's npp * Nlambda packets (skirt_amd.sharding.shard_range)
+    auto shard = [&](uint64_t total, uint64_t& first, uint64_t& count) {
+        first = total * (uint64_t)rank / (uint64_t)world;
+        count = total * (uint64_t)(rank + 1) / (uint64_t)world - first;
+    };
     const Model& m = s->m;
     if (!(m.hasDust && m.pan && m.dustEmission)) return SKIRT_OK;  // no dust emission: nothing to do
     try {
-        int rc = skirt_sim_fetch(s);  // the stellar phase's Labs on the host
-        if (rc) return rc;
+        int rc;
         const int Nl = m.wl.n();
         const std::vector<PlanckTable> tables = planckTables(m);
+        SkirtPhaseParams p{m.minWeightReduction, m.minScattEvents, m.scattBias, 0, 1};
+        // The cell sources between phases: on the device from the device tallies (default), or on the
+        // host by the restatement the oracle shares (SKIRT_AMD_HOST_SOURCES=1, or more than 64 wavelengths)
+        const char* env = getenv("SKIRT_AMD_HOST_SOURCES");
+        const bool hostSources = (env && env[0] == '1') || Nl > 64;
         std::vector<double> lum;
         CellSources src;
-        SkirtPhaseParams p{m.minWeightReduction, m.minScattEvents, m.scattBias, 0, 1};
-        auto upload = [&]() {
+        if (hostSources) {
+            if ((rc = skirt_sim_fetch(s))) return rc;  // the stellar phase's Labs on the host
+        } else {
+            std::vector<double> sigma, kabs, mu, planck;
+            for (int h = 0; h < m.ncomp(); h++) {
+                const DustMix& mx = m.dust[h].mix;
+                sigma.insert(sigma.end(), mx.sigmaabs.begin(), mx.sigmaabs.end());
+                kabs.insert(kabs.end(), mx.kabs.begin(), mx.kabs.end());
+                mu.push_back(mx.mu);
+                planck.insert(planck.end(), tables[h].planckabs.begin(), tables[h].planckabs.end());
+            }
+            SkirtEmissivityDesc ed{m.ncells(), Nl, m.ncomp(), (int)tables[0].Tv.size(), m.volume.data(), kabs.data(),
+                                   sigma.data(), mu.data(), tables[0].Tv.data(), planck.data(), m.wl.lambda.data(),
+                                   m.wl.dlambda.data(), m.dustEmissionBias};
+            if ((rc = check(s, skirt_mcrt_upload_emissivity(s->eng, &ed)))) return rc;
+        }
+        auto prepare = [&](bool withDust) -> int {
+            if (!hostSources) return check(s, skirt_mcrt_compute_cell_sources(s->eng, withDust ? 1 : 0));
+            const std::vector<double>* dust = withDust ? &s->labsDust : nullptr;
+            dustEmissionSpectra(m, tables, totalLabs(m, s->labs, dust), lum);
+            cellSources(m, s->labs, dust, lum, src);
             SkirtCellSourceDesc d{src.ncells, src.nlambda, src.lv.data(), src.cdf.data(), src.ltot.data(),
                                   m.dustEmissionBias};
             return check(s, skirt_mcrt_upload_cell_sources(s->eng, &d));
@@ -207,32 +242,42 @@ int skirt_sim_run_dust(SkirtSim* s) {
         s->dustTotals.clear();
         if (m.selfAbsorption) {
             // PanMonteCarloSimulation::rundustselfabsorption (PanMonteCarloSimulation.cpp:109-181)
-            s->labsDust.assign(s->labs.size(), 0.0);
+            s->labsDust.assign((size_t)m.ncells() * Nl, 0.0);
             SelfAbsorptionSchedule sched;
             sched.fixedCycles = m.cycles;
             uint32_t cycle = 0;
             while (sched.next()) {
-                dustEmissionSpectra(m, tables, totalLabs(m, s->labs, &s->labsDust), lum);
-                cellSources(m, s->labs, &s->labsDust, lum, src);
-                if ((rc = upload())) return rc;
+                if ((rc = prepare(true))) return rc;  // calculatedustemission, Labsbolv = Labs(m)
                 if ((rc = check(s, skirt_mcrt_zero_dust_labs(s->eng)))) return rc;  // rebootLabsdust
                 uint64_t npp = (uint64_t)std::ceil(m.packages * SelfAbsorptionSchedule::factor(sched.stage));
-                if ((rc = check(s, skirt_mcrt_run_phase(s->eng, SKIRT_PHASE_DUST_SELFABS, cycle++, npp, 0,
-                                                        npp * (uint64_t)Nl, m.seed, &p))))
+                uint64_t first, count;
+                shard(npp * (uint64_t)Nl, first, count);
+                if ((rc = check(s, skirt_mcrt_run_phase(s->eng, SKIRT_PHASE_DUST_SELFABS, cycle++, npp, first,
+                                                        count, m.seed, &p))))
                     return rc;
-                if ((rc = check(s, skirt_mcrt_download_dust_labs(s->eng, s->labsDust.data())))) return rc;
-                s->dustTotals.push_back(tableTotal(s->labsDust));
-                sched.finishCycle(s->dustTotals.back());
+                // PanDustSystem::Labsdusttot sums over processes: the caller all-reduces the dust Labs
+                if (world > 1 && (rc = reduce(user, SKIRT_REDUCE_DUST_LABS))) {
+                    g_err = "the dust Labs reduction failed";
+                    return rc;
+                }
+                double total = 0;
+                if (hostSources) {
+                    if ((rc = check(s, skirt_mcrt_download_dust_labs(s->eng, s->labsDust.data())))) return rc;
+                    total = tableTotal(s->labsDust);
+                } else if ((rc = check(s, skirt_mcrt_dust_labs_total(s->eng, &total)))) {
+                    return rc;
+                }
+                s->dustTotals.push_back(total);
+                sched.finishCycle(total);
             }
+            if (!hostSources && (rc = check(s, skirt_mcrt_download_dust_labs(s->eng, s->labsDust.data())))) return rc;
         }
         // PanMonteCarloSimulation::rundustemission (PanMonteCarloSimulation.cpp:245-264)
-        const std::vector<double>* dust = m.selfAbsorption ? &s->labsDust : nullptr;
-        dustEmissionSpectra(m, tables, totalLabs(m, s->labs, dust), lum);
-        cellSources(m, s->labs, dust, lum, src);
-        if ((rc = upload())) return rc;
+        if ((rc = prepare(m.selfAbsorption))) return rc;
         uint64_t npp = (uint64_t)std::ceil(m.packages * m.emissionBoost);
-        return check(s, skirt_mcrt_run_phase(s->eng, SKIRT_PHASE_DUST_EMISSION, 0, npp, 0, npp * (uint64_t)Nl,
-                                             m.seed, &p));
+        uint64_t first, count;
+        shard(npp * (uint64_t)Nl, first, count);
+        return check(s, skirt_mcrt_run_phase(s->eng, SKIRT_PHASE_DUST_EMISSION, 0, npp, first, count, m.seed, &p));
     } catch (std::exception& e) {
         g_err = e.what();
         return SKIRT_ERR_ARG;

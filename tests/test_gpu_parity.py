@@ -120,6 +120,22 @@ def test_dust_phases_match_oracle_same_streams(name, packages):
     assert close_fraction(frames, orc.frames[0], 1e-8) > 0.99
 
 
+@pytest.mark.parametrize("name", ["pan_oct", "pan_cart16_sa"])
+def test_device_cell_sources_equal_host_cell_sources(name, monkeypatch):
+    """The grey-body spectra and cell distributions computed on the device between phases give the
+    same dust phases as the host restatement shared with the oracle (to rounding)."""
+    runs = []
+    for host in ("0", "1"):
+        monkeypatch.setenv("SKIRT_AMD_HOST_SOURCES", host)
+        runs.append(run_gpu(name, packages=1000, dust=True))
+    dev, host = runs
+    np.testing.assert_allclose(dev.selfabs_totals(), host.selfabs_totals(), rtol=1e-9)
+    fd, sd = dev.instrument(0)
+    fh, sh = host.instrument(0)
+    np.testing.assert_allclose(sd, sh, rtol=1e-9, atol=1e-300)
+    np.testing.assert_allclose(fd.sum(axis=2), fh.sum(axis=2), rtol=1e-9, atol=1e-300)
+
+
 def test_sharded_packet_ranges_sum_to_the_whole():
     """Two disjoint packet ranges (as two GPUs would run) add up to the full run exactly."""
     name = "pan_cart16"
