@@ -207,6 +207,95 @@ void cartesianPath(const CartesianGrid& g, Vec3 r, Vec3 k, Path& p) {
     }
 }
 
+
+// DustGridPath::moveInside (DustGridPath.cpp:57-150) for a box {xmin ymin zmin xmax ymax zmax}: the
+// segments outside the box (m = -1) and the entry point, or infinity when the path misses the box
+void moveInsideBox(const double* b, double eps, Vec3 k, Path& p, double& rx, double& ry, double& rz) {
+    double kx = k.x, ky = k.y, kz = k.z;
+    bool outside = false;
+    if (rx <= b[0]) {
+        if (kx <= 0.0) outside = true;
+        else { double ds = (b[0] - rx) / kx; p.add(-1, ds); rx = b[0] + eps; ry += ky * ds; rz += kz * ds; }
+    } else if (rx >= b[3]) {
+        if (kx >= 0.0) outside = true;
+        else { double ds = (b[3] - rx) / kx; p.add(-1, ds); rx = b[3] - eps; ry += ky * ds; rz += kz * ds; }
+    }
+    if (!outside) {
+        if (ry <= b[1]) {
+            if (ky <= 0.0) outside = true;
+            else { double ds = (b[1] - ry) / ky; p.add(-1, ds); rx += kx * ds; ry = b[1] + eps; rz += kz * ds; }
+        } else if (ry >= b[4]) {
+            if (ky >= 0.0) outside = true;
+            else { double ds = (b[4] - ry) / ky; p.add(-1, ds); rx += kx * ds; ry = b[4] - eps; rz += kz * ds; }
+        }
+    }
+    if (!outside) {
+        if (rz <= b[2]) {
+            if (kz <= 0.0) outside = true;
+            else { double ds = (b[2] - rz) / kz; p.add(-1, ds); rx += kx * ds; ry += ky * ds; rz = b[2] + eps; }
+        } else if (rz >= b[5]) {
+            if (kz >= 0.0) outside = true;
+            else { double ds = (b[5] - rz) / kz; p.add(-1, ds); rx += kx * ds; ry += ky * ds; rz = b[5] - eps; }
+        }
+    }
+    if (outside) { rx = ry = rz = INFINITY; }
+}
+
+// VoronoiMesh::path (VoronoiMesh.cpp:749-844): from the current cell, the nearest positive crossing of
+// the bisector planes with its neighbours (or of the domain walls)
+void voronoiPath(const VoronoiGrid& g, Vec3 r0, Vec3 k, Path& p) {
+    p.clear();
+    const double box[6] = {g.xmin, g.ymin, g.zmin, g.xmax, g.ymax, g.zmax};
+    double rx = r0.x, ry = r0.y, rz = r0.z;
+    moveInsideBox(box, g.eps, k, p, rx, ry, rz);
+    int mr = g.cellIndex(rx, ry, rz);
+    if (mr < 0) return p.clear();
+    const double* S = g.site.data();
+    long guard = 0;
+    while (mr >= 0) {
+        if (++guard > 10000000)
+            throw std::runtime_error("Voronoi path does not advance: cell " + std::to_string(mr) + " at (" +
+                                     std::to_string(rx) + "," + std::to_string(ry) + "," + std::to_string(rz) + ") k (" +
+                                     std::to_string(k.x) + "," + std::to_string(k.y) + "," + std::to_string(k.z) + ")");
+        const double prx = S[3 * mr], pry = S[3 * mr + 1], prz = S[3 * mr + 2];
+        double sq = DBL_MAX;
+        const int NO_INDEX = -99;
+        int mq = NO_INDEX;
+        for (int q = g.nbrOffset[mr]; q < g.nbrOffset[mr + 1]; q++) {
+            const int mi = g.nbrList[q];
+            double si = 0;
+            if (mi >= 0) {
+                const double pix = S[3 * mi], piy = S[3 * mi + 1], piz = S[3 * mi + 2];
+                const double nx = pix - prx, ny = piy - pry, nz = piz - prz;
+                const double ndotk = nx * k.x + ny * k.y + nz * k.z;
+                if (ndotk > 0) {
+                    const double px = 0.5 * (pix + prx), py = 0.5 * (piy + pry), pz = 0.5 * (piz + prz);
+                    si = (nx * (px - rx) + ny * (py - ry) + nz * (pz - rz)) / ndotk;
+                }
+            } else {
+                switch (mi) {
+                case -1: si = (g.xmin - rx) / k.x; break;
+                case -2: si = (g.xmax - rx) / k.x; break;
+                case -3: si = (g.ymin - ry) / k.y; break;
+                case -4: si = (g.ymax - ry) / k.y; break;
+                case -5: si = (g.zmin - rz) / k.z; break;
+                case -6: si = (g.zmax - rz) / k.z; break;
+                default: throw std::runtime_error("Invalid neighbor ID");
+                }
+            }
+            if (si > 0 && si < sq) { sq = si; mq = mi; }
+        }
+        if (mq == NO_INDEX) {
+            rx += k.x * g.eps; ry += k.y * g.eps; rz += k.z * g.eps;
+            mr = g.cellIndex(rx, ry, rz);
+        } else {
+            p.add(mr, sq);
+            rx += (sq + g.eps) * k.x; ry += (sq + g.eps) * k.y; rz += (sq + g.eps) * k.z;
+            mr = mq;
+        }
+    }
+}
+
 // TreeNode::whichnode(r) from the root (TreeNode.cpp:70-80), OctTreeNode::child(r)
 int rootWhichnode(const OctreeGrid& t, double x, double y, double z) {
     const double* b = &t.box[0];
@@ -336,6 +425,7 @@ public:
 
     void path(Vec3 r, Vec3 k, Path& p) const {
         if (M.grid.kind == GridKind::Cartesian) cartesianPath(M.grid.cart, r, k, p);
+        else if (M.grid.kind == GridKind::Voronoi) voronoiPath(M.grid.vor, r, k, p);
         else {
             if (M.grid.tree.search == 2) throw std::runtime_error("Bookkeeping tree search is not supported");
             octreePath(M.grid.tree, r, k, p);
@@ -624,12 +714,23 @@ public:
         } else {
             m = locateClip(X);
         }
-        double b[6];
-        M.grid.cellBox(m, b);
-        double x = rng.uniform();
-        double y = rng.uniform();
-        double z = rng.uniform();
-        Vec3 pos{b[0] + x * (b[3] - b[0]), b[1] + y * (b[4] - b[1]), b[2] + z * (b[5] - b[2])};
+        Vec3 pos;
+        if (M.grid.kind == GridKind::Voronoi) {
+            // VoronoiMesh::randomPosition (VoronoiMesh.cpp:591-604)
+            struct Src final : UniformSource {
+                Rng& r;
+                explicit Src(Rng& x) : r(x) {}
+                double uniform() override { return r.uniform(); }
+            } src(rng);
+            voronoiRandomPosition(M.grid.vor, src, m, pos.x, pos.y, pos.z);
+        } else {
+            double b[6];
+            M.grid.cellBox(m, b);
+            double x = rng.uniform();
+            double y = rng.uniform();
+            double z = rng.uniform();
+            pos = Vec3{b[0] + x * (b[3] - b[0]), b[1] + y * (b[4] - b[1]), b[2] + z * (b[5] - b[2])};
+        }
         Vec3 k = isotropic(rng);
         pp = Packet{Lw, ell, pos, k, 0, -1};
     }

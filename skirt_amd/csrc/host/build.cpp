@@ -120,6 +120,10 @@ double WavelengthGrid::lambdamax(int ell) const {
 }
 
 void DustGrid::cellBox(int m, double b[6]) const {
+    if (kind == GridKind::Voronoi) {
+        for (int q = 0; q < 6; q++) b[q] = vor.bbox[6 * (size_t)m + q];
+        return;
+    }
     if (kind == GridKind::Cartesian) {
         const CartesianGrid& g = cart;
         int i = m / (g.Nz * g.Ny), j = (m / g.Nz) % g.Ny, k = m % g.Nz;  // CartesianDustGrid::box
@@ -131,13 +135,25 @@ void DustGrid::cellBox(int m, double b[6]) const {
     }
 }
 
+void DustGrid::cellCenter(int m, double c[3]) const {
+    if (kind == GridKind::Voronoi) {
+        for (int q = 0; q < 3; q++) c[q] = vor.centroid[3 * (size_t)m + q];
+        return;
+    }
+    double b[6];
+    cellBox(m, b);
+    for (int q = 0; q < 3; q++) c[q] = 0.5 * (b[q] + b[3 + q]);
+}
+
 double DustGrid::cellVolume(int m) const {
+    if (kind == GridKind::Voronoi) return vor.volume[m];
     double b[6];
     cellBox(m, b);
     return (b[3] - b[0]) * (b[4] - b[1]) * (b[5] - b[2]);
 }
 
 int DustGrid::whichcell(double x, double y, double z) const {
+    if (kind == GridKind::Voronoi) return vor.cellIndex(x, y, z);
     if (kind == GridKind::Cartesian) {
         int i = nr::locateFail(cart.xv, x), j = nr::locateFail(cart.yv, y), k = nr::locateFail(cart.zv, z);
         if (i < 0 || j < 0 || k < 0) return -1;
@@ -728,6 +744,64 @@ Instrument parseInstrument(const Ctx& c, const XmlElement* e) {
 
 // ============================================================ loadSki
 
+// VoronoiDustGrid::setupSelfBefore (VoronoiDustGrid.cpp:28-138): the sites for the Uniform and
+// DustDensity distributions, then the tessellation
+static void buildVoronoiGrid(const Ctx& c, const XmlElement* ge, Model& m, UniformSource& rng) {
+    const double xmin = attr(c, ge, "minX", "length", 0), xmax = attr(c, ge, "maxX", "length", 0);
+    const double ymin = attr(c, ge, "minY", "length", 0), ymax = attr(c, ge, "maxY", "length", 0);
+    const double zmin = attr(c, ge, "minZ", "length", 0), zmax = attr(c, ge, "maxZ", "length", 0);
+    const int N = attrInt(ge, "numParticles", 0);
+    if (N < 10) throw std::runtime_error("The number of particles should be at least 10");
+    const std::string dist = ge->get("distribution", "DustDensity");
+    auto contains = [&](double x, double y, double z) {  // Box::contains
+        return x >= xmin && x <= xmax && y >= ymin && y <= ymax && z >= zmin && z <= zmax;
+    };
+    std::vector<double> sites(3 * (size_t)N);
+    if (dist == "Uniform") {
+        for (int q = 0; q < N; q++) {
+            double fx = rng.uniform(), fy = rng.uniform(), fz = rng.uniform();  // Random::position(extent)
+            sites[3 * q] = xmin + fx * (xmax - xmin);
+            sites[3 * q + 1] = ymin + fy * (ymax - ymin);
+            sites[3 * q + 2] = zmin + fz * (zmax - zmin);
+        }
+    } else if (dist == "DustDensity") {
+        // CompDustDistribution::generatePosition: a component by mass (NR::locate_clip on the normalized
+        // cumulative masses), then its geometry's generatePosition; points outside the domain are redrawn
+        std::vector<double> masses, cum;
+        for (const DustComp& d : m.dust) masses.push_back(d.nf);
+        nr::cdf(cum, masses);
+        for (int q = 0; q < N; q++) {
+            while (true) {
+                double X = rng.uniform();
+                int h;
+                if (X < cum[0]) h = 0;
+                else h = nr::locateBasic(cum, X, (int)cum.size() - 1);
+                const Geometry& geo = m.dust[h].geom;
+                // PlummerGeometry::randomradius, then SpheGeometry::generatePosition (Random::direction)
+                double t = std::pow(rng.uniform(), 1.0 / 3.0);
+                double r = geo.c * t / std::sqrt((1.0 - t) * (1.0 + t));
+                double theta = std::acos(2.0 * rng.uniform() - 1.0);
+                double phi = 2.0 * M_PI * rng.uniform();
+                double kx, ky, kz;
+                if (theta <= 1e-8) { kx = 0; ky = 0; kz = 1; }  // Direction(theta, phi), Direction.cpp
+                else if (theta >= M_PI - 1e-8) { kx = 0; ky = 0; kz = -1; }
+                else {
+                    double st = std::sin(theta);
+                    kx = st * std::cos(phi); ky = st * std::sin(phi); kz = std::cos(theta);
+                }
+                double x = r * kx, y = r * ky, z = r * kz;
+                if (contains(x, y, z)) {
+                    sites[3 * q] = x; sites[3 * q + 1] = y; sites[3 * q + 2] = z;
+                    break;
+                }
+            }
+        }
+    } else {
+        throw std::runtime_error("unsupported Voronoi particle distribution " + dist);
+    }
+    buildVoronoi(m.grid.vor, sites, xmin, xmax, ymin, ymax, zmin, zmax);
+}
+
 Model loadSki(const std::string& path, UniformSource& rng, const std::string& datadir) {
     auto doc = parseXmlFile(path);
     if (doc->children.empty()) throw std::runtime_error("empty ski file");
@@ -858,6 +932,10 @@ Model loadSki(const std::string& path, UniformSource& rng, const std::string& da
             m.grid.kind = GridKind::Octree;
             buildOctree(c, ge, m, m.grid.tree);
             m.grid.ncells = (int)m.grid.tree.idv.size();
+        } else if (ge->name == "VoronoiDustGrid") {
+            m.grid.kind = GridKind::Voronoi;
+            buildVoronoiGrid(c, ge, m, rng);
+            m.grid.ncells = m.grid.vor.ncells();
         } else {
             throw std::runtime_error("unsupported dust grid " + ge->name);
         }
@@ -873,8 +951,13 @@ Model loadSki(const std::string& path, UniformSource& rng, const std::string& da
             m.grid.cellBox(cell, b);
             std::fill(sumv.begin(), sumv.end(), 0.0);
             for (int n = 0; n < m.sampleCount; n++) {
-                double fx = rng.uniform(), fy = rng.uniform(), fz = rng.uniform();
-                double x = b[0] + fx * (b[3] - b[0]), y = b[1] + fy * (b[4] - b[1]), z = b[2] + fz * (b[5] - b[2]);
+                double x, y, z;
+                if (m.grid.kind == GridKind::Voronoi) {
+                    voronoiRandomPosition(m.grid.vor, rng, cell, x, y, z);  // VoronoiMesh::randomPosition
+                } else {
+                    double fx = rng.uniform(), fy = rng.uniform(), fz = rng.uniform();
+                    x = b[0] + fx * (b[3] - b[0]); y = b[1] + fy * (b[4] - b[1]); z = b[2] + fz * (b[5] - b[2]);
+                }
                 for (int h = 0; h < Ncomp; h++) sumv[h] += m.dust[h].density(x, y, z);
             }
             for (int h = 0; h < Ncomp; h++) m.rho[(size_t)cell * Ncomp + h] = 1.0 * sumv[h] / m.sampleCount;

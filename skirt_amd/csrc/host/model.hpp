@@ -12,6 +12,7 @@
 
 #include "mt_random.hpp"
 #include "units.hpp"
+#include "voronoi.hpp"
 
 namespace skirt {
 
@@ -80,15 +81,18 @@ struct OctreeGrid {
     int nnodes() const { return (int)firstChild.size(); }
 };
 
-enum class GridKind : int { Cartesian = 0, Octree = 1 };
+enum class GridKind : int { Cartesian = 0, Octree = 1, Voronoi = 2 };
 
 struct DustGrid {
     GridKind kind = GridKind::Cartesian;
     CartesianGrid cart;
     OctreeGrid tree;
+    VoronoiGrid vor;
     int ncells = 0;
-    void cellBox(int m, double b[6]) const;  // xmin ymin zmin xmax ymax zmax
+    void cellBox(int m, double b[6]) const;  // xmin ymin zmin xmax ymax zmax (Voronoi: the enclosing box)
     double cellVolume(int m) const;
+    // DustGrid::centralPositionInCell: the box centre, or the centroid of a Voronoi cell
+    void cellCenter(int m, double c[3]) const;
     int whichcell(double x, double y, double z) const;
 };
 

@@ -275,10 +275,9 @@ void writeOutputs(const Model& m, const std::string& prefix, const std::vector<s
             double Ltot = 0;
             for (int ell = 0; ell < Nl; ell++) Ltot += labs[(size_t)c * Nl + ell];
             if (!(Ltot > 0.0)) continue;
-            double b[6];
-            m.grid.cellBox(c, b);
-            std::vector<double> vals{(double)c, units.olength(0.5 * (b[0] + b[3])), units.olength(0.5 * (b[1] + b[4])),
-                                     units.olength(0.5 * (b[2] + b[5]))};
+            double ctr[3];
+            m.grid.cellCenter(c, ctr);
+            std::vector<double> vals{(double)c, units.olength(ctr[0]), units.olength(ctr[1]), units.olength(ctr[2])};
             double fac = 4.0 * M_PI * m.volume[c];
             for (int ell = 0; ell < Nl; ell++) {
                 double kappaabsrho = 0.0;

@@ -1,0 +1,289 @@
+// Voronoi tessellation restricted to a box, by convex-cell clipping; see voronoi.hpp.
+#include "voronoi.hpp"
+
+#include <algorithm>
+#include <array>
+#include <cfloat>
+#include <cmath>
+#include <stdexcept>
+
+#include "mt_random.hpp"
+
+namespace skirt {
+
+namespace {
+
+using V3 = std::array<double, 3>;
+
+inline double dot(const V3& a, const V3& b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+inline V3 sub(const V3& a, const V3& b) { return {a[0] - b[0], a[1] - b[1], a[2] - b[2]}; }
+inline V3 cross(const V3& a, const V3& b) {
+    return {a[1] * b[2] - a[2] * b[1], a[2] * b[0] - a[0] * b[2], a[0] * b[1] - a[1] * b[0]};
+}
+
+struct Face {
+    int id;                // neighbour cell or wall (-1 .. -6)
+    std::vector<V3> pts;   // convex polygon, in order around the face
+};
+
+// A convex cell: its faces. Clipping keeps the half space dot(n, x) <= c.
+struct Cell {
+    std::vector<Face> faces;
+
+    double maxDist2(const V3& s) const {
+        double r = 0;
+        for (const Face& f : faces)
+            for (const V3& p : f.pts) r = std::max(r, dot(sub(p, s), sub(p, s)));
+        return r;
+    }
+
+    // the point where edge (a, b) crosses the plane, computed from the lexicographically smaller end so
+    // that the two faces sharing the edge produce the same bits
+    static V3 crossing(const V3& a0, const V3& b0, const V3& n, double c) {
+        const bool swap = b0 < a0;
+        const V3& a = swap ? b0 : a0;
+        const V3& b = swap ? a0 : b0;
+        const double da = dot(n, a) - c, db = dot(n, b) - c;
+        const double t = da / (da - db);
+        return {a[0] + t * (b[0] - a[0]), a[1] + t * (b[1] - a[1]), a[2] + t * (b[2] - a[2])};
+    }
+
+    // clips by dot(n, x) <= c; the new face gets `id`. Returns whether the cell changed.
+    bool clip(const V3& n, double c, double tol, int id) {
+        double dmax = -DBL_MAX;
+        for (const Face& f : faces)
+            for (const V3& p : f.pts) dmax = std::max(dmax, dot(n, p) - c);
+        if (dmax <= tol) return false;  // entirely inside: the plane does not cut
+        std::vector<V3> cap;
+        std::vector<Face> out;
+        out.reserve(faces.size() + 1);
+        for (const Face& f : faces) {
+            const int m = (int)f.pts.size();
+            Face g{f.id, {}};
+            for (int k = 0; k < m; k++) {
+                const V3& a = f.pts[k];
+                const V3& b = f.pts[(k + 1) % m];
+                const double da = dot(n, a) - c, db = dot(n, b) - c;
+                const bool ina = da <= tol, inb = db <= tol;
+                if (ina) {
+                    g.pts.push_back(a);
+                    if (da >= -tol) cap.push_back(a);  // on the plane: also a vertex of the new face
+                }
+                if (ina != inb && std::fabs(da) > tol && std::fabs(db) > tol) {
+                    V3 q = crossing(a, b, n, c);
+                    g.pts.push_back(q);
+                    cap.push_back(q);
+                }
+            }
+            if (g.pts.size() >= 3) out.push_back(std::move(g));
+        }
+        // the new face: the distinct cut points ordered by angle around their centre
+        std::sort(cap.begin(), cap.end());
+        cap.erase(std::unique(cap.begin(), cap.end()), cap.end());
+        if (cap.size() >= 3) {
+            V3 ctr{0, 0, 0};
+            for (const V3& p : cap)
+                for (int q = 0; q < 3; q++) ctr[q] += p[q];
+            for (int q = 0; q < 3; q++) ctr[q] /= (double)cap.size();
+            // in-plane basis of equal lengths: u and n^ x u (n normalized, or the angles would be stretched)
+            const double nl = std::sqrt(dot(n, n));
+            const V3 nh{n[0] / nl, n[1] / nl, n[2] / nl};
+            V3 u = sub(cap[0], ctr);
+            V3 v = cross(nh, u);
+            std::vector<std::pair<double, V3>> ang;
+            for (const V3& p : cap) {
+                const V3 d = sub(p, ctr);
+                ang.push_back({std::atan2(dot(d, v), dot(d, u)), p});
+            }
+            std::sort(ang.begin(), ang.end(), [](const auto& x, const auto& y) { return x.first < y.first; });
+            Face nf{id, {}};
+            for (auto& a : ang) nf.pts.push_back(a.second);
+            out.push_back(std::move(nf));
+        }
+        faces = std::move(out);
+        return true;
+    }
+};
+
+}  // namespace
+
+void VoronoiGrid::blockIndices(double x, double y, double z, int& i, int& j, int& k) const {
+    i = std::max(0, std::min(nb - 1, static_cast<int>(nb * (x - xmin) / (xmax - xmin))));
+    j = std::max(0, std::min(nb - 1, static_cast<int>(nb * (y - ymin) / (ymax - ymin))));
+    k = std::max(0, std::min(nb - 1, static_cast<int>(nb * (z - zmin) / (zmax - zmin))));
+}
+
+int VoronoiGrid::cellIndex(double x, double y, double z) const {
+    if (!(x >= xmin && x <= xmax && y >= ymin && y <= ymax && z >= zmin && z <= zmax)) return -1;
+    int i, j, k;
+    blockIndices(x, y, z, i, j, k);
+    const int b = i * nb * nb + j * nb + k;
+    int m = -1;
+    double best = DBL_MAX;
+    for (int q = blockOffset[b]; q < blockOffset[b + 1]; q++) {
+        const int c = blockList[q];
+        const double dx = x - site[3 * c], dy = y - site[3 * c + 1], dz = z - site[3 * c + 2];
+        const double d = dx * dx + dy * dy + dz * dz;  // Vec::norm2 of (r - site)
+        if (d < best) { best = d; m = c; }
+    }
+    return m;
+}
+
+bool VoronoiGrid::isPointClosestTo(double x, double y, double z, int m) const {
+    auto d2 = [&](int c) {
+        const double dx = x - site[3 * c], dy = y - site[3 * c + 1], dz = z - site[3 * c + 2];
+        return dx * dx + dy * dy + dz * dz;
+    };
+    const double target = d2(m);
+    for (int q = nbrOffset[m]; q < nbrOffset[m + 1]; q++) {
+        const int id = nbrList[q];
+        if (id >= 0 && d2(id) < target) return false;
+    }
+    return true;
+}
+
+void buildVoronoi(VoronoiGrid& g, const std::vector<double>& sites, double xmin, double xmax, double ymin, double ymax,
+                  double zmin, double zmax) {
+    g.xmin = xmin; g.xmax = xmax; g.ymin = ymin; g.ymax = ymax; g.zmin = zmin; g.zmax = zmax;
+    const double wx = xmax - xmin, wy = ymax - ymin, wz = zmax - zmin;
+    const double L = std::sqrt(wx * wx + wy * wy + wz * wz);
+    g.eps = 1e-12 * L;
+    g.site = sites;
+    const int N = g.ncells();
+    if (N < 1) throw std::runtime_error("a Voronoi grid needs sites");
+
+    // bucket grid over the sites: the candidates of a cell come shell by shell around its bucket
+    const int ng = std::max(1, (int)std::cbrt(N / 2.0));
+    const double bw[3] = {wx / ng, wy / ng, wz / ng};
+    const double wmin = std::min(bw[0], std::min(bw[1], bw[2]));
+    auto bucketOf = [&](const double* p, int* b) {
+        const double lo[3] = {xmin, ymin, zmin};
+        for (int q = 0; q < 3; q++) b[q] = std::max(0, std::min(ng - 1, (int)((p[q] - lo[q]) / bw[q])));
+    };
+    std::vector<int> bOff((size_t)ng * ng * ng + 1, 0), bList(N);
+    for (int m = 0; m < N; m++) {
+        int b[3];
+        bucketOf(&sites[3 * m], b);
+        bOff[(b[0] * ng + b[1]) * ng + b[2] + 1]++;
+    }
+    for (size_t q = 1; q < bOff.size(); q++) bOff[q] += bOff[q - 1];
+    {
+        std::vector<int> fill(bOff.begin(), bOff.end() - 1);
+        for (int m = 0; m < N; m++) {
+            int b[3];
+            bucketOf(&sites[3 * m], b);
+            bList[fill[(b[0] * ng + b[1]) * ng + b[2]]++] = m;
+        }
+    }
+
+    g.nbrOffset.assign(N + 1, 0);
+    g.nbrList.clear();
+    g.bbox.assign(6 * (size_t)N, 0);
+    g.volume.assign(N, 0);
+    g.centroid.assign(3 * (size_t)N, 0);
+    std::vector<std::pair<double, int>> cand;
+    for (int i = 0; i < N; i++) {
+        const V3 s{sites[3 * i], sites[3 * i + 1], sites[3 * i + 2]};
+        // the domain box, faces labelled with the wall ids of the reference (Voro++ walls)
+        const V3 c000{xmin, ymin, zmin}, c100{xmax, ymin, zmin}, c010{xmin, ymax, zmin}, c110{xmax, ymax, zmin};
+        const V3 c001{xmin, ymin, zmax}, c101{xmax, ymin, zmax}, c011{xmin, ymax, zmax}, c111{xmax, ymax, zmax};
+        Cell cell;
+        cell.faces = {{-1, {c000, c001, c011, c010}}, {-2, {c100, c110, c111, c101}},
+                      {-3, {c000, c100, c101, c001}}, {-4, {c010, c011, c111, c110}},
+                      {-5, {c000, c010, c110, c100}}, {-6, {c001, c101, c111, c011}}};
+        double R2 = cell.maxDist2(s);
+        int b[3];
+        bucketOf(&sites[3 * i], b);
+        for (int r = 0; r < ng; r++) {
+            if (r > 0 && ((r - 1) * wmin) * ((r - 1) * wmin) >= 4 * R2) break;  // no site beyond can cut
+            cand.clear();
+            for (int bx = std::max(0, b[0] - r); bx <= std::min(ng - 1, b[0] + r); bx++)
+                for (int by = std::max(0, b[1] - r); by <= std::min(ng - 1, b[1] + r); by++)
+                    for (int bz = std::max(0, b[2] - r); bz <= std::min(ng - 1, b[2] + r); bz++) {
+                        if (std::max(std::abs(bx - b[0]), std::max(std::abs(by - b[1]), std::abs(bz - b[2]))) != r) continue;
+                        const int bb = (bx * ng + by) * ng + bz;
+                        for (int q = bOff[bb]; q < bOff[bb + 1]; q++) {
+                            const int j = bList[q];
+                            if (j == i) continue;
+                            const V3 pj{sites[3 * j], sites[3 * j + 1], sites[3 * j + 2]};
+                            const V3 d = sub(pj, s);
+                            cand.push_back({dot(d, d), j});
+                        }
+                    }
+            std::sort(cand.begin(), cand.end());
+            for (auto& cj : cand) {
+                if (cj.first >= 4 * R2) break;  // too far to cut (|pj - s| / 2 >= farthest vertex)
+                const int j = cj.second;
+                const V3 pj{sites[3 * j], sites[3 * j + 1], sites[3 * j + 2]};
+                const V3 n = sub(pj, s);
+                const V3 mid{0.5 * (pj[0] + s[0]), 0.5 * (pj[1] + s[1]), 0.5 * (pj[2] + s[2])};
+                const double tol = 1e-12 * std::sqrt(cj.first) * L;
+                if (cell.clip(n, dot(n, mid), tol, j)) R2 = cell.maxDist2(s);
+            }
+            if (r == ng - 1) break;
+        }
+        // neighbours, bounding box, volume and centroid of the finished cell
+        std::vector<int> ids;
+        double bmin[3] = {DBL_MAX, DBL_MAX, DBL_MAX}, bmax[3] = {-DBL_MAX, -DBL_MAX, -DBL_MAX};
+        double vol = 0, cx = 0, cy = 0, cz = 0;
+        for (const Face& f : cell.faces) {
+            ids.push_back(f.id);
+            for (const V3& p : f.pts)
+                for (int q = 0; q < 3; q++) { bmin[q] = std::min(bmin[q], p[q]); bmax[q] = std::max(bmax[q], p[q]); }
+            for (size_t k = 1; k + 1 < f.pts.size(); k++) {
+                const V3 a = sub(f.pts[0], s), bq = sub(f.pts[k], s), cq = sub(f.pts[k + 1], s);
+                const double v = std::fabs(dot(a, cross(bq, cq))) / 6.0;
+                vol += v;
+                cx += v * (s[0] + (f.pts[0][0] + f.pts[k][0] + f.pts[k + 1][0] - 3 * s[0]) / 4.0);
+                cy += v * (s[1] + (f.pts[0][1] + f.pts[k][1] + f.pts[k + 1][1] - 3 * s[1]) / 4.0);
+                cz += v * (s[2] + (f.pts[0][2] + f.pts[k][2] + f.pts[k + 1][2] - 3 * s[2]) / 4.0);
+            }
+        }
+        std::sort(ids.begin(), ids.end());
+        ids.erase(std::unique(ids.begin(), ids.end()), ids.end());
+        g.nbrList.insert(g.nbrList.end(), ids.begin(), ids.end());
+        g.nbrOffset[i + 1] = (int)g.nbrList.size();
+        for (int q = 0; q < 3; q++) { g.bbox[6 * (size_t)i + q] = bmin[q]; g.bbox[6 * (size_t)i + 3 + q] = bmax[q]; }
+        g.volume[i] = vol;
+        g.centroid[3 * (size_t)i] = vol > 0 ? cx / vol : s[0];
+        g.centroid[3 * (size_t)i + 1] = vol > 0 ? cy / vol : s[1];
+        g.centroid[3 * (size_t)i + 2] = vol > 0 ? cz / vol : s[2];
+    }
+
+    // block lists (VoronoiMesh::buildMesh): nb = max(3, min(1000, int(3 N^(1/3)))) blocks per axis
+    g.nb = std::max(3, std::min(1000, static_cast<int>(3. * std::pow(N, 1. / 3.))));
+    const int nb = g.nb, nb3 = nb * nb * nb;
+    std::vector<std::vector<int>> lists(nb3);
+    for (int m = 0; m < N; m++) {
+        int i1, j1, k1, i2, j2, k2;
+        const double* bx = &g.bbox[6 * (size_t)m];
+        g.blockIndices(bx[0] - g.eps, bx[1] - g.eps, bx[2] - g.eps, i1, j1, k1);
+        g.blockIndices(bx[3] + g.eps, bx[4] + g.eps, bx[5] + g.eps, i2, j2, k2);
+        for (int i = i1; i <= i2; i++)
+            for (int j = j1; j <= j2; j++)
+                for (int k = k1; k <= k2; k++) lists[(size_t)i * nb * nb + j * nb + k].push_back(m);
+    }
+    g.blockOffset.assign(nb3 + 1, 0);
+    g.blockList.clear();
+    for (int b = 0; b < nb3; b++) {
+        g.blockList.insert(g.blockList.end(), lists[b].begin(), lists[b].end());
+        g.blockOffset[b + 1] = (int)g.blockList.size();
+    }
+}
+
+void voronoiRandomPosition(const VoronoiGrid& g, UniformSource& rng, int m, double& x, double& y, double& z) {
+    const double* b = &g.bbox[6 * (size_t)m];
+    for (int i = 0; i < 10000; i++) {
+        // Random::position(box) then Box::fracpos
+        double fx = rng.uniform();
+        double fy = rng.uniform();
+        double fz = rng.uniform();
+        x = b[0] + fx * (b[3] - b[0]);
+        y = b[1] + fy * (b[4] - b[1]);
+        z = b[2] + fz * (b[5] - b[2]);
+        if (g.isPointClosestTo(x, y, z, m)) return;
+    }
+    throw std::runtime_error("Can't find random position in cell");
+}
+
+}  // namespace skirt

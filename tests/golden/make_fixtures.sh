@@ -22,7 +22,7 @@ run() {  # run <ski> <seed> <tag>
       *) cp "$f" "$OUT/" ;;
     esac
   done
-  grep -h "Finished the stellar emission phase\|Total number of\|Total extinction\|absorbed dust luminosity\|absorbed stellar luminosity\|Convergence" "$WORK/$tag"_log.txt > "$OUT/${tag}_log_excerpt.txt" || true
+  grep -h "Finished the stellar emission phase\|Total number of\|Total extinction\|absorbed dust luminosity\|absorbed stellar luminosity\|Convergence\|neighbors per cell\|Computed Voronoi" "$WORK/$tag"_log.txt > "$OUT/${tag}_log_excerpt.txt" || true
 }
 all() {
   run c1_oligo16 4357 c1_oligo16_s4357
@@ -33,6 +33,8 @@ all() {
   run pan_oct 99 pan_oct_s99
   run pan_cart16_sa 4357 pan_cart16_sa_s4357
   run pan_cart16_sac 4357 pan_cart16_sac_s4357
+  run vor_oligo 4357 vor_oligo_s4357
+  run vor_pan 4357 vor_pan_s4357
 }
 # usage: make_fixtures.sh [ski seed tag]   (no arguments: every fixture)
 if [ $# -eq 3 ]; then run "$1" "$2" "$3"; else all; fi

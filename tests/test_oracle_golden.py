@@ -17,7 +17,8 @@ import oracle_lib as O
 import skirt_files as F
 
 RUNS = [("c1_oligo16", 4357), ("c1_oligo16", 777), ("oligo_2comp", 1234), ("pan_cart16", 4357),
-        ("pan_oct", 4357), ("pan_oct", 99), ("pan_cart16_sa", 4357), ("pan_cart16_sac", 4357)]
+        ("pan_oct", 4357), ("pan_oct", 99), ("pan_cart16_sa", 4357), ("pan_cart16_sac", 4357),
+        ("vor_oligo", 4357), ("vor_pan", 4357)]
 LSUN = 3.839e26  # W (Units.cpp)
 
 
