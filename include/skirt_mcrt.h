@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define SKIRT_MCRT_ABI_VERSION 3
+#define SKIRT_MCRT_ABI_VERSION 4
 
 enum {
     SKIRT_OK = 0,
@@ -42,7 +42,7 @@ enum {
     SKIRT_ERR_UNSUPPORTED = 5
 };
 
-enum { SKIRT_GRID_CARTESIAN = 0, SKIRT_GRID_OCTREE = 1 };
+enum { SKIRT_GRID_CARTESIAN = 0, SKIRT_GRID_OCTREE = 1, SKIRT_GRID_VORONOI = 2 };
 enum { SKIRT_TREE_TOPDOWN = 0, SKIRT_TREE_NEIGHBOR = 1 };
 enum { SKIRT_GEOM_PLUMMER = 0 };
 enum { SKIRT_INSTR_FULL = 0, SKIRT_INSTR_SIMPLE = 1, SKIRT_INSTR_SED = 2, SKIRT_INSTR_FRAME = 3 };
@@ -67,8 +67,19 @@ typedef struct {
     const int* cellnumber;      /* nnodes */
     const int* nbr_offset;      /* 6 * nnodes + 1 */
     const int* nbr_list;        /* nbr_offset[6*nnodes] entries */
-    double eps;                 /* TreeDustGrid::_eps = 1e-12 * |extent widths| */
+    double eps;                 /* TreeDustGrid::_eps / VoronoiMesh::_eps = 1e-12 * |extent widths| */
     int search;                 /* SKIRT_TREE_* */
+    /* Voronoi (VoronoiMesh.cpp:250-306, 512-541, 749-844): per cell its site and neighbour list (CSR;
+     * walls -1 xmin, -2 xmax, -3 ymin, -4 ymax, -5 zmin, -6 zmax), its enclosing box; the domain; the
+     * nb^3 block lists of cells whose box overlaps each block (for the nearest-site cell index) */
+    const double* site;         /* 3 * ncells */
+    const int* cell_nbr_offset; /* ncells + 1 */
+    const int* cell_nbr_list;
+    const double* cell_bbox;    /* 6 * ncells */
+    double extent[6];           /* xmin ymin zmin xmax ymax zmax */
+    int nblocks;                /* nb blocks per axis */
+    const int* block_offset;    /* nb^3 + 1 */
+    const int* block_list;
 } SkirtGridDesc;
 
 /* Dust media (replaces DustSystem::density and the KappaRho functor, DustSystem.cpp:465-491).

@@ -23,7 +23,7 @@ PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(PKG_DIR, os.environ.get("SKIRT_AMD_LIB", "libskirt_amd.so"))
 DATA_DIR = os.path.join(PKG_DIR, "data")
 
-GRID_CARTESIAN, GRID_OCTREE = 0, 1
+GRID_CARTESIAN, GRID_OCTREE, GRID_VORONOI = 0, 1, 2
 
 
 class SkirtError(RuntimeError):

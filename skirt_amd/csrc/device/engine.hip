@@ -111,6 +111,13 @@ struct Args {
     const int* nbrList;
     double eps;
     int search;
+    const double* site;          // Voronoi: 3 per cell
+    const int* cellNbrOffset;    // Voronoi neighbour lists (walls -1 .. -6)
+    const int* cellNbrList;
+    const double* cellBbox;      // Voronoi: enclosing box per cell
+    int vnb;                     // Voronoi block grid: blocks per axis
+    const int* blockOffset;
+    const int* blockList;
     const LeafEntry* leafMap;       // octree leaf map: Morton-ordered finest-level cells -> leaf
     const double* treeT;         // octree split coordinates per axis, 3 x (mapN + 1) (staged in LDS)
     int mapL, mapN;              // leaf map depth and 2^depth
@@ -645,6 +652,112 @@ struct Grid<SKIRT_GRID_OCTREE> {
         if (!inside(a, x, y, z)) return -1;
         int fx, fy, fz;
         return (int)(lookup(a, sh, x, y, z, fx, fy, fz).cl & kLeafCellMask);
+    }
+};
+
+// Voronoi grid: VoronoiMesh::path (VoronoiMesh.cpp:749-844), cellIndex (:512-541), with the
+// reference's arithmetic order (bisector plane through the midpoint, Vec::dot left to right)
+template <>
+struct Grid<SKIRT_GRID_VORONOI> {
+    __device__ static __forceinline__ bool inside(const Args& a, double x, double y, double z) {
+        return x >= a.gx0 && x <= a.gx1 && y >= a.gy0 && y <= a.gy1 && z >= a.gz0 && z <= a.gz1;
+    }
+
+    // the cell whose site is nearest, over the cells listed for the point's block (Box::cellindices)
+    __device__ static __forceinline__ int cellIndex(const Args& a, double x, double y, double z) {
+        if (!inside(a, x, y, z)) return -1;
+        const int nb = a.vnb;
+        const int i = max(0, min(nb - 1, static_cast<int>(nb * (x - a.gx0) / (a.gx1 - a.gx0))));
+        const int j = max(0, min(nb - 1, static_cast<int>(nb * (y - a.gy0) / (a.gy1 - a.gy0))));
+        const int k = max(0, min(nb - 1, static_cast<int>(nb * (z - a.gz0) / (a.gz1 - a.gz0))));
+        const int b = i * nb * nb + j * nb + k;
+        int m = -1;
+        double best = kDblMax;
+        for (int q = a.blockOffset[b]; q < a.blockOffset[b + 1]; q++) {
+            const int c = a.blockList[q];
+            const double dx = x - a.site[3 * c], dy = y - a.site[3 * c + 1], dz = z - a.site[3 * c + 2];
+            const double d = dx * dx + dy * dy + dz * dz;
+            if (d < best) { best = d; m = c; }
+        }
+        return m;
+    }
+
+    template <class SegFn>
+    __device__ static __forceinline__ bool begin(const Args& a, const Shared&, Ray& r, SegFn seg) {
+        double rx = r.x, ry = r.y, rz = r.z, d[3];
+        if (!Grid<kOctreeNodes>::enterGrid(a, rx, ry, rz, r.dx, r.dy, r.dz, d)) return false;
+        const int m = cellIndex(a, rx, ry, rz);
+        if (m < 0) return false;
+        for (int q = 0; q < 3; q++)
+            if (d[q] > 0) seg(-1, 0.0, d[q]);
+        r.x = rx; r.y = ry; r.z = rz;
+        r.ci = m;
+        return true;
+    }
+
+    template <class SegFn>
+    __device__ static __forceinline__ bool step(const Args& a, const Shared&, Ray& r, SegFn seg) {
+        const int mr = r.ci;
+        const double* S = a.site;
+        const double prx = S[3 * mr], pry = S[3 * mr + 1], prz = S[3 * mr + 2];
+        const double kx = r.dx, ky = r.dy, kz = r.dz;
+        double sq = kDblMax;
+        constexpr int NO_INDEX = -99;
+        int mq = NO_INDEX;
+        const int qe = a.cellNbrOffset[mr + 1];
+        for (int q = a.cellNbrOffset[mr]; q < qe; q++) {
+            const int mi = a.cellNbrList[q];
+            double si = 0;
+            if (mi >= 0) {
+                const double pix = S[3 * mi], piy = S[3 * mi + 1], piz = S[3 * mi + 2];
+                const double nx = pix - prx, ny = piy - pry, nz = piz - prz;
+                const double ndotk = nx * kx + ny * ky + nz * kz;
+                if (ndotk > 0) {
+                    const double px = 0.5 * (pix + prx), py = 0.5 * (piy + pry), pz = 0.5 * (piz + prz);
+                    si = (nx * (px - r.x) + ny * (py - r.y) + nz * (pz - r.z)) / ndotk;
+                }
+            } else {
+                switch (mi) {
+                case -1: si = (a.gx0 - r.x) / kx; break;
+                case -2: si = (a.gx1 - r.x) / kx; break;
+                case -3: si = (a.gy0 - r.y) / ky; break;
+                case -4: si = (a.gy1 - r.y) / ky; break;
+                case -5: si = (a.gz0 - r.z) / kz; break;
+                default: si = (a.gz1 - r.z) / kz; break;
+                }
+            }
+            if (si > 0 && si < sq) { sq = si; mq = mi; }
+        }
+        if (mq == NO_INDEX) {
+            // no exit found: advance by eps and locate again (VoronoiMesh.cpp:831-835)
+            r.x += kx * a.eps; r.y += ky * a.eps; r.z += kz * a.eps;
+            r.ci = cellIndex(a, r.x, r.y, r.z);
+            return r.ci >= 0;
+        }
+        if (!seg(mr, a.rho[(size_t)mr * a.ncomp], sq)) return false;
+        r.x += (sq + a.eps) * kx; r.y += (sq + a.eps) * ky; r.z += (sq + a.eps) * kz;
+        r.ci = mq;
+        return mq >= 0;
+    }
+
+    __device__ static __forceinline__ void resume(const Args&, Ray&) {}
+
+    __device__ static __forceinline__ int whichcell(const Args& a, const Shared&, double x, double y, double z) {
+        return cellIndex(a, x, y, z);
+    }
+
+    // VoronoiMesh::isPointClosestTo
+    __device__ static __forceinline__ bool closestTo(const Args& a, double x, double y, double z, int m) {
+        auto d2 = [&](int c) {
+            const double dx = x - a.site[3 * c], dy = y - a.site[3 * c + 1], dz = z - a.site[3 * c + 2];
+            return dx * dx + dy * dy + dz * dz;
+        };
+        const double target = d2(m);
+        for (int q = a.cellNbrOffset[m]; q < a.cellNbrOffset[m + 1]; q++) {
+            const int id = a.cellNbrList[q];
+            if (id >= 0 && d2(id) < target) return false;
+        }
+        return true;
     }
 };
 
@@ -1277,12 +1390,16 @@ struct Events {
         }
         double b[6];
         cellBox(m, b);
-        const double x = p.rng.uniform();
-        const double y = p.rng.uniform();
-        const double z = p.rng.uniform();
-        p.rx = b[0] + x * (b[3] - b[0]);
-        p.ry = b[1] + y * (b[4] - b[1]);
-        p.rz = b[2] + z * (b[5] - b[2]);
+        // VoronoiMesh::randomPosition: points in the enclosing box until one lies in the cell
+        for (int trial = 0; trial < (GRID == SKIRT_GRID_VORONOI ? 10000 : 1); trial++) {
+            const double x = p.rng.uniform();
+            const double y = p.rng.uniform();
+            const double z = p.rng.uniform();
+            p.rx = b[0] + x * (b[3] - b[0]);
+            p.ry = b[1] + y * (b[4] - b[1]);
+            p.rz = b[2] + z * (b[5] - b[2]);
+            if (GRID != SKIRT_GRID_VORONOI || Grid<SKIRT_GRID_VORONOI>::closestTo(a, p.rx, p.ry, p.rz, m)) break;
+        }
         isotropic(p.rng, p.kx, p.ky, p.kz);
         p.L = L;
         p.nscatt = 0;
@@ -1310,6 +1427,8 @@ struct Events {
             const double* zv = yv + a.ny + 1;
             const int i = m / (a.nz * a.ny), j = (m / a.nz) % a.ny, k = m % a.nz;
             b[0] = xv[i]; b[1] = yv[j]; b[2] = zv[k]; b[3] = xv[i + 1]; b[4] = yv[j + 1]; b[5] = zv[k + 1];
+        } else if (GRID == SKIRT_GRID_VORONOI) {
+            for (int q = 0; q < 6; q++) b[q] = a.cellBbox[6 * (size_t)m + q];
         } else {
             const double* bx = a.box + 6 * (size_t)a.cellNode[m];
             for (int q = 0; q < 6; q++) b[q] = bx[q];
@@ -1579,6 +1698,10 @@ struct SkirtMcrt {
     double* dMesh = nullptr;
     double* dBox = nullptr;
     int *dFirstChild = nullptr, *dCellnumber = nullptr, *dNbrOffset = nullptr, *dNbrList = nullptr;
+    // Voronoi grid
+    double *dSite = nullptr, *dCellBbox = nullptr;
+    int *dCellNbrOffset = nullptr, *dCellNbrList = nullptr, *dBlockOffset = nullptr, *dBlockList = nullptr;
+    int vnb = 0;
     // octree leaf map (mapL < 0: walk the node arrays)
     int mapL = -1, mapN = 0;
     double mapInv[3] = {0, 0, 0};
@@ -1883,6 +2006,33 @@ int skirt_mcrt_upload_grid(SkirtMcrt* c, const SkirtGridDesc* g) {
         std::vector<int> dummy(1, 0);
         if ((rc = upload(c, c->dNbrList, nnbr ? g->nbr_list : dummy.data(), nnbr ? (size_t)nnbr : 1))) return rc;
         if ((rc = planLeafMap(c, g))) return rc;
+    } else if (g->kind == SKIRT_GRID_VORONOI) {
+        const int N = g->ncells;
+        if (N < 1 || !g->site || !g->cell_nbr_offset || !g->cell_nbr_list || !g->cell_bbox || g->nblocks < 1 ||
+            !g->block_offset || !g->block_list)
+            return fail(c, SKIRT_ERR_ARG, "bad Voronoi grid");
+        const int nnbr = g->cell_nbr_offset[N];
+        for (int m = 0; m < N; m++)
+            if (g->cell_nbr_offset[m] < 0 || g->cell_nbr_offset[m] > g->cell_nbr_offset[m + 1])
+                return fail(c, SKIRT_ERR_ARG, "bad Voronoi neighbour offsets");
+        for (int q = 0; q < nnbr; q++)
+            if (g->cell_nbr_list[q] < -6 || g->cell_nbr_list[q] >= N) return fail(c, SKIRT_ERR_ARG, "Voronoi neighbour out of range");
+        const size_t nb3 = (size_t)g->nblocks * g->nblocks * g->nblocks;
+        const int nbl = g->block_offset[nb3];
+        for (int q = 0; q < nbl; q++)
+            if (g->block_list[q] < 0 || g->block_list[q] >= N) return fail(c, SKIRT_ERR_ARG, "Voronoi block list out of range");
+        c->eps = g->eps;
+        c->gx0 = g->extent[0]; c->gy0 = g->extent[1]; c->gz0 = g->extent[2];
+        c->gx1 = g->extent[3]; c->gy1 = g->extent[4]; c->gz1 = g->extent[5];
+        c->vnb = g->nblocks;
+        int rc;
+        std::vector<int> dummy(1, 0);
+        if ((rc = upload(c, c->dSite, g->site, 3 * (size_t)N))) return rc;
+        if ((rc = upload(c, c->dCellBbox, g->cell_bbox, 6 * (size_t)N))) return rc;
+        if ((rc = upload(c, c->dCellNbrOffset, g->cell_nbr_offset, (size_t)N + 1))) return rc;
+        if ((rc = upload(c, c->dCellNbrList, nnbr ? g->cell_nbr_list : dummy.data(), nnbr ? (size_t)nnbr : 1))) return rc;
+        if ((rc = upload(c, c->dBlockOffset, g->block_offset, nb3 + 1))) return rc;
+        if ((rc = upload(c, c->dBlockList, nbl ? g->block_list : dummy.data(), nbl ? (size_t)nbl : 1))) return rc;
     } else {
         return fail(c, SKIRT_ERR_UNSUPPORTED, "unsupported grid kind");
     }
@@ -2228,6 +2378,8 @@ int skirt_mcrt_run_phase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, 
     a.gx0 = c->gx0; a.gx1 = c->gx1; a.gy0 = c->gy0; a.gy1 = c->gy1; a.gz0 = c->gz0; a.gz1 = c->gz1;
     a.box = c->dBox; a.firstChild = c->dFirstChild; a.cellnumber = c->dCellnumber;
     a.nbrOffset = c->dNbrOffset; a.nbrList = c->dNbrList; a.eps = c->eps; a.search = c->search;
+    a.site = c->dSite; a.cellNbrOffset = c->dCellNbrOffset; a.cellNbrList = c->dCellNbrList; a.cellBbox = c->dCellBbox;
+    a.vnb = c->vnb; a.blockOffset = c->dBlockOffset; a.blockList = c->dBlockList;
     const bool leafMap = c->gridKind == SKIRT_GRID_OCTREE && c->mapL >= 0 && p->has_dust;
     if (leafMap) {
         if ((rc = ensureLeafMap(c))) return rc;
@@ -2276,12 +2428,15 @@ int skirt_mcrt_run_phase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, 
                             + (size_t)kLabsBuf * kBlock * (sizeof(double) + sizeof(unsigned));  // + Labs buffers
     const size_t ldsEvent = (size_t)a.ldsSedOff * sizeof(double);           // + instruments
     if (lds > 64 * 1024) return fail(c, SKIRT_ERR_UNSUPPORTED, "tables do not fit in LDS (" + std::to_string(lds) + " bytes)");
-    const int kind = c->gridKind == SKIRT_GRID_CARTESIAN ? SKIRT_GRID_CARTESIAN : (leafMap ? SKIRT_GRID_OCTREE : kOctreeNodes);
+    const int kind = c->gridKind == SKIRT_GRID_CARTESIAN ? SKIRT_GRID_CARTESIAN
+                     : c->gridKind == SKIRT_GRID_VORONOI ? SKIRT_GRID_VORONOI
+                     : (leafMap ? SKIRT_GRID_OCTREE : kOctreeNodes);
     const bool one = a.ncomp == 1;
     const void* traceFn = nullptr;
     auto pick = [&](auto fn1, auto fnN) { traceFn = one ? (const void*)fn1 : (const void*)fnN; };
     if (kind == SKIRT_GRID_CARTESIAN) pick(traceKernel<SKIRT_GRID_CARTESIAN, true>, traceKernel<SKIRT_GRID_CARTESIAN, false>);
     else if (kind == SKIRT_GRID_OCTREE) pick(traceKernel<SKIRT_GRID_OCTREE, true>, traceKernel<SKIRT_GRID_OCTREE, false>);
+    else if (kind == SKIRT_GRID_VORONOI) pick(traceKernel<SKIRT_GRID_VORONOI, true>, traceKernel<SKIRT_GRID_VORONOI, false>);
     else pick(traceKernel<kOctreeNodes, true>, traceKernel<kOctreeNodes, false>);
     int tgrid = c->traceGrid;
     if (tgrid <= 0) {
@@ -2302,6 +2457,7 @@ int skirt_mcrt_run_phase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, 
 #define SKIRT_EVENT(G, O) hipLaunchKernelGGL((eventKernel<G, O>), dim3(egrid), dim3(kBlock), ldsEvent, st, aa)
         if (kind == SKIRT_GRID_CARTESIAN) { if (one) SKIRT_EVENT(SKIRT_GRID_CARTESIAN, true); else SKIRT_EVENT(SKIRT_GRID_CARTESIAN, false); }
         else if (kind == SKIRT_GRID_OCTREE) { if (one) SKIRT_EVENT(SKIRT_GRID_OCTREE, true); else SKIRT_EVENT(SKIRT_GRID_OCTREE, false); }
+        else if (kind == SKIRT_GRID_VORONOI) { if (one) SKIRT_EVENT(SKIRT_GRID_VORONOI, true); else SKIRT_EVENT(SKIRT_GRID_VORONOI, false); }
         else { if (one) SKIRT_EVENT(kOctreeNodes, true); else SKIRT_EVENT(kOctreeNodes, false); }
 #undef SKIRT_EVENT
     };
@@ -2309,6 +2465,7 @@ int skirt_mcrt_run_phase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, 
 #define SKIRT_TRACE(G, O) hipLaunchKernelGGL((traceKernel<G, O>), dim3(tgrid), dim3(kBlock), ldsTrace, st, aa)
         if (kind == SKIRT_GRID_CARTESIAN) { if (one) SKIRT_TRACE(SKIRT_GRID_CARTESIAN, true); else SKIRT_TRACE(SKIRT_GRID_CARTESIAN, false); }
         else if (kind == SKIRT_GRID_OCTREE) { if (one) SKIRT_TRACE(SKIRT_GRID_OCTREE, true); else SKIRT_TRACE(SKIRT_GRID_OCTREE, false); }
+        else if (kind == SKIRT_GRID_VORONOI) { if (one) SKIRT_TRACE(SKIRT_GRID_VORONOI, true); else SKIRT_TRACE(SKIRT_GRID_VORONOI, false); }
         else { if (one) SKIRT_TRACE(kOctreeNodes, true); else SKIRT_TRACE(kOctreeNodes, false); }
 #undef SKIRT_TRACE
     };
@@ -2457,7 +2614,8 @@ void skirt_mcrt_destroy(SkirtMcrt* c) {
     void* bufs[] = {c->dMesh, c->dBox, c->dFirstChild, c->dCellnumber, c->dNbrOffset, c->dNbrList, c->dTreeT,
                     c->dLeafMap, c->dCellLv, c->dCellCdf, c->dCellLtot, c->dCellNode, c->dEmisVolume, c->dEmisKabs,
                     c->dEmisSigma, c->dEmisMu, c->dEmisTv, c->dEmisPlanck, c->dEmisLambda, c->dEmisDlambda,
-                    c->dEmisScratch, c->dDevCell, c->dRho,
+                    c->dEmisScratch, c->dDevCell, c->dSite, c->dCellBbox, c->dCellNbrOffset, c->dCellNbrList,
+                    c->dBlockOffset, c->dBlockList, c->dRho,
                     c->dOptics, c->dGeomParam, c->dLum, c->dLumtot, c->dCdf, c->dInstr,
                     c->dClaim, c->dStats, c->dError, c->dCtr, c->dPool};
     for (void* b : bufs)

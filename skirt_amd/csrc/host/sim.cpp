@@ -95,7 +95,8 @@ int skirt_sim_info(SkirtSim* s, SkirtSimInfo* o) {
     o->nlambda = s->m.wl.n();
     o->ncomp = s->m.ncomp();
     o->ninstruments = (int)s->m.instruments.size();
-    o->grid_kind = s->m.grid.kind == GridKind::Octree ? SKIRT_GRID_OCTREE : SKIRT_GRID_CARTESIAN;
+    o->grid_kind = s->m.grid.kind == GridKind::Octree ? SKIRT_GRID_OCTREE
+                   : s->m.grid.kind == GridKind::Voronoi ? SKIRT_GRID_VORONOI : SKIRT_GRID_CARTESIAN;
     o->nnodes = s->m.grid.kind == GridKind::Octree ? s->m.grid.tree.nnodes() : 0;
     o->npp = s->npp;
     o->total_packets = s->npp * (uint64_t)s->m.wl.n();
@@ -116,7 +117,20 @@ int skirt_sim_attach(SkirtSim* s, int device) {
     if (m.hasDust) {
         SkirtGridDesc g{};
         g.ncells = m.ncells();
-        if (m.grid.kind == GridKind::Cartesian) {
+        if (m.grid.kind == GridKind::Voronoi) {
+            const VoronoiGrid& v = m.grid.vor;
+            g.kind = SKIRT_GRID_VORONOI;
+            g.site = v.site.data();
+            g.cell_nbr_offset = v.nbrOffset.data();
+            g.cell_nbr_list = v.nbrList.data();
+            g.cell_bbox = v.bbox.data();
+            g.extent[0] = v.xmin; g.extent[1] = v.ymin; g.extent[2] = v.zmin;
+            g.extent[3] = v.xmax; g.extent[4] = v.ymax; g.extent[5] = v.zmax;
+            g.eps = v.eps;
+            g.nblocks = v.nb;
+            g.block_offset = v.blockOffset.data();
+            g.block_list = v.blockList.data();
+        } else if (m.grid.kind == GridKind::Cartesian) {
             g.kind = SKIRT_GRID_CARTESIAN;
             g.nx = m.grid.cart.Nx; g.ny = m.grid.cart.Ny; g.nz = m.grid.cart.Nz;
             g.xv = m.grid.cart.xv.data(); g.yv = m.grid.cart.yv.data(); g.zv = m.grid.cart.zv.data();

@@ -47,7 +47,7 @@ def close_fraction(a, b, rtol, floor=1e-15):
 
 
 @pytest.mark.parametrize("name,packages", [("c1_oligo16", 20000), ("oligo_2comp", 5000), ("pan_cart16", 3000),
-                                           ("pan_oct", 3000)])
+                                           ("pan_oct", 3000), ("vor_oligo", 5000), ("vor_pan", 1000)])
 def test_engine_matches_oracle_same_streams(name, packages):
     sim = run_gpu(name, packages=packages)
     orc = O.run(ski(name), rng=O.RNG_PHILOX, threads=16, packages=packages)
@@ -93,7 +93,8 @@ def test_leaf_map_walk_equals_node_walk(path, packages, monkeypatch):
     np.testing.assert_allclose(fa, fb, rtol=1e-10, atol=1e-300)
 
 
-@pytest.mark.parametrize("name,packages", [("pan_cart16", 2000), ("pan_oct", 2000), ("pan_cart16_sa", 1000)])
+@pytest.mark.parametrize("name,packages", [("pan_cart16", 2000), ("pan_oct", 2000), ("pan_cart16_sa", 1000),
+                                           ("vor_pan", 1000)])
 def test_dust_phases_match_oracle_same_streams(name, packages):
     """Stellar emission, the self-absorption cycles (if the model has them) and the dust emission phase
     (PanMonteCarloSimulation::runSelf) on the GPU against the oracle on the same Philox streams. The
@@ -158,7 +159,7 @@ def _isrf_sums(path):
     return F.read_text_table(path)[:, 4:].sum(axis=0)
 
 
-@pytest.mark.parametrize("name", ["pan_cart16", "pan_oct", "pan_cart16_sa"])
+@pytest.mark.parametrize("name", ["pan_cart16", "pan_oct", "pan_cart16_sa", "vor_pan"])
 def test_engine_matches_reference_statistically(tmp_path, name):
     """All phases (stellar, self-absorption, dust emission) against `skirt -t 1`: per-wavelength ISRF sums
     and every SED column -- total, direct and scattered stellar, dust emission, dust scattered,
