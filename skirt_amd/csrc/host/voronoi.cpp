@@ -5,7 +5,10 @@
 #include <array>
 #include <cfloat>
 #include <cmath>
+#include <atomic>
 #include <stdexcept>
+#include <string>
+#include <thread>
 
 #include "mt_random.hpp"
 
@@ -176,13 +179,12 @@ void buildVoronoi(VoronoiGrid& g, const std::vector<double>& sites, double xmin,
         }
     }
 
-    g.nbrOffset.assign(N + 1, 0);
-    g.nbrList.clear();
     g.bbox.assign(6 * (size_t)N, 0);
     g.volume.assign(N, 0);
     g.centroid.assign(3 * (size_t)N, 0);
-    std::vector<std::pair<double, int>> cand;
-    for (int i = 0; i < N; i++) {
+    std::vector<std::vector<int>> cellIds(N);
+    // the cells are independent: computed by worker threads over chunks of cell indices
+    auto buildCell = [&](int i, std::vector<std::pair<double, int>>& cand) {
         const V3 s{sites[3 * i], sites[3 * i + 1], sites[3 * i + 2]};
         // the domain box, faces labelled with the wall ids of the reference (Voro++ walls)
         const V3 c000{xmin, ymin, zmin}, c100{xmax, ymin, zmin}, c010{xmin, ymax, zmin}, c110{xmax, ymax, zmin};
@@ -223,7 +225,7 @@ void buildVoronoi(VoronoiGrid& g, const std::vector<double>& sites, double xmin,
             if (r == ng - 1) break;
         }
         // neighbours, bounding box, volume and centroid of the finished cell
-        std::vector<int> ids;
+        std::vector<int>& ids = cellIds[i];
         double bmin[3] = {DBL_MAX, DBL_MAX, DBL_MAX}, bmax[3] = {-DBL_MAX, -DBL_MAX, -DBL_MAX};
         double vol = 0, cx = 0, cy = 0, cz = 0;
         for (const Face& f : cell.faces) {
@@ -241,13 +243,36 @@ void buildVoronoi(VoronoiGrid& g, const std::vector<double>& sites, double xmin,
         }
         std::sort(ids.begin(), ids.end());
         ids.erase(std::unique(ids.begin(), ids.end()), ids.end());
-        g.nbrList.insert(g.nbrList.end(), ids.begin(), ids.end());
-        g.nbrOffset[i + 1] = (int)g.nbrList.size();
         for (int q = 0; q < 3; q++) { g.bbox[6 * (size_t)i + q] = bmin[q]; g.bbox[6 * (size_t)i + 3 + q] = bmax[q]; }
         g.volume[i] = vol;
         g.centroid[3 * (size_t)i] = vol > 0 ? cx / vol : s[0];
         g.centroid[3 * (size_t)i + 1] = vol > 0 ? cy / vol : s[1];
         g.centroid[3 * (size_t)i + 2] = vol > 0 ? cz / vol : s[2];
+    };
+    {
+        const int T = std::max(1, std::min(16, (int)std::thread::hardware_concurrency()));
+        std::atomic<int> next{0};
+        std::vector<std::thread> th;
+        std::vector<std::string> errs(T);
+        for (int w = 0; w < T; w++)
+            th.emplace_back([&, w] {
+                try {
+                    std::vector<std::pair<double, int>> cand;
+                    for (int c0; (c0 = next.fetch_add(64)) < N;)
+                        for (int i = c0; i < std::min(N, c0 + 64); i++) buildCell(i, cand);
+                } catch (std::exception& e) {
+                    errs[w] = e.what();
+                }
+            });
+        for (auto& t : th) t.join();
+        for (auto& e : errs)
+            if (!e.empty()) throw std::runtime_error(e);
+    }
+    g.nbrOffset.assign(N + 1, 0);
+    g.nbrList.clear();
+    for (int i = 0; i < N; i++) {
+        g.nbrList.insert(g.nbrList.end(), cellIds[i].begin(), cellIds[i].end());
+        g.nbrOffset[i + 1] = (int)g.nbrList.size();
     }
 
     // block lists (VoronoiMesh::buildMesh): nb = max(3, min(1000, int(3 N^(1/3)))) blocks per axis
