@@ -8,7 +8,7 @@ wavelengths, peel-off to a 250x250 FullInstrument, Plummer stars + dust (benchma
 Weak scaling: every rank shoots its own slice of the global packet index space and, for N > 1, the
 phase ends with the reference's reductions (Labs all-reduce, instrument all-reduce) done by RCCL.
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2]
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2|c4|c5]
        (N > 1: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...)
 """
 import argparse
@@ -24,6 +24,8 @@ CONFIGS = {
     # name: (ski, packets per wavelength per rank, segment geometry bytes, description)
     "c3": ("benchmarks/c3_oct128.ski", 400000, 56, "C3 octree 128^3 (levels 3-7, mass fraction 1e-6), 25 lambda, peel-off"),
     "c2": ("benchmarks/c2_cart64.ski", 1000000, 0, "C2 Cartesian 64^3, 10 lambda, peel-off"),
+    "c4": ("benchmarks/c4_vor1e5.ski", 200000, 438,
+           "C4 Voronoi 1e5 sites (DustDensity), 25 lambda, peel-off"),
     "c5": ("benchmarks/c5_oct128_sa.ski", 400000, 56,
            "C5 = C3 + dust self-absorption (3 cycles) + dust emission, all phases per step"),
 }
@@ -45,7 +47,7 @@ def pmc_traffic(config):
 
 def algorithmic_bytes(stats, geom_bytes, ncomp):
     """SURVEY.md section 8(d): per segment the cell geometry (octree: 48 B box + 8 B index/neighbour;
-    Cartesian: 0, the mesh lives in LDS) plus 8*Ncomp B of density; 16 B read-modify-write per absorbed
+    Voronoi: 4 + 28 k B for k ~ 15.5 neighbours; Cartesian: 0, the mesh lives in LDS) plus 8*Ncomp B of density; 16 B read-modify-write per absorbed
     segment (Labs) and per frame pixel update of a detection."""
     segs = stats["segments_fill"] + stats["segments_walk"] + stats["segments_peel"]
     return segs * (geom_bytes + 8 * ncomp) + stats["absorb_adds"] * 16 + stats["detects"] * 16
@@ -215,7 +217,7 @@ def main():
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
             "traffic": traffic["bytes_per_launch"] if traffic else None,
-            "kernel": "traceKernel<octree leaf map>" if info.grid_kind == 1 else "traceKernel<cartesian>",
+            "kernel": {0: "traceKernel<cartesian>", 1: "traceKernel<octree leaf map>", 2: "traceKernel<voronoi>"}[info.grid_kind],
             "launch_ms_avg": launch_s * 1e3,
             "launches_per_step": trace_launches / args.steps,
             "algorithmic_bytes_per_launch": bytes_per_launch,
