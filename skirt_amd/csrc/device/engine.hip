@@ -95,6 +95,21 @@ __device__ __forceinline__ int rayEll(unsigned f) { return (int)(f >> 18); }
 
 struct LeafEntry;
 
+// one entry of a Voronoi cell's neighbour list: the neighbour's device cell number (walls -1 .. -6)
+// with its site inline, so that a step reads the cell's list as one contiguous run instead of
+// gathering the neighbours' sites, and where the neighbour's own list starts, so that the next step
+// needs no offset lookup. The last entry of every list has bit 31 of `next` set.
+struct alignas(16) VoronoiNbr {
+    double x, y, z;
+    int id;
+    int next;  // start of the neighbour's list | kVorLast on a list's last entry
+};
+constexpr int kVorLast = (int)0x80000000u;
+#ifndef SKIRT_VOR_UNROLL
+#define SKIRT_VOR_UNROLL 4
+#endif
+constexpr int kVorUnroll = SKIRT_VOR_UNROLL;  // list entries loaded per round trip (the array is padded)
+
 // grid kinds of the kernels: SKIRT_GRID_CARTESIAN, SKIRT_GRID_OCTREE (leaf-map walk) and the octree
 // walked through the node arrays (trees deeper than kMaxMapLevel or not split at box centres)
 constexpr int kOctreeNodes = 16;
@@ -111,10 +126,11 @@ struct Args {
     const int* nbrList;
     double eps;
     int search;
-    const double* site;          // Voronoi: 3 per cell
-    const int* cellNbrOffset;    // Voronoi neighbour lists (walls -1 .. -6)
-    const int* cellNbrList;
+    const double* site;          // Voronoi, device cell order: 3 per cell
+    const int* cellNbrOffset;    // Voronoi neighbour lists
+    const VoronoiNbr* cellNbr;
     const double* cellBbox;      // Voronoi: enclosing box per cell
+    const int* devCell;          // reference cell -> device cell (Voronoi launches)
     int vnb;                     // Voronoi block grid: blocks per axis
     const int* blockOffset;
     const int* blockList;
@@ -692,51 +708,66 @@ struct Grid<SKIRT_GRID_VORONOI> {
             if (d[q] > 0) seg(-1, 0.0, d[q]);
         r.x = rx; r.y = ry; r.z = rz;
         r.ci = m;
+        r.cj = a.cellNbrOffset[m];
         return true;
     }
 
+    // r.ci: the current (device) cell, r.cj: where its neighbour list starts
     template <class SegFn>
     __device__ static __forceinline__ bool step(const Args& a, const Shared&, Ray& r, SegFn seg) {
         const int mr = r.ci;
         const double* S = a.site;
         const double prx = S[3 * mr], pry = S[3 * mr + 1], prz = S[3 * mr + 2];
+        const double rho0 = a.rho[(size_t)mr * a.ncomp];
         const double kx = r.dx, ky = r.dy, kz = r.dz;
         double sq = kDblMax;
         constexpr int NO_INDEX = -99;
-        int mq = NO_INDEX;
-        const int qe = a.cellNbrOffset[mr + 1];
-        for (int q = a.cellNbrOffset[mr]; q < qe; q++) {
-            const int mi = a.cellNbrList[q];
-            double si = 0;
-            if (mi >= 0) {
-                const double pix = S[3 * mi], piy = S[3 * mi + 1], piz = S[3 * mi + 2];
-                const double nx = pix - prx, ny = piy - pry, nz = piz - prz;
-                const double ndotk = nx * kx + ny * ky + nz * kz;
-                if (ndotk > 0) {
-                    const double px = 0.5 * (pix + prx), py = 0.5 * (piy + pry), pz = 0.5 * (piz + prz);
-                    si = (nx * (px - r.x) + ny * (py - r.y) + nz * (pz - r.z)) / ndotk;
+        int mq = NO_INDEX, mqList = 0;
+        for (int q = r.cj;; q += kVorUnroll) {
+            VoronoiNbr e[kVorUnroll];
+#pragma unroll
+            for (int u = 0; u < kVorUnroll; u++) e[u] = a.cellNbr[q + u];
+            bool last = false;
+#pragma unroll
+            for (int u = 0; u < kVorUnroll; u++) {
+                if (last) break;
+                const int mi = e[u].id;
+                double si = 0;
+                if (mi >= 0) {
+                    const double pix = e[u].x, piy = e[u].y, piz = e[u].z;
+                    const double nx = pix - prx, ny = piy - pry, nz = piz - prz;
+                    const double ndotk = nx * kx + ny * ky + nz * kz;
+                    if (ndotk > 0) {
+                        const double px = 0.5 * (pix + prx), py = 0.5 * (piy + pry), pz = 0.5 * (piz + prz);
+                        si = (nx * (px - r.x) + ny * (py - r.y) + nz * (pz - r.z)) / ndotk;
+                    }
+                } else {
+                    switch (mi) {
+                    case -1: si = (a.gx0 - r.x) / kx; break;
+                    case -2: si = (a.gx1 - r.x) / kx; break;
+                    case -3: si = (a.gy0 - r.y) / ky; break;
+                    case -4: si = (a.gy1 - r.y) / ky; break;
+                    case -5: si = (a.gz0 - r.z) / kz; break;
+                    default: si = (a.gz1 - r.z) / kz; break;
+                    }
                 }
-            } else {
-                switch (mi) {
-                case -1: si = (a.gx0 - r.x) / kx; break;
-                case -2: si = (a.gx1 - r.x) / kx; break;
-                case -3: si = (a.gy0 - r.y) / ky; break;
-                case -4: si = (a.gy1 - r.y) / ky; break;
-                case -5: si = (a.gz0 - r.z) / kz; break;
-                default: si = (a.gz1 - r.z) / kz; break;
-                }
+                if (si > 0 && si < sq) { sq = si; mq = mi; mqList = e[u].next & ~kVorLast; }
+                last = e[u].next < 0;
             }
-            if (si > 0 && si < sq) { sq = si; mq = mi; }
+            if (last) break;
         }
         if (mq == NO_INDEX) {
             // no exit found: advance by eps and locate again (VoronoiMesh.cpp:831-835)
             r.x += kx * a.eps; r.y += ky * a.eps; r.z += kz * a.eps;
             r.ci = cellIndex(a, r.x, r.y, r.z);
-            return r.ci >= 0;
+            if (r.ci < 0) return false;
+            r.cj = a.cellNbrOffset[r.ci];
+            return true;
         }
-        if (!seg(mr, a.rho[(size_t)mr * a.ncomp], sq)) return false;
+        if (!seg(mr, rho0, sq)) return false;
         r.x += (sq + a.eps) * kx; r.y += (sq + a.eps) * ky; r.z += (sq + a.eps) * kz;
         r.ci = mq;
+        r.cj = mqList;
         return mq >= 0;
     }
 
@@ -748,14 +779,14 @@ struct Grid<SKIRT_GRID_VORONOI> {
 
     // VoronoiMesh::isPointClosestTo
     __device__ static __forceinline__ bool closestTo(const Args& a, double x, double y, double z, int m) {
-        auto d2 = [&](int c) {
-            const double dx = x - a.site[3 * c], dy = y - a.site[3 * c + 1], dz = z - a.site[3 * c + 2];
+        auto d2 = [&](double sx, double sy, double sz) {
+            const double dx = x - sx, dy = y - sy, dz = z - sz;
             return dx * dx + dy * dy + dz * dz;
         };
-        const double target = d2(m);
+        const double target = d2(a.site[3 * m], a.site[3 * m + 1], a.site[3 * m + 2]);
         for (int q = a.cellNbrOffset[m]; q < a.cellNbrOffset[m + 1]; q++) {
-            const int id = a.cellNbrList[q];
-            if (id >= 0 && d2(id) < target) return false;
+            const VoronoiNbr nb = a.cellNbr[q];
+            if (nb.id >= 0 && d2(nb.x, nb.y, nb.z) < target) return false;
         }
         return true;
     }
@@ -1388,6 +1419,7 @@ struct Events {
         } else {
             m = locateClipGlobal(cdf, N + 1, X);
         }
+        if (GRID == SKIRT_GRID_VORONOI) m = a.devCell[m];  // the Voronoi arrays are in device order
         double b[6];
         cellBox(m, b);
         // VoronoiMesh::randomPosition: points in the enclosing box until one lies in the cell
@@ -1419,7 +1451,8 @@ struct Events {
         return jl;
     }
 
-    // the box of reference cell m (CartesianDustGrid::box, TreeDustGrid::getnode(m)->extent())
+    // the box of cell m (CartesianDustGrid::box, TreeDustGrid::getnode(m)->extent()): reference cell
+    // numbers, except the Voronoi grid's device numbers
     __device__ __forceinline__ void cellBox(int m, double (&b)[6]) const {
         if (GRID == SKIRT_GRID_CARTESIAN) {
             const double* xv = sh.mesh;
@@ -1700,7 +1733,8 @@ struct SkirtMcrt {
     int *dFirstChild = nullptr, *dCellnumber = nullptr, *dNbrOffset = nullptr, *dNbrList = nullptr;
     // Voronoi grid
     double *dSite = nullptr, *dCellBbox = nullptr;
-    int *dCellNbrOffset = nullptr, *dCellNbrList = nullptr, *dBlockOffset = nullptr, *dBlockList = nullptr;
+    VoronoiNbr* dCellNbr = nullptr;
+    int *dCellNbrOffset = nullptr, *dBlockOffset = nullptr, *dBlockList = nullptr;
     int vnb = 0;
     // octree leaf map (mapL < 0: walk the node arrays)
     int mapL = -1, mapN = 0;
@@ -2025,14 +2059,66 @@ int skirt_mcrt_upload_grid(SkirtMcrt* c, const SkirtGridDesc* g) {
         c->gx0 = g->extent[0]; c->gy0 = g->extent[1]; c->gz0 = g->extent[2];
         c->gx1 = g->extent[3]; c->gy1 = g->extent[4]; c->gz1 = g->extent[5];
         c->vnb = g->nblocks;
+        // device cell numbers in Morton order of the sites (21 bits per axis, ties by reference number):
+        // cells adjacent in space are adjacent in memory, for the neighbour lists, the densities and the
+        // Labs tallies alike. Every list keeps its reference order (first-minimum choices depend on it).
+        c->devCell.assign(N, 0);
+        {
+            std::vector<std::pair<uint64_t, int>> key(N);
+            const double ext[3] = {c->gx1 - c->gx0, c->gy1 - c->gy0, c->gz1 - c->gz0};
+            const double lo[3] = {c->gx0, c->gy0, c->gz0};
+            for (int m = 0; m < N; m++) {
+                uint64_t code = 0;
+                for (int d = 0; d < 3; d++) {
+                    const double f = (g->site[3 * (size_t)m + d] - lo[d]) / ext[d];
+                    const uint64_t u = (uint64_t)std::max(0.0, std::min(2097151.0, f * 2097152.0));
+                    for (int bit = 0; bit < 21; bit++) code |= ((u >> bit) & 1ull) << (3 * bit + (2 - d));
+                }
+                key[m] = {code, m};
+            }
+            std::sort(key.begin(), key.end());
+            for (int q = 0; q < N; q++) c->devCell[key[q].second] = q;
+        }
+        std::vector<int> refOf(N);
+        for (int m = 0; m < N; m++) refOf[c->devCell[m]] = m;
+        std::vector<double> site(3 * (size_t)N), bbox(6 * (size_t)N);
+        std::vector<int> offset(N + 1, 0);
+        for (int d = 0; d < N; d++) {
+            const int m = refOf[d];
+            const int cnt = g->cell_nbr_offset[m + 1] - g->cell_nbr_offset[m];
+            if (cnt < 1) return fail(c, SKIRT_ERR_ARG, "Voronoi cell without neighbours");
+            offset[d + 1] = offset[d] + cnt;
+        }
+        // kVorUnroll - 1 entries of padding: a step loads whole groups of entries
+        std::vector<VoronoiNbr> nbr((size_t)nnbr + kVorUnroll, VoronoiNbr{0., 0., 0., -1, kVorLast});
+        for (int d = 0; d < N; d++) {
+            const int m = refOf[d];
+            for (int q = 0; q < 3; q++) site[3 * (size_t)d + q] = g->site[3 * (size_t)m + q];
+            for (int q = 0; q < 6; q++) bbox[6 * (size_t)d + q] = g->cell_bbox[6 * (size_t)m + q];
+            int o = offset[d];
+            for (int q = g->cell_nbr_offset[m]; q < g->cell_nbr_offset[m + 1]; q++, o++) {
+                const int id = g->cell_nbr_list[q];
+                VoronoiNbr& e = nbr[o];
+                e = VoronoiNbr{0., 0., 0., id, 0};
+                if (id >= 0) {
+                    const int did = c->devCell[id];
+                    e.id = did;
+                    e.next = offset[did];
+                    e.x = g->site[3 * (size_t)id]; e.y = g->site[3 * (size_t)id + 1]; e.z = g->site[3 * (size_t)id + 2];
+                }
+                if (q + 1 == g->cell_nbr_offset[m + 1]) e.next |= kVorLast;
+            }
+        }
+        std::vector<int> blocks(std::max(nbl, 1), 0);
+        for (int q = 0; q < nbl; q++) blocks[q] = c->devCell[g->block_list[q]];
         int rc;
-        std::vector<int> dummy(1, 0);
-        if ((rc = upload(c, c->dSite, g->site, 3 * (size_t)N))) return rc;
-        if ((rc = upload(c, c->dCellBbox, g->cell_bbox, 6 * (size_t)N))) return rc;
-        if ((rc = upload(c, c->dCellNbrOffset, g->cell_nbr_offset, (size_t)N + 1))) return rc;
-        if ((rc = upload(c, c->dCellNbrList, nnbr ? g->cell_nbr_list : dummy.data(), nnbr ? (size_t)nnbr : 1))) return rc;
+        if ((rc = upload(c, c->dSite, site.data(), site.size()))) return rc;
+        if ((rc = upload(c, c->dCellBbox, bbox.data(), bbox.size()))) return rc;
+        if ((rc = upload(c, c->dCellNbrOffset, offset.data(), offset.size()))) return rc;
+        if ((rc = upload(c, c->dCellNbr, nbr.data(), nbr.size()))) return rc;
         if ((rc = upload(c, c->dBlockOffset, g->block_offset, nb3 + 1))) return rc;
-        if ((rc = upload(c, c->dBlockList, nbl ? g->block_list : dummy.data(), nbl ? (size_t)nbl : 1))) return rc;
+        if ((rc = upload(c, c->dBlockList, blocks.data(), blocks.size()))) return rc;
+        if ((rc = upload(c, c->dDevCell, c->devCell.data(), c->devCell.size()))) return rc;
     } else {
         return fail(c, SKIRT_ERR_UNSUPPORTED, "unsupported grid kind");
     }
@@ -2378,7 +2464,8 @@ int skirt_mcrt_run_phase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, 
     a.gx0 = c->gx0; a.gx1 = c->gx1; a.gy0 = c->gy0; a.gy1 = c->gy1; a.gz0 = c->gz0; a.gz1 = c->gz1;
     a.box = c->dBox; a.firstChild = c->dFirstChild; a.cellnumber = c->dCellnumber;
     a.nbrOffset = c->dNbrOffset; a.nbrList = c->dNbrList; a.eps = c->eps; a.search = c->search;
-    a.site = c->dSite; a.cellNbrOffset = c->dCellNbrOffset; a.cellNbrList = c->dCellNbrList; a.cellBbox = c->dCellBbox;
+    a.site = c->dSite; a.cellNbrOffset = c->dCellNbrOffset; a.cellNbr = c->dCellNbr; a.cellBbox = c->dCellBbox;
+    a.devCell = c->dDevCell;
     a.vnb = c->vnb; a.blockOffset = c->dBlockOffset; a.blockList = c->dBlockList;
     const bool leafMap = c->gridKind == SKIRT_GRID_OCTREE && c->mapL >= 0 && p->has_dust;
     if (leafMap) {
@@ -2614,7 +2701,7 @@ void skirt_mcrt_destroy(SkirtMcrt* c) {
     void* bufs[] = {c->dMesh, c->dBox, c->dFirstChild, c->dCellnumber, c->dNbrOffset, c->dNbrList, c->dTreeT,
                     c->dLeafMap, c->dCellLv, c->dCellCdf, c->dCellLtot, c->dCellNode, c->dEmisVolume, c->dEmisKabs,
                     c->dEmisSigma, c->dEmisMu, c->dEmisTv, c->dEmisPlanck, c->dEmisLambda, c->dEmisDlambda,
-                    c->dEmisScratch, c->dDevCell, c->dSite, c->dCellBbox, c->dCellNbrOffset, c->dCellNbrList,
+                    c->dEmisScratch, c->dDevCell, c->dSite, c->dCellBbox, c->dCellNbrOffset, c->dCellNbr,
                     c->dBlockOffset, c->dBlockList, c->dRho,
                     c->dOptics, c->dGeomParam, c->dLum, c->dLumtot, c->dCdf, c->dInstr,
                     c->dClaim, c->dStats, c->dError, c->dCtr, c->dPool};
