@@ -8,19 +8,93 @@
 // caller's UniformSource so that a single-threaded reference run and this setup produce bit-identical
 // densities and trees.
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <dlfcn.h>
 #include <fstream>
 #include <numeric>
 #include <sstream>
 #include <stdexcept>
+#include <thread>
 
 #include "model.hpp"
+#include "mt_random.hpp"
 #include "xml.hpp"
 
 namespace skirt {
+
+namespace {
+// SKIRT_AMD_SETUP_TIMES=1 prints the duration of every setup stage to stderr
+struct StageTimer {
+    const char* name;
+    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+    explicit StageTimer(const char* n) : name(n) {}
+    ~StageTimer() {
+        static const bool on = std::getenv("SKIRT_AMD_SETUP_TIMES") != nullptr;
+        if (on)
+            std::fprintf(stderr, "[setup] %-24s %.3f s\n", name,
+                         std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
+    }
+};
+
+// Runs fn(q, u) for the items q in [0, n) on worker threads, where u points to the `per` uniform
+// deviates item q would have drawn had the items been processed one after the other, drawing as they
+// go: the deviates are drawn ahead, in item order, one chunk at a time (the next chunk while the
+// workers evaluate the current one). Results are therefore identical to the sequential loop's.
+template <class Fn>
+void parallelDraws(UniformSource& rng, size_t n, int per, Fn fn) {
+    if (n == 0) return;
+    const size_t chunk = std::max<size_t>(1, (size_t)(1 << 20) / std::max(1, per));
+    const int T = std::max(1, std::min(16, (int)std::thread::hardware_concurrency()));
+    // the Mersenne twister hands over raw words (the sequential part); the workers convert them
+    MTRandom* mt = dynamic_cast<MTRandom*>(&rng);
+    std::vector<uint32_t> wbuf[2];
+    std::vector<double> dbuf[2];
+    auto draw = [&](int k, size_t q0) {
+        const size_t m = (std::min(n, q0 + chunk) - q0) * per;
+        if (mt) {
+            wbuf[k].resize(m);
+            mt->words(wbuf[k].data(), m);
+        } else {
+            dbuf[k].resize(m);
+            for (double& u : dbuf[k]) u = rng.uniform();
+        }
+    };
+    draw(0, 0);
+    for (size_t q0 = 0, k = 0; q0 < n; q0 += chunk, k ^= 1) {
+        const size_t q1 = std::min(n, q0 + chunk);
+        std::atomic<size_t> next{q0};
+        std::vector<std::thread> th;
+        std::vector<std::string> errs(T);
+        for (int w = 0; w < T; w++)
+            th.emplace_back([&, w] {
+                try {
+                    std::vector<double> u(per);
+                    for (size_t q; (q = next.fetch_add(64)) < q1;)
+                        for (size_t e = q; e < std::min(q1, q + 64); e++) {
+                            if (mt) {
+                                const uint32_t* y = &wbuf[k][(e - q0) * per];
+                                for (int i = 0; i < per; i++) u[i] = MTRandom::deviate(y[i]);
+                                fn(e, u.data());
+                            } else {
+                                fn(e, &dbuf[k][(e - q0) * per]);
+                            }
+                        }
+                } catch (std::exception& ex) {
+                    errs[w] = ex.what();
+                }
+            });
+        if (q1 < n) draw((int)(k ^ 1), q1);
+        for (auto& t : th) t.join();
+        for (auto& e : errs)
+            if (!e.empty()) throw std::runtime_error(e);
+    }
+}
+}  // namespace
 
 // ============================================================ small numeric helpers (Fundamentals/NR.hpp)
 namespace nr {
@@ -622,18 +696,26 @@ void buildOctree(const Ctx& c, const XmlElement* e, const Model& model, OctreeGr
 
     TreeBuilder tb(t);
     tb.addNode(-1, t.xmin, t.ymin, t.zmin, t.xmax, t.ymax, t.zmax);
-    std::vector<double> rhov(Nrandom);
-    for (size_t l = 0; l < t.firstChild.size(); l++) {
-        if (t.firstChild[l] >= 0) continue;
-        int level = t.level[l];
-        if (level <= t.minLevel) {
-            tb.createChildren((int)l);
-        } else if (level < t.maxLevel) {
+    // TreeDustGrid::setupSelfBefore visits the nodes in creation order, subdividing as it goes. The nodes
+    // that exist when a pass starts are decided together: the sampling ones draw their positions in
+    // node order (parallelDraws), the subdivisions are then applied in node order, so that every node
+    // number and every random draw is the reference's.
+    const bool always = maxOpticalDepth == 0 && maxMassFraction == 0 && maxDensDispFraction == 0;
+    for (size_t l0 = 0; l0 < t.firstChild.size();) {
+        const size_t l1 = t.firstChild.size();
+        std::vector<int> sampled;  // nodes that sample the density, in node order
+        for (size_t l = l0; l < l1; l++)
+            if (t.level[l] > t.minLevel && t.level[l] < t.maxLevel) sampled.push_back((int)l);
+        std::vector<char> divide(l1 - l0, 0);
+        for (size_t l = l0; l < l1; l++) divide[l - l0] = t.level[l] <= t.minLevel;
+        parallelDraws(*c.rng, sampled.size(), 3 * Nrandom, [&](size_t q, const double* u) {
             // TreeNodeSampleDensityCalculator: Nrandom positions in the node, density of all components
+            const int l = sampled[q];
             double b[6];
-            std::memcpy(b, tb.box((int)l), sizeof b);
+            std::memcpy(b, tb.box(l), sizeof b);
+            std::vector<double> rhov(Nrandom);
             for (int n = 0; n < Nrandom; n++) {
-                double fx = c.rng->uniform(), fy = c.rng->uniform(), fz = c.rng->uniform();
+                double fx = u[3 * n], fy = u[3 * n + 1], fz = u[3 * n + 2];
                 double x = b[0] + fx * (b[3] - b[0]), y = b[1] + fy * (b[4] - b[1]), z = b[2] + fz * (b[5] - b[2]);
                 double rho = 0;
                 for (auto& d : model.dust) rho += d.density(x, y, z);
@@ -641,7 +723,7 @@ void buildOctree(const Ctx& c, const XmlElement* e, const Model& model, OctreeGr
             }
             double vol = (b[3] - b[0]) * (b[4] - b[1]) * (b[5] - b[2]);
             double mass = nr::sum(rhov) / Nrandom * vol;
-            bool needDivision = (maxOpticalDepth == 0 && maxMassFraction == 0 && maxDensDispFraction == 0);
+            bool needDivision = always;
             if (!needDivision && maxMassFraction > 0 && mass / totalmass >= maxMassFraction) needDivision = true;
             if (!needDivision && maxOpticalDepth > 0 &&
                 constants::kappaV * mass / std::pow(vol, 2. / 3.) >= maxOpticalDepth)
@@ -652,8 +734,11 @@ void buildOctree(const Ctx& c, const XmlElement* e, const Model& model, OctreeGr
                 double disp = mx > 0 ? (mx - mn) / mx : 0;
                 if (disp >= maxDensDispFraction) needDivision = true;
             }
-            if (needDivision) tb.createChildren((int)l);
-        }
+            divide[l - l0] = needDivision;
+        });
+        for (size_t l = l0; l < l1; l++)
+            if (divide[l - l0]) tb.createChildren((int)l);
+        l0 = l1;
     }
     int Nnodes = t.nnodes();
     t.cellnumber.assign(Nnodes, -1);
@@ -799,6 +884,7 @@ static void buildVoronoiGrid(const Ctx& c, const XmlElement* ge, Model& m, Unifo
     } else {
         throw std::runtime_error("unsupported Voronoi particle distribution " + dist);
     }
+    StageTimer st("tessellation");
     buildVoronoi(m.grid.vor, sites, xmin, xmax, ymin, ymax, zmin, zmax);
 }
 
@@ -930,10 +1016,12 @@ Model loadSki(const std::string& path, UniformSource& rng, const std::string& da
             m.grid.ncells = g.Nx * g.Ny * g.Nz;
         } else if (ge->name == "OctTreeDustGrid") {
             m.grid.kind = GridKind::Octree;
+            StageTimer st("octree");
             buildOctree(c, ge, m, m.grid.tree);
             m.grid.ncells = (int)m.grid.tree.idv.size();
         } else if (ge->name == "VoronoiDustGrid") {
             m.grid.kind = GridKind::Voronoi;
+            StageTimer st("voronoi");
             buildVoronoiGrid(c, ge, m, rng);
             m.grid.ncells = m.grid.vor.ncells();
         } else {
@@ -941,26 +1029,36 @@ Model loadSki(const std::string& path, UniformSource& rng, const std::string& da
         }
 
         // DustSystem::setupSelfAfter: volumes, then densities sampled at sampleCount random positions
+        StageTimer st("cell densities");
         int Ncells = m.grid.ncells, Ncomp = m.ncomp();
         m.volume.resize(Ncells);
         for (int cell = 0; cell < Ncells; cell++) m.volume[cell] = m.grid.cellVolume(cell);
         m.rho.assign((size_t)Ncells * Ncomp, 0.0);
-        std::vector<double> sumv(Ncomp);
-        for (int cell = 0; cell < Ncells; cell++) {
-            double b[6];
-            m.grid.cellBox(cell, b);
-            std::fill(sumv.begin(), sumv.end(), 0.0);
-            for (int n = 0; n < m.sampleCount; n++) {
-                double x, y, z;
-                if (m.grid.kind == GridKind::Voronoi) {
+        if (m.grid.kind == GridKind::Voronoi) {
+            // rejection sampling draws a data-dependent number of deviates: one cell after the other
+            std::vector<double> sumv(Ncomp);
+            for (int cell = 0; cell < Ncells; cell++) {
+                std::fill(sumv.begin(), sumv.end(), 0.0);
+                for (int n = 0; n < m.sampleCount; n++) {
+                    double x, y, z;
                     voronoiRandomPosition(m.grid.vor, rng, cell, x, y, z);  // VoronoiMesh::randomPosition
-                } else {
-                    double fx = rng.uniform(), fy = rng.uniform(), fz = rng.uniform();
-                    x = b[0] + fx * (b[3] - b[0]); y = b[1] + fy * (b[4] - b[1]); z = b[2] + fz * (b[5] - b[2]);
+                    for (int h = 0; h < Ncomp; h++) sumv[h] += m.dust[h].density(x, y, z);
                 }
-                for (int h = 0; h < Ncomp; h++) sumv[h] += m.dust[h].density(x, y, z);
+                for (int h = 0; h < Ncomp; h++) m.rho[(size_t)cell * Ncomp + h] = 1.0 * sumv[h] / m.sampleCount;
             }
-            for (int h = 0; h < Ncomp; h++) m.rho[(size_t)cell * Ncomp + h] = 1.0 * sumv[h] / m.sampleCount;
+        } else {
+            // Random::position(box) per sample: three deviates, drawn ahead in cell order
+            parallelDraws(rng, (size_t)Ncells, 3 * m.sampleCount, [&](size_t cell, const double* u) {
+                double b[6];
+                m.grid.cellBox((int)cell, b);
+                std::vector<double> sumv(Ncomp, 0.0);
+                for (int n = 0; n < m.sampleCount; n++) {
+                    const double fx = u[3 * n], fy = u[3 * n + 1], fz = u[3 * n + 2];
+                    const double x = b[0] + fx * (b[3] - b[0]), y = b[1] + fy * (b[4] - b[1]), z = b[2] + fz * (b[5] - b[2]);
+                    for (int h = 0; h < Ncomp; h++) sumv[h] += m.dust[h].density(x, y, z);
+                }
+                for (int h = 0; h < Ncomp; h++) m.rho[cell * Ncomp + h] = 1.0 * sumv[h] / m.sampleCount;
+            });
         }
     }
 

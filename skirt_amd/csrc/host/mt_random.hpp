@@ -8,6 +8,7 @@
 // The photon-shooting hot path on the GPU uses Philox (see device/philox.hpp), not this generator.
 #pragma once
 
+#include <cstddef>
 #include <cstdint>
 
 namespace skirt {
@@ -21,6 +22,21 @@ public:
 class MTRandom final : public UniformSource {
 public:
     explicit MTRandom(unsigned long seed = 4357) { seed_(seed); }
+
+    // the tempered 32-bit outputs behind the next n deviates: uniform() == word / 0xffffffff, and the
+    // words it rejects (0 and 0xffffffff, the deviates 0 and 1) are skipped here as there
+    void words(uint32_t* out, size_t n) {
+        for (size_t q = 0; q < n;) {
+            if (mti_ >= 624) refill_();
+            unsigned long y = mt_[mti_++];
+            y ^= (y >> 11);
+            y ^= (y << 7) & 0x9d2c5680UL;
+            y ^= (y << 15) & 0xefc60000UL;
+            y ^= (y >> 18);
+            if (y != 0 && y != 0xffffffffUL) out[q++] = (uint32_t)y;
+        }
+    }
+    static double deviate(uint32_t y) { return static_cast<double>(y) / static_cast<unsigned long>(0xffffffffUL); }
 
     double uniform() override {
         double ans;

@@ -5,6 +5,7 @@
 #include <array>
 #include <cfloat>
 #include <cmath>
+#include <cstdint>
 #include <atomic>
 #include <stdexcept>
 #include <string>
@@ -108,6 +109,98 @@ struct Cell {
     }
 };
 
+
+// A k-d tree over the sites (leaves of at most 8, split at the median of the widest axis) answering
+// "the k nearest sites to p other than `self`, in (squared distance, index) order".
+class SiteTree {
+public:
+    explicit SiteTree(const std::vector<double>& s) : site_(s), idx_(s.size() / 3) {
+        for (size_t q = 0; q < idx_.size(); q++) idx_[q] = (int)q;
+        if (!idx_.empty()) build(0, (int)idx_.size());
+    }
+
+    void nearest(const V3& p, int self, int k, std::vector<std::pair<double, int>>& out) const {
+        out.clear();
+        if (nodes_.empty()) return;
+        // max-heap of the best k by (d2, index)
+        auto worse = [](const std::pair<double, int>& x, const std::pair<double, int>& y) { return x < y; };
+        std::vector<int> stack{0};
+        while (!stack.empty()) {
+            const Node& nd = nodes_[stack.back()];
+            stack.pop_back();
+            if ((int)out.size() == k && boxDist2(nd, p) > out.front().first) continue;
+            if (nd.left < 0) {
+                for (int q = nd.lo; q < nd.hi; q++) {
+                    const int j = idx_[q];
+                    if (j == self) continue;
+                    const double dx = site_[3 * j] - p[0], dy = site_[3 * j + 1] - p[1], dz = site_[3 * j + 2] - p[2];
+                    const std::pair<double, int> c{dx * dx + dy * dy + dz * dz, j};
+                    if ((int)out.size() < k) {
+                        out.push_back(c);
+                        std::push_heap(out.begin(), out.end(), worse);
+                    } else if (c < out.front()) {
+                        std::pop_heap(out.begin(), out.end(), worse);
+                        out.back() = c;
+                        std::push_heap(out.begin(), out.end(), worse);
+                    }
+                }
+            } else {
+                // nearer child last, so that it is visited first
+                const bool leftFirst = p[nd.dim] < nd.split;
+                stack.push_back(leftFirst ? nd.right : nd.left);
+                stack.push_back(leftFirst ? nd.left : nd.right);
+            }
+        }
+        std::sort_heap(out.begin(), out.end(), worse);
+    }
+
+private:
+    struct Node {
+        int lo, hi, left = -1, right = -1, dim = 0;
+        double split = 0, bmin[3], bmax[3];
+    };
+    const std::vector<double>& site_;
+    std::vector<int> idx_;
+    std::vector<Node> nodes_;
+
+    static double boxDist2(const Node& nd, const V3& p) {
+        double d2 = 0;
+        for (int q = 0; q < 3; q++) {
+            const double d = p[q] < nd.bmin[q] ? nd.bmin[q] - p[q] : p[q] > nd.bmax[q] ? p[q] - nd.bmax[q] : 0.;
+            d2 += d * d;
+        }
+        return d2;
+    }
+
+    int build(int lo, int hi) {
+        const int me = (int)nodes_.size();
+        nodes_.push_back(Node{lo, hi});
+        Node nd{lo, hi};
+        for (int q = 0; q < 3; q++) { nd.bmin[q] = DBL_MAX; nd.bmax[q] = -DBL_MAX; }
+        for (int t = lo; t < hi; t++)
+            for (int q = 0; q < 3; q++) {
+                nd.bmin[q] = std::min(nd.bmin[q], site_[3 * (size_t)idx_[t] + q]);
+                nd.bmax[q] = std::max(nd.bmax[q], site_[3 * (size_t)idx_[t] + q]);
+            }
+        if (hi - lo > 8) {
+            int dim = 0;
+            for (int q = 1; q < 3; q++)
+                if (nd.bmax[q] - nd.bmin[q] > nd.bmax[dim] - nd.bmin[dim]) dim = q;
+            const int mid = (lo + hi) / 2;
+            std::nth_element(idx_.begin() + lo, idx_.begin() + mid, idx_.begin() + hi, [&](int x, int y) {
+                const double a = site_[3 * (size_t)x + dim], b = site_[3 * (size_t)y + dim];
+                return a < b || (a == b && x < y);
+            });
+            nd.dim = dim;
+            nd.split = site_[3 * (size_t)idx_[mid] + dim];
+            nd.left = build(lo, mid);
+            nd.right = build(mid, hi);
+        }
+        nodes_[me] = nd;
+        return me;
+    }
+};
+
 }  // namespace
 
 void VoronoiGrid::blockIndices(double x, double y, double z, int& i, int& j, int& k) const {
@@ -155,30 +248,9 @@ void buildVoronoi(VoronoiGrid& g, const std::vector<double>& sites, double xmin,
     const int N = g.ncells();
     if (N < 1) throw std::runtime_error("a Voronoi grid needs sites");
 
-    // bucket grid over the sites: the candidates of a cell come shell by shell around its bucket
-    const int ng = std::max(1, (int)std::cbrt(N / 2.0));
-    const double bw[3] = {wx / ng, wy / ng, wz / ng};
-    const double wmin = std::min(bw[0], std::min(bw[1], bw[2]));
-    auto bucketOf = [&](const double* p, int* b) {
-        const double lo[3] = {xmin, ymin, zmin};
-        for (int q = 0; q < 3; q++) b[q] = std::max(0, std::min(ng - 1, (int)((p[q] - lo[q]) / bw[q])));
-    };
-    std::vector<int> bOff((size_t)ng * ng * ng + 1, 0), bList(N);
-    for (int m = 0; m < N; m++) {
-        int b[3];
-        bucketOf(&sites[3 * m], b);
-        bOff[(b[0] * ng + b[1]) * ng + b[2] + 1]++;
-    }
-    for (size_t q = 1; q < bOff.size(); q++) bOff[q] += bOff[q - 1];
-    {
-        std::vector<int> fill(bOff.begin(), bOff.end() - 1);
-        for (int m = 0; m < N; m++) {
-            int b[3];
-            bucketOf(&sites[3 * m], b);
-            bList[fill[(b[0] * ng + b[1]) * ng + b[2]]++] = m;
-        }
-    }
-
+    // candidate neighbours come nearest first from a k-d tree over the sites (the sites of a
+    // DustDensity grid cluster by orders of magnitude, which a uniform bucket grid cannot follow)
+    const SiteTree tree(sites);
     g.bbox.assign(6 * (size_t)N, 0);
     g.volume.assign(N, 0);
     g.centroid.assign(3 * (size_t)N, 0);
@@ -194,27 +266,14 @@ void buildVoronoi(VoronoiGrid& g, const std::vector<double>& sites, double xmin,
                       {-3, {c000, c100, c101, c001}}, {-4, {c010, c011, c111, c110}},
                       {-5, {c000, c010, c110, c100}}, {-6, {c001, c101, c111, c011}}};
         double R2 = cell.maxDist2(s);
-        int b[3];
-        bucketOf(&sites[3 * i], b);
-        for (int r = 0; r < ng; r++) {
-            if (r > 0 && ((r - 1) * wmin) * ((r - 1) * wmin) >= 4 * R2) break;  // no site beyond can cut
-            cand.clear();
-            for (int bx = std::max(0, b[0] - r); bx <= std::min(ng - 1, b[0] + r); bx++)
-                for (int by = std::max(0, b[1] - r); by <= std::min(ng - 1, b[1] + r); by++)
-                    for (int bz = std::max(0, b[2] - r); bz <= std::min(ng - 1, b[2] + r); bz++) {
-                        if (std::max(std::abs(bx - b[0]), std::max(std::abs(by - b[1]), std::abs(bz - b[2]))) != r) continue;
-                        const int bb = (bx * ng + by) * ng + bz;
-                        for (int q = bOff[bb]; q < bOff[bb + 1]; q++) {
-                            const int j = bList[q];
-                            if (j == i) continue;
-                            const V3 pj{sites[3 * j], sites[3 * j + 1], sites[3 * j + 2]};
-                            const V3 d = sub(pj, s);
-                            cand.push_back({dot(d, d), j});
-                        }
-                    }
-            std::sort(cand.begin(), cand.end());
-            for (auto& cj : cand) {
-                if (cj.first >= 4 * R2) break;  // too far to cut (|pj - s| / 2 >= farthest vertex)
+        // the k nearest sites in (distance, index) order; each larger query extends the previous one
+        size_t done = 0;
+        for (int k = 32;; k *= 2) {
+            tree.nearest(s, i, k, cand);
+            bool stop = false;
+            for (size_t q = done; q < cand.size(); q++) {
+                const auto& cj = cand[q];
+                if (cj.first >= 4 * R2) { stop = true; break; }  // too far to cut (|pj - s| / 2 >= farthest vertex)
                 const int j = cj.second;
                 const V3 pj{sites[3 * j], sites[3 * j + 1], sites[3 * j + 2]};
                 const V3 n = sub(pj, s);
@@ -222,7 +281,8 @@ void buildVoronoi(VoronoiGrid& g, const std::vector<double>& sites, double xmin,
                 const double tol = 1e-12 * std::sqrt(cj.first) * L;
                 if (cell.clip(n, dot(n, mid), tol, j)) R2 = cell.maxDist2(s);
             }
-            if (r == ng - 1) break;
+            if (stop || (int)cand.size() < k) break;  // cut off, or every other site seen
+            done = cand.size();
         }
         // neighbours, bounding box, volume and centroid of the finished cell
         std::vector<int>& ids = cellIds[i];
@@ -277,23 +337,39 @@ void buildVoronoi(VoronoiGrid& g, const std::vector<double>& sites, double xmin,
 
     // block lists (VoronoiMesh::buildMesh): nb = max(3, min(1000, int(3 N^(1/3)))) blocks per axis
     g.nb = std::max(3, std::min(1000, static_cast<int>(3. * std::pow(N, 1. / 3.))));
-    const int nb = g.nb, nb3 = nb * nb * nb;
-    std::vector<std::vector<int>> lists(nb3);
+    const int nb = g.nb;
+    const size_t nb2 = (size_t)nb * nb, nb3 = nb2 * nb;
+    std::vector<int> range(6 * (size_t)N);  // block index range of every cell's eps-widened box
     for (int m = 0; m < N; m++) {
-        int i1, j1, k1, i2, j2, k2;
         const double* bx = &g.bbox[6 * (size_t)m];
-        g.blockIndices(bx[0] - g.eps, bx[1] - g.eps, bx[2] - g.eps, i1, j1, k1);
-        g.blockIndices(bx[3] + g.eps, bx[4] + g.eps, bx[5] + g.eps, i2, j2, k2);
-        for (int i = i1; i <= i2; i++)
-            for (int j = j1; j <= j2; j++)
-                for (int k = k1; k <= k2; k++) lists[(size_t)i * nb * nb + j * nb + k].push_back(m);
+        int* r = &range[6 * (size_t)m];
+        g.blockIndices(bx[0] - g.eps, bx[1] - g.eps, bx[2] - g.eps, r[0], r[1], r[2]);
+        g.blockIndices(bx[3] + g.eps, bx[4] + g.eps, bx[5] + g.eps, r[3], r[4], r[5]);
     }
-    g.blockOffset.assign(nb3 + 1, 0);
-    g.blockList.clear();
-    for (int b = 0; b < nb3; b++) {
-        g.blockList.insert(g.blockList.end(), lists[b].begin(), lists[b].end());
-        g.blockOffset[b + 1] = (int)g.blockList.size();
-    }
+    // CSR over the blocks, each list in cell order; worker threads own slabs of the first block index
+    std::vector<size_t> count(nb3 + 1, 0);
+    const int T = std::max(1, std::min(16, (int)std::thread::hardware_concurrency()));
+    auto slabs = [&](auto&& fn) {
+        std::vector<std::thread> th;
+        for (int w = 0; w < T; w++)
+            th.emplace_back([&, w] {
+                const int i0 = (int)((long long)nb * w / T), i1 = (int)((long long)nb * (w + 1) / T);
+                for (int m = 0; m < N; m++) {
+                    const int* r = &range[6 * (size_t)m];
+                    for (int i = std::max(r[0], i0); i <= std::min(r[3], i1 - 1); i++)
+                        for (int j = r[1]; j <= r[4]; j++)
+                            for (int k = r[2]; k <= r[5]; k++) fn((size_t)i * nb2 + (size_t)j * nb + k, m);
+                }
+            });
+        for (auto& t : th) t.join();
+    };
+    slabs([&](size_t b, int) { count[b + 1]++; });
+    for (size_t b = 0; b < nb3; b++) count[b + 1] += count[b];
+    if (count[nb3] > (size_t)INT32_MAX) throw std::runtime_error("Voronoi block lists too long");
+    g.blockOffset.assign(count.begin(), count.end());
+    g.blockList.assign(count[nb3], 0);
+    std::vector<int> fill(g.blockOffset.begin(), g.blockOffset.end() - 1);
+    slabs([&](size_t b, int m) { g.blockList[fill[b]++] = m; });
 }
 
 void voronoiRandomPosition(const VoronoiGrid& g, UniformSource& rng, int m, double& x, double& y, double& z) {
