@@ -100,7 +100,9 @@ def main():
     ski_rel, ppl_default, geom_bytes, desc = CONFIGS[args.config]
     ski = os.path.join(REPO, ski_rel)
     ppl = args.packets_per_lambda or ppl_default
+    t_setup = time.perf_counter()
     sim = skirt_amd.Simulation(ski, packages=float(ppl * world))
+    setup_s = time.perf_counter() - t_setup  # host model setup: grid, densities (outside the timed region)
     info = sim.info
     # weak scaling: the phase has ppl packets per wavelength per rank; rank r shoots its contiguous
     # slice of the global packet index space
@@ -207,6 +209,7 @@ def main():
             "segments_per_packet": segs / max(1, delta["packets"]),
             "lane_use": (delta["segments_fill"] + delta["segments_walk"] + delta["segments_peel"]) / max(1, delta["lane_slots"]),
             "iterations": s1["iterations"],
+            "host_setup_s": round(setup_s, 3),
             "per_packet": {k: delta[k] / max(1, delta["packets"]) for k in
                            ("segments_fill", "segments_walk", "segments_peel", "absorb_adds", "detects")},
         },

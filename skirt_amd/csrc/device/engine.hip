@@ -45,7 +45,13 @@ constexpr int kBlock = 256;
 #define SKIRT_LABS_BUF 16
 #endif
 constexpr int kLabsBuf = SKIRT_LABS_BUF;  // buffered Labs adds per trace lane (LDS)
-constexpr int kStepsPerPull = 4;   // grid steps between two ray pulls of a trace wave
+#ifndef SKIRT_STEPS_PER_PULL
+#define SKIRT_STEPS_PER_PULL 4
+#endif
+constexpr int kStepsPerPull = SKIRT_STEPS_PER_PULL;  // grid steps between two ray pulls of a trace wave
+#ifndef SKIRT_PULL_CHUNK
+#define SKIRT_PULL_CHUNK 64        // queue ids a trace wave reserves at once (0: exactly its idle lanes; >= 64)
+#endif
 // The slot pool runs as kHalves independent pipelines on their own streams: while one half's trace
 // kernel drains its queue, the other half's event and detect kernels (and its trace kernel's first
 // waves) fill the CUs the finishing waves leave idle.
@@ -55,6 +61,9 @@ constexpr int kPollRing = 3;       // copies in flight per half (the host reads 
 // occupancy attribute of the trace kernel (a build knob for tuning variants, tools/build_variant.sh)
 #ifndef SKIRT_TRACE_ATTR
 #define SKIRT_TRACE_ATTR
+#endif
+#ifndef SKIRT_EVENT_ATTR
+#define SKIRT_EVENT_ATTR
 #endif
 
 // ------------------------------------------------------------------ descriptors
@@ -260,13 +269,17 @@ __device__ __forceinline__ constexpr int gridParts() {
     return GRID == SKIRT_GRID_CARTESIAN ? STAGE_MESH : (GRID == SKIRT_GRID_OCTREE ? STAGE_TREE : 0);
 }
 
+// The counters live in kStatCopies copies of one 64-byte line each (summed by the host): the waves of a
+// launch end together, and same-line atomics from all of them would queue on one L2 channel.
+constexpr int kStatCopies = 64;
 __device__ __forceinline__ void flushStats(const Args& a, const unsigned long long (&vals)[7]) {
     const int lane = threadIdx.x & 63;
+    unsigned long long* dst = a.stats + 8 * ((blockIdx.x * (kBlock / 64) + threadIdx.x / 64) & (kStatCopies - 1));
 #pragma unroll
     for (int q = 0; q < 7; q++) {
         unsigned long long v = vals[q];
         for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
-        if (lane == 0 && v) atomicAdd(a.stats + q, v);
+        if (lane == 0 && v) atomicAdd(dst + q, v);
     }
 }
 
@@ -820,7 +833,11 @@ struct Tracer {
             const int src = G * i + lane / kLabsBuf;
             const int n = __shfl(npend, src);
             const int q = j * kBlock + wbase + src;
+#ifdef SKIRT_EXPERIMENT_NO_LABS_ATOMICS  // tuning experiment only: the cost of the Labs atomics
+            if (j < n && pendVal[q] == -1.0) atomicAddF64(a.labs + pendIdx[q], pendVal[q]);
+#else
             if (j < n) atomicAddF64(a.labs + pendIdx[q], pendVal[q]);
+#endif
         }
         npend = 0;
     }
@@ -1140,19 +1157,42 @@ __global__ void __launch_bounds__(kBlock) SKIRT_TRACE_ATTR traceKernel(const Arg
     Ray r;
     r.mode = RAY_NONE;
     bool done = false;
+#if SKIRT_PULL_CHUNK
+    // the wave reserves queue ids kPullChunk at a time and hands them to its idle lanes; the next
+    // reservation is requested while the current one still lasts, so a pull rarely waits for the atomic
+    constexpr unsigned kPullChunk = SKIRT_PULL_CHUNK;
+    unsigned cur = 0, curEnd = 0, nxt = 0;
+    bool haveNext = false;
+    auto reserve = [&]() {
+        unsigned int base = 0;
+        if (lane == 0) base = atomicAdd(a.ctr + 4, kPullChunk);
+        return __shfl(base, 0);
+    };
+#endif
     while (true) {
         const bool idle = (r.mode == RAY_NONE) && !done;
         const unsigned long long imask = __ballot(idle);
         const unsigned long long amask = __ballot(r.mode != RAY_NONE);
         if (imask == 0 && amask == 0) break;
         if (imask != 0 && (amask == 0 || __popcll(imask) >= a.threshold)) {
+            const unsigned int rank = (unsigned int)__popcll(imask & ((1ull << lane) - 1ull));
+#if SKIRT_PULL_CHUNK
+            const unsigned int k = (unsigned int)__popcll(imask);
+            const unsigned int avail = curEnd - cur;
+            if (avail < k && !haveNext) { nxt = reserve(); haveNext = true; }
+            const unsigned int id = rank < avail ? cur + rank : nxt + (rank - avail);
+            if (avail >= k) cur += k;
+            else { cur = nxt + (k - avail); curEnd = nxt + kPullChunk; haveNext = false; }
+            if (!haveNext && curEnd - cur < kPullChunk / 2 && cur < nrays) { nxt = reserve(); haveNext = true; }
+#else
             // idle lanes pull consecutive rays from the queue with one atomic per wave
             const int leader = __ffsll((long long)imask) - 1;
             unsigned int base = 0;
             if (lane == leader) base = atomicAdd(a.ctr + 4, (unsigned int)__popcll(imask));
             base = __shfl(base, leader);
+            const unsigned int id = base + rank;
+#endif
             if (idle) {
-                const unsigned int id = base + (unsigned int)__popcll(imask & ((1ull << lane) - 1ull));
                 if (id >= nrays) done = true;
                 else T.load(r, id);  // a RAY_NONE record (empty path) leaves the lane idle
             }
@@ -1543,7 +1583,7 @@ struct Events {
 enum PeelKind : int { PEEL_NONE = 0, PEEL_EMISSION = 1, PEEL_SCATTER = 2 };
 
 template <int GRID, bool ONECOMP>
-__global__ void __launch_bounds__(kBlock) eventKernel(const Args a) {
+__global__ void __launch_bounds__(kBlock) SKIRT_EVENT_ATTR eventKernel(const Args a) {
     extern __shared__ __attribute__((aligned(16))) double lds[];
     if (blockIdx.x == 0 && threadIdx.x == 0) a.ctr[4] = 0;  // the trace kernel's pull counter
     if (!a.init && a.ctr[2 + a.parity] == 0) return;  // an iteration after the end of the phase
@@ -1782,7 +1822,7 @@ struct SkirtMcrt {
     void* dPool = nullptr;               // kHalves pools of nslots / kHalves slots each
     size_t poolBytes = 0;
     // config
-    int traceGrid = 0, threshold = 16, slotsWanted = 0;
+    int traceGrid = 0, threshold = 8, slotsWanted = 0;
     double lastMs = 0;
     std::vector<hipEvent_t> traceEv;  // pairs around the trace launches not yet timed
     int traceLaunches = 0;
@@ -1928,7 +1968,7 @@ int skirt_mcrt_create(int device, SkirtMcrt** out) {
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
         hipMalloc(&c->dClaim, sizeof(unsigned long long)) != hipSuccess ||
-        hipMalloc(&c->dStats, 8 * sizeof(unsigned long long)) != hipSuccess ||
+        hipMalloc(&c->dStats, 8 * kStatCopies * sizeof(unsigned long long)) != hipSuccess ||
         hipMalloc(&c->dError, sizeof(unsigned int)) != hipSuccess ||
         hipMalloc(&c->dCtr, kHalves * 8 * sizeof(unsigned int)) != hipSuccess ||
         hipHostMalloc(&c->hCtr, kHalves * kPollRing * 8 * sizeof(unsigned int)) != hipSuccess ||
@@ -1941,7 +1981,7 @@ int skirt_mcrt_create(int device, SkirtMcrt** out) {
     c->stream = c->own;
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->numCUs = prop.multiProcessorCount;
-    (void)hipMemset(c->dStats, 0, 8 * sizeof(unsigned long long));
+    (void)hipMemset(c->dStats, 0, 8 * kStatCopies * sizeof(unsigned long long));
     (void)hipMemset(c->dError, 0, sizeof(unsigned int));
     *out = c;
     return SKIRT_OK;
@@ -2261,7 +2301,7 @@ int skirt_mcrt_zero_tallies(SkirtMcrt* c) {
     const size_t nl = (size_t)c->ncells * c->nlambda;
     if (c->dLabs && nl) HIPCHECK(c, hipMemsetAsync(c->dLabs, 0, nl * sizeof(double), c->stream));
     if (c->dTally && c->nInstrTally) HIPCHECK(c, hipMemsetAsync(c->dTally, 0, c->nInstrTally * sizeof(double), c->stream));
-    HIPCHECK(c, hipMemsetAsync(c->dStats, 0, 8 * sizeof(unsigned long long), c->stream));
+    HIPCHECK(c, hipMemsetAsync(c->dStats, 0, 8 * kStatCopies * sizeof(unsigned long long), c->stream));
     HIPCHECK(c, hipMemsetAsync(c->dError, 0, sizeof(unsigned int), c->stream));
     return SKIRT_OK;
 }
@@ -2531,7 +2571,9 @@ int skirt_mcrt_run_phase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, 
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, traceFn, kBlock, ldsTrace) != hipSuccess || per < 1) per = 2;
         tgrid = std::max(1, c->numCUs) * per;
     }
-    const int egrid = std::max(1, std::min((slots + kBlock - 1) / kBlock, std::max(1, c->numCUs) * 8));
+    // event kernel blocks per CU (SKIRT_AMD_EVENT_BPC: tuning knob)
+    static const int ebpc = getenv("SKIRT_AMD_EVENT_BPC") ? std::max(1, atoi(getenv("SKIRT_AMD_EVENT_BPC"))) : 2;
+    const int egrid = std::max(1, std::min((slots + kBlock - 1) / kBlock, std::max(1, c->numCUs) * ebpc));
     const int dgrid = std::max(1, std::max(1, c->numCUs) * 4);
 
     HIPCHECK(c, hipMemsetAsync(c->dClaim, 0, sizeof(unsigned long long), c->stream));
@@ -2676,8 +2718,11 @@ int skirt_mcrt_stats(SkirtMcrt* c, SkirtStats* out) {
     if (!c || !out) return SKIRT_ERR_ARG;
     HIPCHECK(c, hipSetDevice(c->device));
     HIPCHECK(c, hipStreamSynchronize(c->stream));
-    unsigned long long v[8];
-    HIPCHECK(c, hipMemcpy(v, c->dStats, sizeof v, hipMemcpyDeviceToHost));
+    std::vector<unsigned long long> copies(8 * kStatCopies);
+    HIPCHECK(c, hipMemcpy(copies.data(), c->dStats, copies.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    unsigned long long v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int k = 0; k < kStatCopies; k++)
+        for (int q = 0; q < 8; q++) v[q] += copies[8 * k + q];
     out->packets = v[0];
     out->segments_fill = v[1];
     out->segments_walk = v[2];
