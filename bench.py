@@ -5,7 +5,8 @@ One "step" is one stellar-emission phase (MonteCarloSimulation::runstellaremissi
 SKIRTcore/MonteCarloSimulation.cpp:251-261) over a fixed number of primary photon packets per GPU on the
 C3 workload: Pan simulation, 128^3-resolution octree (levels 3-7, Saftly mass-fraction refinement), 25
 wavelengths, peel-off to a 250x250 FullInstrument, Plummer stars + dust (benchmarks/c3_oct128.ski).
-Weak scaling: every rank shoots its own slice of the global packet index space and, for N > 1, the
+C3 shoots 4e7 packets per wavelength (1e9 in all) on 8 GPUs, so a step is one rank's share of it:
+5e6 packets per wavelength, 1.25e8 packets. Weak scaling: every rank shoots its own slice of the global packet index space and, for N > 1, the
 phase ends with the reference's reductions (Labs all-reduce, instrument all-reduce) done by RCCL.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2|c4|c5]
@@ -22,7 +23,8 @@ sys.path.insert(0, REPO)
 
 CONFIGS = {
     # name: (ski, packets per wavelength per rank, segment geometry bytes, description)
-    "c3": ("benchmarks/c3_oct128.ski", 400000, 56, "C3 octree 128^3 (levels 3-7, mass fraction 1e-6), 25 lambda, peel-off"),
+    # C3 is 4e7 packets per wavelength (1e9 in all) over 8 GPUs: 5e6 per wavelength per rank
+    "c3": ("benchmarks/c3_oct128.ski", 5000000, 56, "C3 octree 128^3 (levels 3-7, mass fraction 1e-6), 25 lambda, peel-off"),
     "c2": ("benchmarks/c2_cart64.ski", 1000000, 0, "C2 Cartesian 64^3, 10 lambda, peel-off"),
     "c4": ("benchmarks/c4_vor1e5.ski", 200000, 438,
            "C4 Voronoi 1e5 sites (DustDensity), 25 lambda, peel-off"),
