@@ -1582,8 +1582,44 @@ struct Events {
 // peel-off set queued by a slot in this iteration
 enum PeelKind : int { PEEL_NONE = 0, PEEL_EMISSION = 1, PEEL_SCATTER = 2 };
 
+// Block-wide reservation on shared counters: every thread of the block calls it with its counts c0, c1
+// (either may be 0); one atomic per counter per block (a device-wide counter serializes its
+// atomics, so one per block instead of one per wave) returns each thread's first index in r0, r1.
+// wave totals and the block's bases go through `scratch` (static LDS, 2 * (kBlock / 64) + 2 words).
+template <class T0, class T1>
+__device__ __forceinline__ void blockReserve(T0* ctr0, T0 c0, T0& r0, T1* ctr1, T1 c1, T1& r1, unsigned long long* scratch) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    constexpr int W = kBlock / 64;
+    T0 i0 = c0;
+    T1 i1 = c1;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const T0 v0 = __shfl_up(i0, off);
+        const T1 v1 = __shfl_up(i1, off);
+        if (lane >= off) { i0 += v0; i1 += v1; }
+    }
+    if (lane == 63) { scratch[wave] = (unsigned long long)i0; scratch[W + wave] = (unsigned long long)i1; }
+    __syncthreads();
+    T0 w0 = 0, t0 = 0;
+    T1 w1 = 0, t1 = 0;
+#pragma unroll
+    for (int w = 0; w < W; w++) {
+        const T0 s0 = (T0)scratch[w];
+        const T1 s1 = (T1)scratch[W + w];
+        if (w < wave) { w0 += s0; w1 += s1; }
+        t0 += s0; t1 += s1;
+    }
+    if (threadIdx.x == 0) scratch[2 * W] = (ctr0 && t0) ? (unsigned long long)atomicAdd(ctr0, t0) : 0ull;
+    if (threadIdx.x == 64) scratch[2 * W + 1] = (ctr1 && t1) ? (unsigned long long)atomicAdd(ctr1, t1) : 0ull;
+    __syncthreads();
+    r0 = (T0)scratch[2 * W] + w0 + i0 - c0;
+    r1 = (T1)scratch[2 * W + 1] + w1 + i1 - c1;
+    __syncthreads();  // the scratch words are reused by the next call
+}
+
 template <int GRID, bool ONECOMP>
 __global__ void __launch_bounds__(kBlock) SKIRT_EVENT_ATTR eventKernel(const Args a) {
+    __shared__ unsigned long long resv[2 * (kBlock / 64) + 2];
     extern __shared__ __attribute__((aligned(16))) double lds[];
     if (blockIdx.x == 0 && threadIdx.x == 0) a.ctr[4] = 0;  // the trace kernel's pull counter
     if (!a.init && a.ctr[2 + a.parity] == 0) return;  // an iteration after the end of the phase
@@ -1644,16 +1680,13 @@ __global__ void __launch_bounds__(kBlock) SKIRT_EVENT_ATTR eventKernel(const Arg
                 p.state = S_FILL;
             }
         }
-        // slots without a packet claim the next global packet indices (one atomic per wave)
+        // slots without a packet claim the next global packet indices (one atomic per block)
         bool need = valid && p.state == S_NEW && mainMode == RAY_NONE;
-        while (__ballot(need)) {
-            const unsigned long long nmask = __ballot(need);
-            const int leader = __ffsll((long long)nmask) - 1;
-            unsigned long long base = 0;
-            if (lane == leader) base = atomicAdd(a.claim, (unsigned long long)__popcll(nmask));
-            base = __shfl(base, leader);
+        while (__syncthreads_or(need)) {
+            unsigned long long idx = 0;
+            unsigned int unused = 0;
+            blockReserve<unsigned long long, unsigned int>(a.claim, need ? 1ull : 0ull, idx, nullptr, 0u, unused, resv);
             if (need) {
-                const unsigned long long idx = base + __popcll(nmask & ((1ull << lane) - 1ull));
                 if (idx >= total) need = false;  // exhausted: the slot retires
                 else if (E.launch(p, a.first + idx)) {
                     if (!(p.L > 0)) {
@@ -1687,20 +1720,11 @@ __global__ void __launch_bounds__(kBlock) SKIRT_EVENT_ATTR eventKernel(const Arg
             }
         }
         if (mainMode != RAY_NONE) nray++;
-        // wave-wide inclusive scan of nray; one atomic per wave reserves the queue space
-        int incl = nray;
-#pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-            const int v = __shfl_up(incl, off);
-            if (lane >= off) incl += v;
-        }
-        const int totalRays = __shfl(incl, 63);
-        unsigned int qbase = 0;
-        if (totalRays > 0) {
-            if (lane == 63) qbase = atomicAdd(a.ctr + a.parity, (unsigned int)totalRays);
-            qbase = __shfl(qbase, 63);
-        }
-        unsigned int pos = qbase + (unsigned)(incl - nray);
+        // the queue space of the block's rays and the slots staying active: one atomic each per block
+        const bool active = mainMode != RAY_NONE;
+        unsigned int pos = 0, apos = 0;
+        blockReserve<unsigned int, unsigned int>(a.ctr + a.parity, (unsigned)nray, pos, a.ctr + 2 + (1 - a.parity),
+                                                 active ? 1u : 0u, apos, resv);
         const int npeel = nray - (mainMode != RAY_NONE ? 1 : 0);
         int inext = 0;  // next instrument to consider for a peel-off
         for (int k = 0; k < nray; k++) {
@@ -1741,15 +1765,7 @@ __global__ void __launch_bounds__(kBlock) SKIRT_EVENT_ATTR eventKernel(const Arg
             E.emitRay(pos++, p, dx, dy, dz, prm, idx, flags);
         }
         // the slot stays active while it has a FILL/WALK ray in flight
-        const bool active = mainMode != RAY_NONE;
-        const unsigned long long am = __ballot(active);
-        if (am) {
-            const int leader = __ffsll((long long)am) - 1;
-            unsigned int abase = 0;
-            if (lane == leader) abase = atomicAdd(a.ctr + 2 + (1 - a.parity), (unsigned int)__popcll(am));
-            abase = __shfl(abase, leader);
-            if (active) actOut[abase + __popcll(am & ((1ull << lane) - 1ull))] = slot;
-        }
+        if (active) actOut[apos] = slot;
         if (valid) E.store(slot, p);
     }
     const unsigned long long vals[7] = {E.packets, E.segFill, E.segWalk, E.segPeel, E.detects, 0, 0};
