@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define SKIRT_MCRT_ABI_VERSION 4
+#define SKIRT_MCRT_ABI_VERSION 5
 
 enum {
     SKIRT_OK = 0,
@@ -51,7 +51,8 @@ enum { SKIRT_PHASE_STELLAR = 0, SKIRT_PHASE_DUST_EMISSION = 1, SKIRT_PHASE_DUST_
 typedef struct SkirtMcrt SkirtMcrt;
 
 /* Dust grid (replaces DustGrid::path/whichcell). Cartesian: border arrays of nx+1, ny+1, nz+1
- * values, cell index m = k + nz*j + nz*ny*i (CartesianDustGrid.cpp:305-308). Octree: the reference's
+ * values, cell index m = k + nz*j + nz*ny*i (CartesianDustGrid.cpp:305-308). Octree (and k-d tree, see
+ * split_dir): the reference's
  * breadth-first node vector (TreeDustGrid.cpp:50-164): per node a box {xmin,ymin,zmin,xmax,ymax,zmax},
  * the index of its first of 8 consecutive children (-1 for a leaf) and its cell number (-1 for
  * non-leaves); neighbor lists per (node, wall) in CSR form, walls BACK FRONT LEFT RIGHT BOTTOM TOP,
@@ -80,6 +81,10 @@ typedef struct {
     int nblocks;                /* nb blocks per axis */
     const int* block_offset;    /* nb^3 + 1 */
     const int* block_list;
+    /* binary trees (BinTreeDustGrid, the k-d tree; BinTreeNode.cpp): per node the axis its two children
+     * split (0 x, 1 y, 2 z; ignored for leaves). NULL for octrees. first_child then points at the first
+     * of 2 consecutive children. */
+    const signed char* split_dir;
 } SkirtGridDesc;
 
 /* Dust media (replaces DustSystem::density and the KappaRho functor, DustSystem.cpp:465-491).
@@ -164,7 +169,13 @@ typedef struct {
     double kernel_ms;           /* device time of the last run call (HIP events on the engine stream) */
     double trace_ms;            /* trace-kernel time (HIP events around each launch), cumulative */
     uint64_t trace_launches;    /* trace-kernel launches timed so far, cumulative */
+    int32_t grid_walk;          /* walk of the last run: SKIRT_WALK_* */
+    int32_t map_level;          /* tree leaf-map depth (finest cells per axis = 2^map_level), -1 without */
 } SkirtStats;
+
+/* grid walks of the trace kernel (SkirtStats::grid_walk) */
+enum { SKIRT_WALK_CARTESIAN = 0, SKIRT_WALK_OCTREE_MAP = 1, SKIRT_WALK_VORONOI = 2, SKIRT_WALK_TREE_NODES = 3,
+       SKIRT_WALK_KDTREE_MAP = 4 };
 
 int skirt_mcrt_abi_version(void);
 int skirt_mcrt_create(int device, SkirtMcrt** out);

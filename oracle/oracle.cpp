@@ -296,16 +296,12 @@ void voronoiPath(const VoronoiGrid& g, Vec3 r0, Vec3 k, Path& p) {
     }
 }
 
-// TreeNode::whichnode(r) from the root (TreeNode.cpp:70-80), OctTreeNode::child(r)
+// TreeNode::whichnode(r) from the root (TreeNode.cpp:70-80), OctTreeNode::child(r) / BinTreeNode::child(r)
 int rootWhichnode(const OctreeGrid& t, double x, double y, double z) {
     const double* b = &t.box[0];
     if (!(x >= b[0] && x <= b[3] && y >= b[1] && y <= b[4] && z >= b[2] && z <= b[5])) return -1;
     int l = 0;
-    while (t.firstChild[l] >= 0) {
-        int c0 = t.firstChild[l];
-        const double* cb = &t.box[6 * (size_t)c0];
-        l = c0 + (x < cb[3] ? 0 : 1) + (y < cb[4] ? 0 : 2) + (z < cb[5] ? 0 : 4);
-    }
+    while (t.firstChild[l] >= 0) l = t.child(l, x, y, z);
     return l;
 }
 
@@ -938,6 +934,35 @@ const double* oracle_labs_dust(OracleRun* r) { return r->tal.labsDust.empty() ? 
 int oracle_selfabs_cycles(OracleRun* r, const double** totals) {
     *totals = r->labsDustTotals.empty() ? nullptr : r->labsDustTotals.data();
     return (int)r->labsDustTotals.size();
+}
+
+int oracle_grid_paths(const char* ski, const char* datadir, int n, const double* rays, int maxseg, double* out,
+                      int* nseg, int* ncells) {
+    try {
+        std::string dd = datadir && *datadir ? datadir : defaultDataDir();
+        MTRandom mt(readSkiSeed(ski));
+        Model M = loadSki(ski, mt, dd);
+        if (!M.hasDust) throw std::runtime_error("the model has no dust grid");
+        if (ncells) *ncells = M.ncells();
+        Sim sim(M);
+        Path p;
+        for (int i = 0; i < n; i++) {
+            const double* q = rays + 6 * (size_t)i;
+            sim.path(Vec3{q[0], q[1], q[2]}, Vec3{q[3], q[4], q[5]}, p);
+            const int ns = std::min<int>((int)p.v.size(), maxseg);
+            nseg[i] = ns;
+            for (int j = 0; j < ns; j++) {
+                double* o = out + 7 * ((size_t)i * maxseg + j);
+                if (p.v[j].m >= 0) M.grid.cellBox(p.v[j].m, o);
+                else for (int k = 0; k < 6; k++) o[k] = NAN;
+                o[6] = p.v[j].ds;
+            }
+        }
+        return 0;
+    } catch (const std::exception& e) {
+        g_error = e.what();
+        return -1;
+    }
 }
 
 double oracle_seconds(OracleRun* r) { return r->seconds; }

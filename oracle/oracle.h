@@ -63,6 +63,12 @@ int oracle_selfabs_cycles(OracleRun* r, const double** totals);
 int oracle_instrument(OracleRun* r, int i, const double** frames, const double** seds, int* nslots,
                       int* nframe, int* nlambda);
 int oracle_num_instruments(OracleRun* r);
+/* DustGrid::path of the ski's dust grid (built with the ski's seed) for n rays of 6 doubles each
+ * (position, unit direction). Per ray at most maxseg segments are written to out, 7 doubles each: the
+ * cell's box {xmin ymin zmin xmax ymax zmax} (NaN for the segments before the grid) and ds; nseg[i] is
+ * the ray's segment count (capped at maxseg), *ncells the grid's cell count. Returns 0, -1 on failure. */
+int oracle_grid_paths(const char* ski, const char* datadir, int n, const double* rays, int maxseg, double* out,
+                      int* nseg, int* ncells);
 /* statistics: number of packets launched, path segments traversed, wall seconds of the photon phases */
 double oracle_seconds(OracleRun* r);
 uint64_t oracle_packets(OracleRun* r);

@@ -24,6 +24,8 @@ LIB_PATH = os.path.join(PKG_DIR, os.environ.get("SKIRT_AMD_LIB", "libskirt_amd.s
 DATA_DIR = os.path.join(PKG_DIR, "data")
 
 GRID_CARTESIAN, GRID_OCTREE, GRID_VORONOI = 0, 1, 2
+# SkirtStats.grid_walk: the trace kernel's grid walk in the last run (SKIRT_WALK_*)
+WALK_CARTESIAN, WALK_OCTREE_MAP, WALK_VORONOI, WALK_TREE_NODES, WALK_KDTREE_MAP = 0, 1, 2, 3, 4
 
 
 class SkirtError(RuntimeError):
@@ -35,7 +37,7 @@ class SkirtStats(ctypes.Structure):
                 ("segments_walk", ctypes.c_uint64), ("segments_peel", ctypes.c_uint64),
                 ("detects", ctypes.c_uint64), ("absorb_adds", ctypes.c_uint64), ("lane_slots", ctypes.c_uint64),
                 ("iterations", ctypes.c_uint64), ("kernel_ms", ctypes.c_double), ("trace_ms", ctypes.c_double),
-                ("trace_launches", ctypes.c_uint64)]
+                ("trace_launches", ctypes.c_uint64), ("grid_walk", ctypes.c_int32), ("map_level", ctypes.c_int32)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -119,9 +119,11 @@ constexpr int kVorLast = (int)0x80000000u;
 #endif
 constexpr int kVorUnroll = SKIRT_VOR_UNROLL;  // list entries loaded per round trip (the array is padded)
 
-// grid kinds of the kernels: SKIRT_GRID_CARTESIAN, SKIRT_GRID_OCTREE (leaf-map walk) and the octree
-// walked through the node arrays (trees deeper than kMaxMapLevel or not split at box centres)
+// grid kinds of the kernels: SKIRT_GRID_CARTESIAN, SKIRT_GRID_OCTREE (leaf-map walk), the k-d tree
+// through its leaf map, and any tree walked through the node arrays (trees deeper than the leaf maps
+// allow or not split at box centres, e.g. barycentric subdivision)
 constexpr int kOctreeNodes = 16;
+constexpr int kBinTreeMap = 17;
 
 struct Args {
     // grid
@@ -130,6 +132,7 @@ struct Args {
     double gx0, gx1, gy0, gy1, gz0, gz1;
     const double* box;           // octree
     const int* firstChild;
+    const signed char* splitDir;  // binary trees: split axis per node (null for octrees)
     const int* cellnumber;
     const int* nbrOffset;
     const int* nbrList;
@@ -206,6 +209,11 @@ struct __attribute__((aligned(16))) LeafEntry {
 constexpr int kLeafLevelShift = 27;
 constexpr unsigned kLeafCellMask = (1u << kLeafLevelShift) - 1u;
 constexpr int kMaxMapLevel = 9;  // 512^3 x 16 B = 2 GiB of HBM at most
+// k-d tree leaf map entries: cl = cell | (shift x | shift y << 3 | shift z << 6) << kBinCellBits, the
+// leaf's extent along each axis being 2^shift finest cells (binary trees split one axis at a time)
+constexpr int kBinCellBits = 23;
+constexpr unsigned kBinCellMask = (1u << kBinCellBits) - 1u;
+constexpr int kMaxBinMapLevel = 7;
 
 // Morton index of finest-level cell (x, y, z), 10 bits per axis: a ray's consecutive lookups mostly
 // hit the same or a neighbouring 2x2x2 block, i.e. the same 128-byte line
@@ -266,7 +274,7 @@ __device__ __forceinline__ Shared stageTables(const Args& a, double* lds, int pa
 
 template <int GRID>
 __device__ __forceinline__ constexpr int gridParts() {
-    return GRID == SKIRT_GRID_CARTESIAN ? STAGE_MESH : (GRID == SKIRT_GRID_OCTREE ? STAGE_TREE : 0);
+    return GRID == SKIRT_GRID_CARTESIAN ? STAGE_MESH : ((GRID == SKIRT_GRID_OCTREE || GRID == kBinTreeMap) ? STAGE_TREE : 0);
 }
 
 // The counters live in kStatCopies copies of one 64-byte line each (summed by the host): the waves of a
@@ -436,14 +444,20 @@ struct Grid<kOctreeNodes> {
         x0 = p.x; y0 = p.y; z0 = q.x; x1 = q.y; y1 = w.x; z1 = w.y;
     }
 
-    // TreeNode::whichnode from the root + OctTreeNode::child(r): the leaf containing (x,y,z) or -1
+    // TreeNode::whichnode from the root + OctTreeNode::child(r) / BinTreeNode::child(r)
+    // (BinTreeNode.cpp:322-331): the leaf containing (x,y,z) or -1
     __device__ static __forceinline__ int descend(const Args& a, double x, double y, double z) {
         if (!(x >= a.gx0 && x <= a.gx1 && y >= a.gy0 && y <= a.gy1 && z >= a.gz0 && z <= a.gz1)) return -1;
         int l = 0;
         int c0 = a.firstChild[0];
         while (c0 >= 0) {
             const double* cb = a.box + 6 * (size_t)c0 + 3;  // split point = rmax of child 0
-            l = c0 + (x < cb[0] ? 0 : 1) + (y < cb[1] ? 0 : 2) + (z < cb[2] ? 0 : 4);
+            if (a.splitDir) {
+                const int d = a.splitDir[l];
+                l = c0 + ((d == 0 ? x : d == 1 ? y : z) < cb[d] ? 0 : 1);
+            } else {
+                l = c0 + (x < cb[0] ? 0 : 1) + (y < cb[1] ? 0 : 2) + (z < cb[2] ? 0 : 4);
+            }
             c0 = a.firstChild[l];
         }
         return l;
@@ -571,9 +585,22 @@ struct Grid<kOctreeNodes> {
 //     lies exactly on a lower face of the leaf found, or that have not left the current leaf; those
 //     take the node-array search above. The walk is therefore the reference's, step for step.
 // The host builds the map only after checking every node box against the T tables.
-template <>
-struct Grid<SKIRT_GRID_OCTREE> {
+// A k-d tree (BinTreeNode::createchildren_splitdir also halves at the centre, one axis at a time) maps
+// the same way with per-axis leaf extents (BIN): its entries carry the three shifts instead of a level.
+template <bool BIN>
+struct LeafMapGrid {
     using Nodes = Grid<kOctreeNodes>;
+
+    // a leaf's extent along x, y, z in finest cells, as shifts
+    __device__ static __forceinline__ void shifts(const Args& a, unsigned cl, int& sx, int& sy, int& sz) {
+        if (BIN) {
+            const unsigned s = cl >> kBinCellBits;
+            sx = (int)(s & 7u); sy = (int)((s >> 3) & 7u); sz = (int)((s >> 6) & 7u);
+        } else {
+            sx = sy = sz = a.mapL - (int)(cl >> kLeafLevelShift);
+        }
+    }
+    __device__ static __forceinline__ int cellOf(unsigned cl) { return (int)(cl & (BIN ? kBinCellMask : kLeafCellMask)); }
 
     // finest-level index j with T[j] <= v < T[j+1] (the last cell also holds v == T[N]); v in [T[0], T[N]].
     // The split coordinates are uniform to rounding, so the estimate is off by one at most near a
@@ -612,14 +639,16 @@ struct Grid<SKIRT_GRID_OCTREE> {
         return e;
     }
 
+    // r.ck: the leaf's size in finest cells (octree) or its packed shifts (k-d tree)
     __device__ static __forceinline__ void enter(const Args& a, Ray& r, int fx, int fy, int fz, const LeafEntry& e) {
-        const int sh = a.mapL - (int)(e.cl >> kLeafLevelShift);
+        int sx, sy, sz;
+        shifts(a, e.cl, sx, sy, sz);
         r.ci = e.node;
-        r.cj = (int)(e.cl & kLeafCellMask);
-        r.ck = 1 << sh;
-        r.jx = (fx >> sh) << sh;
-        r.jy = (fy >> sh) << sh;
-        r.jz = (fz >> sh) << sh;
+        r.cj = cellOf(e.cl);
+        r.ck = BIN ? (int)(e.cl >> kBinCellBits) : 1 << sx;
+        r.jx = (fx >> sx) << sx;
+        r.jy = (fy >> sy) << sy;
+        r.jz = (fz >> sz) << sz;
         r.rho0 = e.rho0;
     }
 
@@ -643,10 +672,12 @@ struct Grid<SKIRT_GRID_OCTREE> {
         const double* tx = sh.mesh;
         const double* ty = tx + N1;
         const double* tz = ty + N1;
-        const int sz = r.ck;
-        const double xnext = tx[(r.dx < 0.0) ? r.jx : r.jx + sz];
-        const double ynext = ty[(r.dy < 0.0) ? r.jy : r.jy + sz];
-        const double znext = tz[(r.dz < 0.0) ? r.jz : r.jz + sz];
+        const int ex = BIN ? 1 << (r.ck & 7) : r.ck;
+        const int ey = BIN ? 1 << ((r.ck >> 3) & 7) : r.ck;
+        const int ez = BIN ? 1 << ((r.ck >> 6) & 7) : r.ck;
+        const double xnext = tx[(r.dx < 0.0) ? r.jx : r.jx + ex];
+        const double ynext = ty[(r.dy < 0.0) ? r.jy : r.jy + ey];
+        const double znext = tz[(r.dz < 0.0) ? r.jz : r.jz + ez];
         const double dsx = (r.ix != 0.0) ? (xnext - r.x) * r.ix : kDblMax;
         const double dsy = (r.iy != 0.0) ? (ynext - r.y) * r.iy : kDblMax;
         const double dsz = (r.iz != 0.0) ? (znext - r.z) * r.iz : kDblMax;
@@ -662,8 +693,9 @@ struct Grid<SKIRT_GRID_OCTREE> {
         if (!inside(a, x, y, z)) return false;  // no neighbour and no root descent contains it
         int fx, fy, fz;
         LeafEntry e = lookup(a, sh, x, y, z, fx, fy, fz);
-        const int lsh = a.mapL - (int)(e.cl >> kLeafLevelShift);
-        if (e.node == r.ci || x == tx[(fx >> lsh) << lsh] || y == ty[(fy >> lsh) << lsh] || z == tz[(fz >> lsh) << lsh]) {
+        int lx, ly, lz;
+        shifts(a, e.cl, lx, ly, lz);
+        if (e.node == r.ci || x == tx[(fx >> lx) << lx] || y == ty[(fy >> ly) << ly] || z == tz[(fz >> lz) << lz]) {
             // on a face, or not out of the current leaf: the reference's own search decides
             const int next = Nodes::nextNode(a, r.ci, wall, x, y, z, r.dx, r.dy, r.dz);
             if (next < 0) return false;
@@ -680,9 +712,14 @@ struct Grid<SKIRT_GRID_OCTREE> {
     __device__ static __forceinline__ int whichcell(const Args& a, const Shared& sh, double x, double y, double z) {
         if (!inside(a, x, y, z)) return -1;
         int fx, fy, fz;
-        return (int)(lookup(a, sh, x, y, z, fx, fy, fz).cl & kLeafCellMask);
+        return cellOf(lookup(a, sh, x, y, z, fx, fy, fz).cl);
     }
 };
+
+template <>
+struct Grid<SKIRT_GRID_OCTREE> : LeafMapGrid<false> {};
+template <>
+struct Grid<kBinTreeMap> : LeafMapGrid<true> {};
 
 // Voronoi grid: VoronoiMesh::path (VoronoiMesh.cpp:749-844), cellIndex (:512-541), with the
 // reference's arithmetic order (bisector plane through the midpoint, Vec::dot left to right)
@@ -1112,8 +1149,9 @@ __global__ void __launch_bounds__(kBlock) cellCdfKernel(const EmisArgs e) {
 }
 
 // fills the leaf map: one thread per finest-level cell descends the (checked) tree by its index bits
-__global__ void __launch_bounds__(kBlock) buildLeafMapKernel(LeafEntry* map, const int* firstChild, const int* cellnumber,
-                                                             const double* rho, int ncomp, int L) {
+// (a k-d tree by the bit of its split axis at that axis' depth)
+__global__ void __launch_bounds__(kBlock) buildLeafMapKernel(LeafEntry* map, const int* firstChild, const signed char* splitDir,
+                                                             const int* cellnumber, const double* rho, int ncomp, int L) {
     const unsigned long long n = 1ull << (3 * L);
     for (unsigned long long q = blockIdx.x * (unsigned long long)blockDim.x + threadIdx.x; q < n;
          q += (unsigned long long)gridDim.x * blockDim.x) {
@@ -1124,15 +1162,28 @@ __global__ void __launch_bounds__(kBlock) buildLeafMapKernel(LeafEntry* map, con
             fz |= (unsigned)((q >> (3 * b + 2)) & 1u) << b;
         }
         int node = 0, level = 0;
-        while (firstChild[node] >= 0) {
-            const int bit = L - 1 - level;
-            node = firstChild[node] + (int)((fx >> bit) & 1u) + 2 * (int)((fy >> bit) & 1u) + 4 * (int)((fz >> bit) & 1u);
-            level++;
+        LeafEntry e;
+        if (splitDir) {
+            int lv[3] = {0, 0, 0};
+            const unsigned f[3] = {fx, fy, fz};
+            while (firstChild[node] >= 0) {
+                const int d = splitDir[node];
+                const int bit = L - 1 - lv[d];
+                lv[d]++;
+                node = firstChild[node] + (int)((f[d] >> bit) & 1u);
+            }
+            e.cl = (unsigned)cellnumber[node] |
+                   ((unsigned)(L - lv[0]) | (unsigned)(L - lv[1]) << 3 | (unsigned)(L - lv[2]) << 6) << kBinCellBits;
+        } else {
+            while (firstChild[node] >= 0) {
+                const int bit = L - 1 - level;
+                node = firstChild[node] + (int)((fx >> bit) & 1u) + 2 * (int)((fy >> bit) & 1u) + 4 * (int)((fz >> bit) & 1u);
+                level++;
+            }
+            e.cl = (unsigned)cellnumber[node] | ((unsigned)level << kLeafLevelShift);
         }
         const int cell = cellnumber[node];
-        LeafEntry e;
         e.node = node;
-        e.cl = (unsigned)cell | ((unsigned)level << kLeafLevelShift);
         e.rho0 = rho[(size_t)cell * ncomp];
         map[q] = e;
     }
@@ -1787,6 +1838,8 @@ struct SkirtMcrt {
     double* dMesh = nullptr;
     double* dBox = nullptr;
     int *dFirstChild = nullptr, *dCellnumber = nullptr, *dNbrOffset = nullptr, *dNbrList = nullptr;
+    signed char* dSplitDir = nullptr;  // k-d tree split axes (null for octrees)
+    bool binTree = false;
     // Voronoi grid
     double *dSite = nullptr, *dCellBbox = nullptr;
     VoronoiNbr* dCellNbr = nullptr;
@@ -1798,6 +1851,7 @@ struct SkirtMcrt {
     double* dTreeT = nullptr;
     LeafEntry* dLeafMap = nullptr;
     bool mapReady = false;
+    int lastWalk = -1;  // SKIRT_WALK_* of the last run
     // device cell numbering: devCell[reference cell] (empty = identity). Octree cells are renumbered in
     // Morton (depth-first, children in octant order) order so that neighbouring cells share Labs lines;
     // rho is uploaded and Labs downloaded through it.
@@ -1912,9 +1966,11 @@ int planLeafMap(SkirtMcrt* c, const SkirtGridDesc* g) {
     if (c->dLeafMap) { (void)hipFree(c->dLeafMap); c->dLeafMap = nullptr; }
     const char* env = getenv("SKIRT_AMD_LEAFMAP");
     if (env && env[0] == '0') return SKIRT_OK;
-    if (g->ncells >= (int)(1u << kLeafLevelShift)) return SKIRT_OK;
-    struct Item { int node, level, ix, iy, iz; };
-    std::vector<Item> stack{{0, 0, 0, 0, 0}};
+    const bool bin = g->split_dir != nullptr;
+    if (g->ncells >= (int)(1u << (bin ? kBinCellBits : kLeafLevelShift))) return SKIRT_OK;
+    const int maxL = bin ? kMaxBinMapLevel : kMaxMapLevel;
+    struct Item { int node, lv[3], idx[3]; };  // per-axis depth and integer coordinate
+    std::vector<Item> stack{{0, {0, 0, 0}, {0, 0, 0}}};
     std::vector<Item> nodes;
     nodes.reserve(g->nnodes);
     int L = 0;
@@ -1922,12 +1978,30 @@ int planLeafMap(SkirtMcrt* c, const SkirtGridDesc* g) {
         const Item it = stack.back();
         stack.pop_back();
         nodes.push_back(it);
-        L = std::max(L, it.level);
-        if (L > kMaxMapLevel) return SKIRT_OK;
+        L = std::max(L, std::max(it.lv[0], std::max(it.lv[1], it.lv[2])));
+        if (L > maxL) return SKIRT_OK;
         const int fc = g->first_child[it.node];
-        if (fc >= 0)
-            for (int k = 0; k < 8; k++)
-                stack.push_back({fc + k, it.level + 1, 2 * it.ix + (k & 1), 2 * it.iy + ((k >> 1) & 1), 2 * it.iz + ((k >> 2) & 1)});
+        if (fc < 0) continue;
+        if (bin) {
+            const int d = g->split_dir[it.node];
+            for (int k = 0; k < 2; k++) {
+                Item ch = it;
+                ch.node = fc + k;
+                ch.lv[d]++;
+                ch.idx[d] = 2 * it.idx[d] + k;
+                stack.push_back(ch);
+            }
+        } else {
+            for (int k = 0; k < 8; k++) {
+                Item ch;
+                ch.node = fc + k;
+                for (int ax = 0; ax < 3; ax++) {
+                    ch.lv[ax] = it.lv[ax] + 1;
+                    ch.idx[ax] = 2 * it.idx[ax] + ((k >> ax) & 1);
+                }
+                stack.push_back(ch);
+            }
+        }
     }
     if ((int)nodes.size() != g->nnodes) return SKIRT_OK;  // not a tree reachable from node 0
     const int N = 1 << L;
@@ -1942,12 +2016,11 @@ int planLeafMap(SkirtMcrt* c, const SkirtGridDesc* g) {
             if (!(t[j] < t[j + 1])) return SKIRT_OK;
     }
     for (const Item& it : nodes) {
-        const int sh = L - it.level;
-        const int idx[3] = {it.ix, it.iy, it.iz};
         const double* b = g->box + 6 * (size_t)it.node;
         for (int ax = 0; ax < 3; ax++) {
+            const int sh = L - it.lv[ax];
             const double* t = T.data() + ax * (N + 1);
-            if (b[ax] != t[idx[ax] << sh] || b[3 + ax] != t[(idx[ax] + 1) << sh]) return SKIRT_OK;
+            if (b[ax] != t[it.idx[ax] << sh] || b[3 + ax] != t[(it.idx[ax] + 1) << sh]) return SKIRT_OK;
         }
     }
     int rc = upload(c, c->dTreeT, T.data(), T.size());
@@ -1964,7 +2037,7 @@ int ensureLeafMap(SkirtMcrt* c) {
     if (!c->dLeafMap) HIPCHECK(c, hipMalloc(&c->dLeafMap, n * sizeof(LeafEntry)));
     const int blocks = (int)std::min<size_t>((n + kBlock - 1) / kBlock, 65536);
     hipLaunchKernelGGL(buildLeafMapKernel, dim3(blocks), dim3(kBlock), 0, c->stream, c->dLeafMap, c->dFirstChild,
-                       c->dCellnumber, c->dRho, std::max(1, c->ncomp), c->mapL);
+                       c->binTree ? c->dSplitDir : nullptr, c->dCellnumber, c->dRho, std::max(1, c->ncomp), c->mapL);
     HIPCHECK(c, hipGetLastError());
     c->mapReady = true;
     return SKIRT_OK;
@@ -2043,10 +2116,13 @@ int skirt_mcrt_upload_grid(SkirtMcrt* c, const SkirtGridDesc* g) {
         if (g->nnodes < 1 || !g->box || !g->first_child || !g->cellnumber || !g->nbr_offset)
             return fail(c, SKIRT_ERR_ARG, "bad octree grid");
         // validate the index arrays so that the kernels never read out of bounds
+        const bool bin = g->split_dir != nullptr;
+        const int arity = bin ? 2 : 8;
         int nleaf = 0;
         for (int l = 0; l < g->nnodes; l++) {
             const int fc = g->first_child[l];
-            if (fc >= 0 && (fc + 8 > g->nnodes || fc <= l)) return fail(c, SKIRT_ERR_ARG, "octree child index out of range");
+            if (fc >= 0 && (fc + arity > g->nnodes || fc <= l)) return fail(c, SKIRT_ERR_ARG, "octree child index out of range");
+            if (fc >= 0 && bin && (g->split_dir[l] < 0 || g->split_dir[l] > 2)) return fail(c, SKIRT_ERR_ARG, "bad k-d tree split axis");
             if (fc < 0) {
                 if (g->cellnumber[l] < 0 || g->cellnumber[l] >= g->ncells) return fail(c, SKIRT_ERR_ARG, "octree cell number out of range");
                 nleaf++;
@@ -2066,6 +2142,13 @@ int skirt_mcrt_upload_grid(SkirtMcrt* c, const SkirtGridDesc* g) {
         int rc;
         if ((rc = upload(c, c->dBox, g->box, 6 * (size_t)g->nnodes))) return rc;
         if ((rc = upload(c, c->dFirstChild, g->first_child, (size_t)g->nnodes))) return rc;
+        c->binTree = bin;
+        if (bin) {
+            std::vector<signed char> dirs(g->split_dir, g->split_dir + g->nnodes);
+            for (int l = 0; l < g->nnodes; l++)
+                if (g->first_child[l] < 0) dirs[l] = 0;
+            if ((rc = upload(c, c->dSplitDir, dirs.data(), dirs.size()))) return rc;
+        }
         // Morton order of the leaves: depth-first, children in octant order (x, y, z bits)
         c->devCell.assign(g->ncells, -1);
         {
@@ -2079,7 +2162,7 @@ int skirt_mcrt_upload_grid(SkirtMcrt* c, const SkirtGridDesc* g) {
                     if (c->devCell[g->cellnumber[l]] >= 0) return fail(c, SKIRT_ERR_ARG, "octree cell number used twice");
                     c->devCell[g->cellnumber[l]] = next++;
                 } else {
-                    for (int k = 7; k >= 0; k--) stack.push_back(fc + k);
+                    for (int k = arity - 1; k >= 0; k--) stack.push_back(fc + k);
                 }
             }
             if (next != g->ncells) return fail(c, SKIRT_ERR_ARG, "octree leaves do not cover the cells");
@@ -2519,6 +2602,7 @@ int skirt_mcrt_run_phase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, 
     a.mesh = c->dMesh;
     a.gx0 = c->gx0; a.gx1 = c->gx1; a.gy0 = c->gy0; a.gy1 = c->gy1; a.gz0 = c->gz0; a.gz1 = c->gz1;
     a.box = c->dBox; a.firstChild = c->dFirstChild; a.cellnumber = c->dCellnumber;
+    a.splitDir = c->binTree ? c->dSplitDir : nullptr;
     a.nbrOffset = c->dNbrOffset; a.nbrList = c->dNbrList; a.eps = c->eps; a.search = c->search;
     a.site = c->dSite; a.cellNbrOffset = c->dCellNbrOffset; a.cellNbr = c->dCellNbr; a.cellBbox = c->dCellBbox;
     a.devCell = c->dDevCell;
@@ -2573,12 +2657,18 @@ int skirt_mcrt_run_phase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, 
     if (lds > 64 * 1024) return fail(c, SKIRT_ERR_UNSUPPORTED, "tables do not fit in LDS (" + std::to_string(lds) + " bytes)");
     const int kind = c->gridKind == SKIRT_GRID_CARTESIAN ? SKIRT_GRID_CARTESIAN
                      : c->gridKind == SKIRT_GRID_VORONOI ? SKIRT_GRID_VORONOI
-                     : (leafMap ? SKIRT_GRID_OCTREE : kOctreeNodes);
+                     : (leafMap ? (c->binTree ? kBinTreeMap : SKIRT_GRID_OCTREE) : kOctreeNodes);
+    c->lastWalk = kind == SKIRT_GRID_CARTESIAN ? SKIRT_WALK_CARTESIAN
+                  : kind == SKIRT_GRID_OCTREE  ? SKIRT_WALK_OCTREE_MAP
+                  : kind == kBinTreeMap        ? SKIRT_WALK_KDTREE_MAP
+                  : kind == SKIRT_GRID_VORONOI ? SKIRT_WALK_VORONOI
+                                               : SKIRT_WALK_TREE_NODES;
     const bool one = a.ncomp == 1;
     const void* traceFn = nullptr;
     auto pick = [&](auto fn1, auto fnN) { traceFn = one ? (const void*)fn1 : (const void*)fnN; };
     if (kind == SKIRT_GRID_CARTESIAN) pick(traceKernel<SKIRT_GRID_CARTESIAN, true>, traceKernel<SKIRT_GRID_CARTESIAN, false>);
     else if (kind == SKIRT_GRID_OCTREE) pick(traceKernel<SKIRT_GRID_OCTREE, true>, traceKernel<SKIRT_GRID_OCTREE, false>);
+    else if (kind == kBinTreeMap) pick(traceKernel<kBinTreeMap, true>, traceKernel<kBinTreeMap, false>);
     else if (kind == SKIRT_GRID_VORONOI) pick(traceKernel<SKIRT_GRID_VORONOI, true>, traceKernel<SKIRT_GRID_VORONOI, false>);
     else pick(traceKernel<kOctreeNodes, true>, traceKernel<kOctreeNodes, false>);
     int tgrid = c->traceGrid;
@@ -2602,6 +2692,7 @@ int skirt_mcrt_run_phase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, 
 #define SKIRT_EVENT(G, O) hipLaunchKernelGGL((eventKernel<G, O>), dim3(egrid), dim3(kBlock), ldsEvent, st, aa)
         if (kind == SKIRT_GRID_CARTESIAN) { if (one) SKIRT_EVENT(SKIRT_GRID_CARTESIAN, true); else SKIRT_EVENT(SKIRT_GRID_CARTESIAN, false); }
         else if (kind == SKIRT_GRID_OCTREE) { if (one) SKIRT_EVENT(SKIRT_GRID_OCTREE, true); else SKIRT_EVENT(SKIRT_GRID_OCTREE, false); }
+        else if (kind == kBinTreeMap) { if (one) SKIRT_EVENT(kBinTreeMap, true); else SKIRT_EVENT(kBinTreeMap, false); }
         else if (kind == SKIRT_GRID_VORONOI) { if (one) SKIRT_EVENT(SKIRT_GRID_VORONOI, true); else SKIRT_EVENT(SKIRT_GRID_VORONOI, false); }
         else { if (one) SKIRT_EVENT(kOctreeNodes, true); else SKIRT_EVENT(kOctreeNodes, false); }
 #undef SKIRT_EVENT
@@ -2610,6 +2701,7 @@ int skirt_mcrt_run_phase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, 
 #define SKIRT_TRACE(G, O) hipLaunchKernelGGL((traceKernel<G, O>), dim3(tgrid), dim3(kBlock), ldsTrace, st, aa)
         if (kind == SKIRT_GRID_CARTESIAN) { if (one) SKIRT_TRACE(SKIRT_GRID_CARTESIAN, true); else SKIRT_TRACE(SKIRT_GRID_CARTESIAN, false); }
         else if (kind == SKIRT_GRID_OCTREE) { if (one) SKIRT_TRACE(SKIRT_GRID_OCTREE, true); else SKIRT_TRACE(SKIRT_GRID_OCTREE, false); }
+        else if (kind == kBinTreeMap) { if (one) SKIRT_TRACE(kBinTreeMap, true); else SKIRT_TRACE(kBinTreeMap, false); }
         else if (kind == SKIRT_GRID_VORONOI) { if (one) SKIRT_TRACE(SKIRT_GRID_VORONOI, true); else SKIRT_TRACE(SKIRT_GRID_VORONOI, false); }
         else { if (one) SKIRT_TRACE(kOctreeNodes, true); else SKIRT_TRACE(kOctreeNodes, false); }
 #undef SKIRT_TRACE
@@ -2750,6 +2842,8 @@ int skirt_mcrt_stats(SkirtMcrt* c, SkirtStats* out) {
     out->kernel_ms = c->lastMs;
     out->trace_ms = c->traceMs;
     out->trace_launches = c->traceLaunchesTotal;
+    out->grid_walk = c->lastWalk;
+    out->map_level = c->mapL;
     return SKIRT_OK;
 }
 
@@ -2759,7 +2853,7 @@ void skirt_mcrt_destroy(SkirtMcrt* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    void* bufs[] = {c->dMesh, c->dBox, c->dFirstChild, c->dCellnumber, c->dNbrOffset, c->dNbrList, c->dTreeT,
+    void* bufs[] = {c->dMesh, c->dBox, c->dFirstChild, c->dSplitDir, c->dCellnumber, c->dNbrOffset, c->dNbrList, c->dTreeT,
                     c->dLeafMap, c->dCellLv, c->dCellCdf, c->dCellLtot, c->dCellNode, c->dEmisVolume, c->dEmisKabs,
                     c->dEmisSigma, c->dEmisMu, c->dEmisTv, c->dEmisPlanck, c->dEmisLambda, c->dEmisDlambda,
                     c->dEmisScratch, c->dDevCell, c->dSite, c->dCellBbox, c->dCellNbrOffset, c->dCellNbr,

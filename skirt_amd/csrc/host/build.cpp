@@ -8,6 +8,7 @@
 // caller's UniformSource so that a single-threaded reference run and this setup produce bit-identical
 // densities and trees.
 #include <algorithm>
+#include <array>
 #include <atomic>
 #include <chrono>
 #include <cmath>
@@ -236,11 +237,7 @@ int DustGrid::whichcell(double x, double y, double z) const {
     const double* b = &tree.box[0];
     if (!(x >= b[0] && x <= b[3] && y >= b[1] && y <= b[4] && z >= b[2] && z <= b[5])) return -1;
     int l = 0;
-    while (tree.firstChild[l] >= 0) {
-        int c0 = tree.firstChild[l];
-        const double* cb = &tree.box[6 * (size_t)c0];
-        l = c0 + (x < cb[3] ? 0 : 1) + (y < cb[4] ? 0 : 2) + (z < cb[5] ? 0 : 4);
-    }
+    while (tree.firstChild[l] >= 0) l = tree.child(l, x, y, z);
     return tree.cellnumber[l];
 }
 
@@ -519,14 +516,15 @@ struct TreeBuilder {
         t.firstChild.push_back(-1);
         t.father.push_back(father);
         t.level.push_back(father >= 0 ? t.level[father] + 1 : 0);
+        if (t.binary) t.dir.push_back(-1);
         return id;
     }
 
-    void createChildren(int l) {
-        // OctTreeNode::createchildren -> createchildren_splitpoint(id, center())
+    // OctTreeNode::createchildren_splitpoint (OctTreeNode.cpp:38-49): the box centre for
+    // OctTreeNode::createchildren, the sampled barycentre for BaryOctTreeNode::createchildren
+    void createChildren(int l, double rx, double ry, double rz) {
         double b[6];
         std::memcpy(b, box(l), sizeof b);
-        double rx = 0.5 * (b[0] + b[3]), ry = 0.5 * (b[1] + b[4]), rz = 0.5 * (b[2] + b[5]);
         int first = (int)t.firstChild.size();
         t.firstChild[l] = first;
         addNode(l, b[0], b[1], b[2], rx, ry, rz);
@@ -537,6 +535,22 @@ struct TreeBuilder {
         addNode(l, rx, b[1], rz, b[3], ry, b[5]);
         addNode(l, b[0], ry, rz, rx, b[4], b[5]);
         addNode(l, rx, ry, rz, b[3], b[4], b[5]);
+    }
+
+    // BinTreeNode::createchildren_splitdir (BinTreeNode.cpp:38-66): halves along one axis, child 0 below
+    void createChildrenBin(int l, int d) {
+        double b[6];
+        std::memcpy(b, box(l), sizeof b);
+        t.firstChild[l] = (int)t.firstChild.size();
+        t.dir[l] = (signed char)d;
+        double hi[6], lo[6];
+        std::memcpy(lo, b, sizeof b);
+        std::memcpy(hi, b, sizeof b);
+        const double c = 0.5 * (b[d] + b[3 + d]);
+        lo[3 + d] = c;
+        hi[d] = c;
+        addNode(l, lo[0], lo[1], lo[2], lo[3], lo[4], lo[5]);
+        addNode(l, hi[0], hi[1], hi[2], hi[3], hi[4], hi[5]);
     }
 
     void ensure(int l) {
@@ -645,6 +659,35 @@ struct TreeBuilder {
         }
     }
 
+    // BinTreeNode::addneighbors (BinTreeNode.cpp:80-318): the two children become each other's neighbours
+    // across the split wall; every neighbour of the node across the two walls perpendicular to the split
+    // axis takes the child on its side, every other neighbour each child its extent along the axis
+    // reaches. Walls visited in the reference's order BACK FRONT LEFT RIGHT BOTTOM TOP.
+    void addneighborsBin(int l) {
+        if (t.firstChild[l] < 0) return;
+        static const int complementing[] = {FRONT, BACK, RIGHT, LEFT, TOP, BOTTOM};
+        const int C0 = t.firstChild[l], C1 = C0 + 1, d = t.dir[l];
+        const int lowWall = 2 * d, highWall = 2 * d + 1;
+        ensure(l);
+        ensure(C0);
+        ensure(C1);
+        const double c = box(C0)[3 + d];
+        makeneighbors(highWall, C0, C1);
+        for (int wall = BACK; wall <= TOP; wall++) {
+            const int opp = complementing[wall];
+            std::vector<int> ns = lst(l, wall);
+            for (int n : ns) {
+                deleteneighbor(n, opp, l);
+                if (wall == lowWall) makeneighbors(opp, n, C0);
+                else if (wall == highWall) makeneighbors(opp, n, C1);
+                else {
+                    if (box(n)[d] <= c) makeneighbors(opp, n, C0);
+                    if (box(n)[3 + d] >= c) makeneighbors(opp, n, C1);
+                }
+            }
+        }
+    }
+
     // TreeNode::sortneighbors with the LargerOverlap functor (TreeNode.cpp:98-140)
     void sortneighbors(int l) {
         if (!hasLists[l]) return;
@@ -670,7 +713,9 @@ struct TreeBuilder {
     }
 };
 
-void buildOctree(const Ctx& c, const XmlElement* e, const Model& model, OctreeGrid& t) {
+// OctTreeDustGrid (binary = false) or BinTreeDustGrid (binary = true)
+void buildOctree(const Ctx& c, const XmlElement* e, const Model& model, OctreeGrid& t, bool binary) {
+    t.binary = binary;
     t.xmin = attr(c, e, "minX", "length", 0);
     t.xmax = attr(c, e, "maxX", "length", 0);
     t.ymin = attr(c, e, "minY", "length", 0);
@@ -686,8 +731,20 @@ void buildOctree(const Ctx& c, const XmlElement* e, const Model& model, OctreeGr
     double maxOpticalDepth = attr(c, e, "maxOpticalDepth", "", 0);
     double maxMassFraction = attr(c, e, "maxMassFraction", "", 1e-6);
     double maxDensDispFraction = attr(c, e, "maxDensDispFraction", "", 0);
-    if (attrBool(e, "barycentric", false)) throw std::runtime_error("barycentric octree subdivision is not supported");
-    if (t.minLevel < 0 || t.maxLevel < 2 || t.maxLevel <= t.minLevel) throw std::runtime_error("invalid tree levels");
+    // OctTreeDustGrid::barycentric (BaryOctTreeNode) / BinTreeDustGrid::directionMethod (BaryBinTreeNode)
+    bool bary;
+    if (binary) {
+        const std::string method = e->get("directionMethod", "Alternating");
+        if (method != "Alternating" && method != "Barycenter") throw std::runtime_error("unknown direction method " + method);
+        bary = method == "Barycenter";
+        if (t.search == 2) throw std::runtime_error("Bookkeeping method is not compatible with binary tree");  // BinTreeDustGrid.cpp:23-24
+    } else {
+        bary = attrBool(e, "barycentric", false);
+    }
+    if (t.minLevel < 0) throw std::runtime_error("The minimum tree level should be at least 0");
+    if (t.maxLevel < 2) throw std::runtime_error("The maximum tree level should be at least 2");
+    if (t.maxLevel <= t.minLevel) throw std::runtime_error("Maximum tree level should be larger than minimum tree level");
+    if (Nrandom < 1) throw std::runtime_error("Number of random samples must be at least 1");
 
     double wx = t.xmax - t.xmin, wy = t.ymax - t.ymin, wz = t.zmax - t.zmin;
     t.eps = 1e-12 * std::sqrt(wx * wx + wy * wy + wz * wz);
@@ -707,6 +764,7 @@ void buildOctree(const Ctx& c, const XmlElement* e, const Model& model, OctreeGr
         for (size_t l = l0; l < l1; l++)
             if (t.level[l] > t.minLevel && t.level[l] < t.maxLevel) sampled.push_back((int)l);
         std::vector<char> divide(l1 - l0, 0);
+        std::vector<std::array<double, 3>> bc(bary ? l1 - l0 : 0);  // sampled barycentres
         for (size_t l = l0; l < l1; l++) divide[l - l0] = t.level[l] <= t.minLevel;
         parallelDraws(*c.rng, sampled.size(), 3 * Nrandom, [&](size_t q, const double* u) {
             // TreeNodeSampleDensityCalculator: Nrandom positions in the node, density of all components
@@ -714,13 +772,19 @@ void buildOctree(const Ctx& c, const XmlElement* e, const Model& model, OctreeGr
             double b[6];
             std::memcpy(b, tb.box(l), sizeof b);
             std::vector<double> rhov(Nrandom);
+            double sumrho = 0, sx = 0, sy = 0, sz = 0;  // TreeNodeSampleDensityCalculator::barycenter
             for (int n = 0; n < Nrandom; n++) {
                 double fx = u[3 * n], fy = u[3 * n + 1], fz = u[3 * n + 2];
                 double x = b[0] + fx * (b[3] - b[0]), y = b[1] + fy * (b[4] - b[1]), z = b[2] + fz * (b[5] - b[2]);
                 double rho = 0;
                 for (auto& d : model.dust) rho += d.density(x, y, z);
                 rhov[n] = rho;
+                sumrho += rho;
+                sx += rho * x;
+                sy += rho * y;
+                sz += rho * z;
             }
+            if (bary) bc[l - l0] = {sx / sumrho, sy / sumrho, sz / sumrho};
             double vol = (b[3] - b[0]) * (b[4] - b[1]) * (b[5] - b[2]);
             double mass = nr::sum(rhov) / Nrandom * vol;
             bool needDivision = always;
@@ -736,8 +800,31 @@ void buildOctree(const Ctx& c, const XmlElement* e, const Model& model, OctreeGr
             }
             divide[l - l0] = needDivision;
         });
-        for (size_t l = l0; l < l1; l++)
-            if (divide[l - l0]) tb.createChildren((int)l);
+        for (size_t l = l0; l < l1; l++) {
+            if (!divide[l - l0]) continue;
+            const double* b = tb.box((int)l);
+            // at or below minLevel the node is split without a density calculator (TreeDustGrid.cpp:174-178)
+            const bool useBary = bary && t.level[l] > t.minLevel;
+            if (binary) {
+                int d = t.level[l] % 3;  // BinTreeNode::createchildren: alternating x, y, z
+                if (useBary) {
+                    // BaryBinTreeNode::createchildren: the axis whose wall is nearest (relatively) to the
+                    // barycentre; NaN distances (no mass sampled) fall through to z as in the reference
+                    const auto& r = bc[l - l0];
+                    double dx = std::min(r[0] - b[0], b[3] - r[0]) / (b[3] - b[0]);
+                    double dy = std::min(r[1] - b[1], b[4] - r[1]) / (b[4] - b[1]);
+                    double dz = std::min(r[2] - b[2], b[5] - r[2]) / (b[5] - b[2]);
+                    if (dx < dy) d = dx < dz ? 0 : 2;
+                    else d = dy < dz ? 1 : 2;
+                }
+                tb.createChildrenBin((int)l, d);
+            } else if (useBary) {
+                const auto& r = bc[l - l0];
+                tb.createChildren((int)l, r[0], r[1], r[2]);
+            } else {
+                tb.createChildren((int)l, 0.5 * (b[0] + b[3]), 0.5 * (b[1] + b[4]), 0.5 * (b[2] + b[5]));
+            }
+        }
         l0 = l1;
     }
     int Nnodes = t.nnodes();
@@ -751,7 +838,10 @@ void buildOctree(const Ctx& c, const XmlElement* e, const Model& model, OctreeGr
     // neighbor lists (always built: the device engine uses them whatever the search method)
     tb.hasLists.assign(Nnodes, 0);
     tb.nb.assign(6 * (size_t)Nnodes, {});
-    for (int l = 0; l < Nnodes; l++) tb.addneighbors(l);
+    for (int l = 0; l < Nnodes; l++) {
+        if (binary) tb.addneighborsBin(l);
+        else tb.addneighbors(l);
+    }
     for (int l = 0; l < Nnodes; l++) tb.sortneighbors(l);
     t.nbrOffset.assign(6 * (size_t)Nnodes + 1, 0);
     size_t total = 0;
@@ -1014,10 +1104,10 @@ Model loadSki(const std::string& path, UniformSource& rng, const std::string& da
             mesh("meshY", g.Ny, g.yv, g.ymin, g.ymax);
             mesh("meshZ", g.Nz, g.zv, g.zmin, g.zmax);
             m.grid.ncells = g.Nx * g.Ny * g.Nz;
-        } else if (ge->name == "OctTreeDustGrid") {
+        } else if (ge->name == "OctTreeDustGrid" || ge->name == "BinTreeDustGrid") {
             m.grid.kind = GridKind::Octree;
             StageTimer st("octree");
-            buildOctree(c, ge, m, m.grid.tree);
+            buildOctree(c, ge, m, m.grid.tree, ge->name == "BinTreeDustGrid");
             m.grid.ncells = (int)m.grid.tree.idv.size();
         } else if (ge->name == "VoronoiDustGrid") {
             m.grid.kind = GridKind::Voronoi;

@@ -62,8 +62,10 @@ struct CartesianGrid {
     std::vector<double> xv, yv, zv;  // N+1 borders each
 };
 
-// Octree grid: SKIRTcore/TreeDustGrid.cpp + OctTreeNode.cpp, flattened breadth-first exactly as the
-// reference's _tree vector: node l has children firstChild[l] .. firstChild[l]+7 (or -1 for a leaf).
+// Tree grids: SKIRTcore/TreeDustGrid.cpp with OctTreeNode.cpp / BaryOctTreeNode.cpp (OctTreeDustGrid) or
+// BinTreeNode.cpp / BaryBinTreeNode.cpp (BinTreeDustGrid, the k-d tree), flattened breadth-first exactly
+// as the reference's _tree vector: node l has children firstChild[l] .. firstChild[l]+7 (octree) or
+// firstChild[l] .. firstChild[l]+1 (binary tree), or -1 for a leaf.
 struct OctreeGrid {
     double xmin = 0, xmax = 0, ymin = 0, ymax = 0, zmin = 0, zmax = 0;
     double eps = 0;  // 1e-12 * |extent widths| (TreeDustGrid.cpp:76)
@@ -78,7 +80,20 @@ struct OctreeGrid {
     // neighbor lists per (node, wall), walls ordered BACK FRONT LEFT RIGHT BOTTOM TOP (TreeNode.hpp)
     std::vector<int> nbrOffset;   // 6*Nnodes+1
     std::vector<int> nbrList;
+    bool binary = false;              // BinTreeDustGrid: two children per node
+    std::vector<signed char> dir;     // binary trees: split axis per node (0 x, 1 y, 2 z; -1 for leaves)
     int nnodes() const { return (int)firstChild.size(); }
+    // the child of non-leaf node l holding (x,y,z): OctTreeNode::child(r) (OctTreeNode.cpp:184-189) or
+    // BinTreeNode::child(r) (BinTreeNode.cpp:322-331); both compare with the first child's upper corner
+    int child(int l, double x, double y, double z) const {
+        const int c0 = firstChild[l];
+        const double* cb = &box[6 * (size_t)c0];
+        if (binary) {
+            const int d = dir[l];
+            return c0 + ((d == 0 ? x : d == 1 ? y : z) < cb[3 + d] ? 0 : 1);
+        }
+        return c0 + (x < cb[3] ? 0 : 1) + (y < cb[4] ? 0 : 2) + (z < cb[5] ? 0 : 4);
+    }
 };
 
 enum class GridKind : int { Cartesian = 0, Octree = 1, Voronoi = 2 };

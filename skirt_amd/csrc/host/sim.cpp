@@ -140,6 +140,7 @@ int skirt_sim_attach(SkirtSim* s, int device) {
             g.nnodes = t.nnodes();
             g.box = t.box.data();
             g.first_child = t.firstChild.data();
+            g.split_dir = t.binary ? t.dir.data() : nullptr;
             g.cellnumber = t.cellnumber.data();
             g.nbr_offset = t.nbrOffset.data();
             g.nbr_list = t.nbrList.data();

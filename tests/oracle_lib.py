@@ -102,3 +102,25 @@ def philox(ctr, key):
     o = (ctypes.c_uint32 * 4)()
     L.oracle_philox4x32_10(c, k, o)
     return list(o)
+
+
+def grid_paths(ski, rays, maxseg=4096):
+    """DustGrid::path of the ski's dust grid for rays [n, 6] (position, direction): a list of
+    (boxes [nseg, 6] (NaN rows before the grid), ds [nseg]) per ray, and the grid's cell count."""
+    L = lib()
+    L.oracle_grid_paths.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int,
+                                    ctypes.POINTER(ctypes.c_double), ctypes.c_int,
+                                    ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int),
+                                    ctypes.POINTER(ctypes.c_int)]
+    rays = np.ascontiguousarray(rays, dtype=np.float64)
+    n = rays.shape[0]
+    out = np.zeros((n, maxseg, 7))
+    nseg = np.zeros(n, dtype=np.int32)
+    nc = ctypes.c_int()
+    rc = L.oracle_grid_paths(ski.encode(), DATA_DIR.encode(), n,
+                             rays.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), maxseg,
+                             out.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
+                             nseg.ctypes.data_as(ctypes.POINTER(ctypes.c_int)), ctypes.byref(nc))
+    if rc:
+        raise RuntimeError("oracle failed: " + L.oracle_last_error().decode())
+    return [(out[i, :nseg[i], :6], out[i, :nseg[i], 6]) for i in range(n)], nc.value

@@ -32,13 +32,13 @@ def test_library_exports_every_declared_function():
 
 
 def test_abi_version_and_stats_layout():
-    assert S.lib().skirt_mcrt_abi_version() == 4
+    assert S.lib().skirt_mcrt_abi_version() == 5
     text = open(HEADERS[0]).read()
     body = re.search(r"typedef struct \{([^}]*)\} SkirtStats;", text, flags=re.S).group(1)
     body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
-    fields = re.findall(r"(uint64_t|double)\s+(\w+);", body)
+    fields = re.findall(r"(uint64_t|int32_t|double)\s+(\w+);", body)
     assert [n for _, n in fields] == [n for n, _ in S.SkirtStats._fields_]
-    size = {"uint64_t": 8, "double": 8}
+    size = {"uint64_t": 8, "int32_t": 4, "double": 8}
     assert ctypes.sizeof(S.SkirtStats) == sum(size[t] for t, _ in fields)
 
 

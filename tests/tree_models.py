@@ -1,0 +1,55 @@
+"""Tree-grid variants of the golden models, written as .ski files for the tree tests.
+
+The reference fixtures cover the OctTreeDustGrid with centre splits and the Neighbor search
+(pan_oct). Its other tree grids -- BinTreeDustGrid (the k-d tree, Alternating or Barycenter split
+directions, BinTreeDustGrid.cpp, BinTreeNode.cpp, BaryBinTreeNode.cpp), barycentric octrees
+(BaryOctTreeNode.cpp) and the TopDown search -- have no reference outputs here (the reference binary
+cannot be built or run in this repository), so these variants swap only the <dustGrid> element of a
+pinned model and are checked against the pinned octree walk (geometric equivalence) and against the
+oracle on the same random streams.
+"""
+import os
+import re
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "ski")
+BOX = 'minX="-500 pc" maxX="500 pc" minY="-500 pc" maxY="500 pc" minZ="-500 pc" maxZ="500 pc"'
+
+GRIDS = {
+    # full trees: every node is split down to maxLevel, so the octree of level 4 and the k-d tree of
+    # level 12 have the same 4096 leaf boxes (16^3)
+    "oct_full": ("c1_oligo16", '<OctTreeDustGrid writeGrid="false" %s minLevel="1" maxLevel="4" searchMethod="Neighbor" '
+                 'sampleCount="10" maxOpticalDepth="0" maxMassFraction="0" maxDensDispFraction="0" barycentric="false"/>'),
+    "bin_full": ("c1_oligo16", '<BinTreeDustGrid writeGrid="false" %s minLevel="3" maxLevel="12" searchMethod="Neighbor" '
+                 'sampleCount="10" maxOpticalDepth="0" maxMassFraction="0" maxDensDispFraction="0" '
+                 'directionMethod="Alternating"/>'),
+    "bin_full_td": ("c1_oligo16", '<BinTreeDustGrid writeGrid="false" %s minLevel="3" maxLevel="12" searchMethod="TopDown" '
+                    'sampleCount="10" maxOpticalDepth="0" maxMassFraction="0" maxDensDispFraction="0" '
+                    'directionMethod="Alternating"/>'),
+    # adaptive trees on the Pan model of the pan_oct fixture
+    "bin_pan": ("pan_oct", '<BinTreeDustGrid writeGrid="false" %s minLevel="6" maxLevel="18" searchMethod="Neighbor" '
+                'sampleCount="100" maxOpticalDepth="0" maxMassFraction="5e-4" maxDensDispFraction="0" '
+                'directionMethod="Alternating"/>'),
+    "bin_pan_td": ("pan_oct", '<BinTreeDustGrid writeGrid="false" %s minLevel="6" maxLevel="18" searchMethod="TopDown" '
+                   'sampleCount="100" maxOpticalDepth="0" maxMassFraction="5e-4" maxDensDispFraction="0" '
+                   'directionMethod="Alternating"/>'),
+    "bin_bary": ("pan_oct", '<BinTreeDustGrid writeGrid="false" %s minLevel="3" maxLevel="18" searchMethod="Neighbor" '
+                 'sampleCount="100" maxOpticalDepth="0" maxMassFraction="5e-4" maxDensDispFraction="0" '
+                 'directionMethod="Barycenter"/>'),
+    "oct_bary": ("pan_oct", '<OctTreeDustGrid writeGrid="false" %s minLevel="1" maxLevel="6" searchMethod="Neighbor" '
+                 'sampleCount="100" maxOpticalDepth="0" maxMassFraction="5e-4" maxDensDispFraction="0" barycentric="true"/>'),
+    "oct_pan_td": ("pan_oct", '<OctTreeDustGrid writeGrid="false" %s minLevel="2" maxLevel="6" searchMethod="TopDown" '
+                   'sampleCount="100" maxOpticalDepth="0" maxMassFraction="5e-4" maxDensDispFraction="0" barycentric="false"/>'),
+}
+
+
+def write(name, directory):
+    """Writes variant `name` into `directory` and returns its path."""
+    base, grid = GRIDS[name]
+    text = open(os.path.join(GOLD, base + ".ski")).read()
+    text, n = re.subn(r'<dustGrid type="DustGrid">.*?</dustGrid>',
+                      '<dustGrid type="DustGrid">%s</dustGrid>' % (grid % BOX), text, flags=re.S)
+    assert n == 1, name
+    path = os.path.join(directory, name + ".ski")
+    with open(path, "w") as f:
+        f.write(text)
+    return path
