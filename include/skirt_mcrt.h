@@ -43,7 +43,7 @@ enum {
 };
 
 enum { SKIRT_GRID_CARTESIAN = 0, SKIRT_GRID_OCTREE = 1, SKIRT_GRID_VORONOI = 2 };
-enum { SKIRT_TREE_TOPDOWN = 0, SKIRT_TREE_NEIGHBOR = 1 };
+enum { SKIRT_TREE_TOPDOWN = 0, SKIRT_TREE_NEIGHBOR = 1, SKIRT_TREE_BOOKKEEPING = 2 /* octrees only */ };
 enum { SKIRT_GEOM_PLUMMER = 0 };
 enum { SKIRT_INSTR_FULL = 0, SKIRT_INSTR_SIMPLE = 1, SKIRT_INSTR_SED = 2, SKIRT_INSTR_FRAME = 3 };
 enum { SKIRT_PHASE_STELLAR = 0, SKIRT_PHASE_DUST_EMISSION = 1, SKIRT_PHASE_DUST_SELFABS = 2 };
@@ -175,7 +175,7 @@ typedef struct {
 
 /* grid walks of the trace kernel (SkirtStats::grid_walk) */
 enum { SKIRT_WALK_CARTESIAN = 0, SKIRT_WALK_OCTREE_MAP = 1, SKIRT_WALK_VORONOI = 2, SKIRT_WALK_TREE_NODES = 3,
-       SKIRT_WALK_KDTREE_MAP = 4 };
+       SKIRT_WALK_KDTREE_MAP = 4, SKIRT_WALK_OCTREE_BOOKKEEPING = 5 };
 
 int skirt_mcrt_abi_version(void);
 int skirt_mcrt_create(int device, SkirtMcrt** out);

@@ -305,6 +305,76 @@ int rootWhichnode(const OctreeGrid& t, double x, double y, double z) {
     return l;
 }
 
+// TreeDustGrid::path, Bookkeeping search (TreeDustGrid.cpp:523-659): octrees only; the next node comes
+// from the breadth-first numbering (children of a node are 8 consecutive ids in octant order, so
+// (l-1) % 8 is a node's octant): climb while the node lies on the far side of its father, step to the
+// sibling across the wall, descend with "<=" to the leaf holding the exit point. No eps nudge: the
+// position is put on the crossed wall exactly.
+void bookkeepingPath(const OctreeGrid& t, int l, double x, double y, double z, double kx, double ky, double kz,
+                     Path& p) {
+    auto B = [&](int n) { return &t.box[6 * (size_t)n]; };
+    auto child = [&](int n, int k) { return t.firstChild[n] + k; };
+    while (true) {
+        const double* b = B(l);
+        double xnext = (kx < 0.0) ? b[0] : b[3];
+        double ynext = (ky < 0.0) ? b[1] : b[4];
+        double znext = (kz < 0.0) ? b[2] : b[5];
+        double dsx = (fabs(kx) > 1e-15) ? (xnext - x) / kx : DBL_MAX;
+        double dsy = (fabs(ky) > 1e-15) ? (ynext - y) / ky : DBL_MAX;
+        double dsz = (fabs(kz) > 1e-15) ? (znext - z) / kz : DBL_MAX;
+        if (dsx <= dsy && dsx <= dsz) {
+            p.add(t.cellnumber[l], dsx);
+            x = xnext; y += ky * dsx; z += kz * dsx;
+            while (true) {
+                int oct = ((l - 1) % 8) + 1;
+                bool place = (kx < 0.0) ? (oct % 2 == 1) : (oct % 2 == 0);
+                if (!place) break;
+                l = t.father[l];
+                if (l == 0) return;
+            }
+            l += (kx < 0.0) ? -1 : 1;
+            while (t.cellnumber[l] == -1) {
+                double yM = B(child(l, 0))[4], zM = B(child(l, 0))[5];
+                if (kx < 0.0) l = (y <= yM) ? ((z <= zM) ? child(l, 1) : child(l, 5)) : ((z <= zM) ? child(l, 3) : child(l, 7));
+                else l = (y <= yM) ? ((z <= zM) ? child(l, 0) : child(l, 4)) : ((z <= zM) ? child(l, 2) : child(l, 6));
+            }
+        } else if (dsy < dsx && dsy <= dsz) {
+            p.add(t.cellnumber[l], dsy);
+            x += kx * dsy; y = ynext; z += kz * dsy;
+            while (true) {
+                bool place = (ky < 0.0) ? ((l - 1) % 4 < 2) : ((l - 1) % 4 > 1);
+                if (!place) break;
+                l = t.father[l];
+                if (l == 0) return;
+            }
+            l += (ky < 0.0) ? -2 : 2;
+            while (t.cellnumber[l] == -1) {
+                double xM = B(child(l, 0))[3], zM = B(child(l, 0))[5];
+                if (ky < 0.0) l = (x <= xM) ? ((z <= zM) ? child(l, 2) : child(l, 6)) : ((z <= zM) ? child(l, 3) : child(l, 7));
+                else l = (x <= xM) ? ((z <= zM) ? child(l, 0) : child(l, 4)) : ((z <= zM) ? child(l, 1) : child(l, 5));
+            }
+        } else if (dsz < dsx && dsz < dsy) {
+            p.add(t.cellnumber[l], dsz);
+            x += kx * dsz; y += ky * dsz; z = znext;
+            while (true) {
+                int oct = ((l - 1) % 8) + 1;
+                bool place = (kz < 0.0) ? (oct < 5) : (oct > 4);
+                if (!place) break;
+                l = t.father[l];
+                if (l == 0) return;
+            }
+            l += (kz < 0.0) ? -4 : 4;
+            while (t.cellnumber[l] == -1) {
+                double xM = B(child(l, 0))[3], yM = B(child(l, 0))[4];
+                if (kz < 0.0) l = (x <= xM) ? ((y <= yM) ? child(l, 4) : child(l, 6)) : ((y <= yM) ? child(l, 5) : child(l, 7));
+                else l = (x <= xM) ? ((y <= yM) ? child(l, 0) : child(l, 2)) : ((y <= yM) ? child(l, 1) : child(l, 3));
+            }
+        } else {
+            return;  // NaN distances: the reference would loop forever; end the path
+        }
+    }
+}
+
 // TreeDustGrid::path, TopDown and Neighbor search (TreeDustGrid.cpp:390-521); moveInside
 // (DustGridPath.cpp:57-150)
 void octreePath(const OctreeGrid& t, Vec3 r, Vec3 k, Path& p) {
@@ -345,6 +415,7 @@ void octreePath(const OctreeGrid& t, Vec3 r, Vec3 k, Path& p) {
     int node = rootWhichnode(t, rx, ry, rz);
     if (node < 0) return p.clear();
     double x = rx, y = ry, z = rz;
+    if (t.search == 2) return bookkeepingPath(t, node, x, y, z, kx, ky, kz, p);
     while (node >= 0) {
         const double* b = &t.box[6 * (size_t)node];
         double xnext = (kx < 0.0) ? b[0] : b[3];
@@ -423,7 +494,6 @@ public:
         if (M.grid.kind == GridKind::Cartesian) cartesianPath(M.grid.cart, r, k, p);
         else if (M.grid.kind == GridKind::Voronoi) voronoiPath(M.grid.vor, r, k, p);
         else {
-            if (M.grid.tree.search == 2) throw std::runtime_error("Bookkeeping tree search is not supported");
             octreePath(M.grid.tree, r, k, p);
         }
     }

@@ -25,7 +25,7 @@ DATA_DIR = os.path.join(PKG_DIR, "data")
 
 GRID_CARTESIAN, GRID_OCTREE, GRID_VORONOI = 0, 1, 2
 # SkirtStats.grid_walk: the trace kernel's grid walk in the last run (SKIRT_WALK_*)
-WALK_CARTESIAN, WALK_OCTREE_MAP, WALK_VORONOI, WALK_TREE_NODES, WALK_KDTREE_MAP = 0, 1, 2, 3, 4
+WALK_CARTESIAN, WALK_OCTREE_MAP, WALK_VORONOI, WALK_TREE_NODES, WALK_KDTREE_MAP, WALK_OCTREE_BOOKKEEPING = 0, 1, 2, 3, 4, 5
 
 
 class SkirtError(RuntimeError):

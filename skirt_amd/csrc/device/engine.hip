@@ -124,6 +124,7 @@ constexpr int kVorUnroll = SKIRT_VOR_UNROLL;  // list entries loaded per round t
 // allow or not split at box centres, e.g. barycentric subdivision)
 constexpr int kOctreeNodes = 16;
 constexpr int kBinTreeMap = 17;
+constexpr int kOctreeBookkeeping = 18;  // octree, Bookkeeping search (node arrays)
 
 struct Args {
     // grid
@@ -133,6 +134,7 @@ struct Args {
     const double* box;           // octree
     const int* firstChild;
     const signed char* splitDir;  // binary trees: split axis per node (null for octrees)
+    const int* father;            // octree, Bookkeeping search: father of every node (-1 for the root)
     const int* cellnumber;
     const int* nbrOffset;
     const int* nbrList;
@@ -570,6 +572,86 @@ struct Grid<kOctreeNodes> {
     __device__ static __forceinline__ int whichcell(const Args& a, const Shared&, double x, double y, double z) {
         const int l = descend(a, x, y, z);
         return l < 0 ? -1 : a.cellnumber[l];
+    }
+};
+
+// Octree grid, Bookkeeping search (TreeDustGrid.cpp:523-659): the next node follows from the breadth-first
+// numbering (the 8 children of a node are consecutive ids in octant order, so (l-1) % 8 is the octant of
+// node l): climb while the node lies on the far side of its father, step to the sibling across the wall,
+// descend with "<=" to the leaf holding the exit point. The position is put on the crossed wall exactly
+// (no eps). Entry into the grid as for the other searches.
+template <>
+struct Grid<kOctreeBookkeeping> {
+    using Nodes = Grid<kOctreeNodes>;
+
+    template <class SegFn>
+    __device__ static __forceinline__ bool begin(const Args& a, const Shared& sh, Ray& r, SegFn seg) {
+        return Nodes::begin(a, sh, r, seg);
+    }
+    __device__ static __forceinline__ void resume(const Args& a, Ray& r) { Nodes::resume(a, r); }
+    __device__ static __forceinline__ int whichcell(const Args& a, const Shared& sh, double x, double y, double z) {
+        return Nodes::whichcell(a, sh, x, y, z);
+    }
+
+    __device__ static __forceinline__ const double* childBox(const Args& a, int l) {
+        return a.box + 6 * (size_t)a.firstChild[l];
+    }
+
+    template <class SegFn>
+    __device__ static __forceinline__ bool step(const Args& a, const Shared&, Ray& r, SegFn seg) {
+        const double xnext = (r.dx < 0.0) ? r.bx0 : r.bx1;
+        const double ynext = (r.dy < 0.0) ? r.by0 : r.by1;
+        const double znext = (r.dz < 0.0) ? r.bz0 : r.bz1;
+        const double dsx = (r.ix != 0.0) ? (xnext - r.x) * r.ix : kDblMax;
+        const double dsy = (r.iy != 0.0) ? (ynext - r.y) * r.iy : kDblMax;
+        const double dsz = (r.iz != 0.0) ? (znext - r.z) * r.iz : kDblMax;
+        int l = r.ci;
+        if (dsx <= dsy && dsx <= dsz) {
+            if (!seg(r.cj, a.rho[(size_t)r.cj * a.ncomp], dsx)) return false;
+            r.x = xnext; r.y += r.dy * dsx; r.z += r.dz * dsx;
+            while ((r.dx < 0.0) ? (((l - 1) & 1) == 0) : (((l - 1) & 1) == 1)) {
+                l = a.father[l];
+                if (l == 0) return false;
+            }
+            l += (r.dx < 0.0) ? -1 : 1;
+            while (a.cellnumber[l] < 0) {
+                const double* cb = childBox(a, l);
+                const int k = (r.dx < 0.0 ? 1 : 0) + (r.y <= cb[4] ? 0 : 2) + (r.z <= cb[5] ? 0 : 4);
+                l = a.firstChild[l] + k;
+            }
+        } else if (dsy < dsx && dsy <= dsz) {
+            if (!seg(r.cj, a.rho[(size_t)r.cj * a.ncomp], dsy)) return false;
+            r.x += r.dx * dsy; r.y = ynext; r.z += r.dz * dsy;
+            while ((r.dy < 0.0) ? (((l - 1) & 2) == 0) : (((l - 1) & 2) != 0)) {
+                l = a.father[l];
+                if (l == 0) return false;
+            }
+            l += (r.dy < 0.0) ? -2 : 2;
+            while (a.cellnumber[l] < 0) {
+                const double* cb = childBox(a, l);
+                const int k = (r.x <= cb[3] ? 0 : 1) + (r.dy < 0.0 ? 2 : 0) + (r.z <= cb[5] ? 0 : 4);
+                l = a.firstChild[l] + k;
+            }
+        } else if (dsz < dsx && dsz < dsy) {
+            if (!seg(r.cj, a.rho[(size_t)r.cj * a.ncomp], dsz)) return false;
+            r.x += r.dx * dsz; r.y += r.dy * dsz; r.z = znext;
+            while ((r.dz < 0.0) ? (((l - 1) & 4) == 0) : (((l - 1) & 4) != 0)) {
+                l = a.father[l];
+                if (l == 0) return false;
+            }
+            l += (r.dz < 0.0) ? -4 : 4;
+            while (a.cellnumber[l] < 0) {
+                const double* cb = childBox(a, l);
+                const int k = (r.x <= cb[3] ? 0 : 1) + (r.y <= cb[4] ? 0 : 2) + (r.dz < 0.0 ? 4 : 0);
+                l = a.firstChild[l] + k;
+            }
+        } else {
+            return false;  // NaN distances
+        }
+        r.ci = l;
+        r.cj = a.cellnumber[l];
+        Nodes::loadBox(a, l, r.bx0, r.by0, r.bz0, r.bx1, r.by1, r.bz1);
+        return true;
     }
 };
 
@@ -1839,6 +1921,7 @@ struct SkirtMcrt {
     double* dBox = nullptr;
     int *dFirstChild = nullptr, *dCellnumber = nullptr, *dNbrOffset = nullptr, *dNbrList = nullptr;
     signed char* dSplitDir = nullptr;  // k-d tree split axes (null for octrees)
+    int* dFather = nullptr;            // octree fathers (Bookkeeping search)
     bool binTree = false;
     // Voronoi grid
     double *dSite = nullptr, *dCellBbox = nullptr;
@@ -2134,6 +2217,20 @@ int skirt_mcrt_upload_grid(SkirtMcrt* c, const SkirtGridDesc* g) {
             if (g->nbr_offset[q] < 0 || g->nbr_offset[q] > g->nbr_offset[q + 1]) return fail(c, SKIRT_ERR_ARG, "bad neighbor offsets");
         for (int q = 0; q < nnbr; q++)
             if (g->nbr_list[q] < 0 || g->nbr_list[q] >= g->nnodes) return fail(c, SKIRT_ERR_ARG, "neighbor index out of range");
+        if (g->search < SKIRT_TREE_TOPDOWN || g->search > SKIRT_TREE_BOOKKEEPING) return fail(c, SKIRT_ERR_ARG, "bad tree search method");
+        std::vector<int> father;
+        if (g->search == SKIRT_TREE_BOOKKEEPING) {
+            // the Bookkeeping search reads octants off the breadth-first numbering: every group of
+            // children must start at an id = 1 (mod 8) (TreeDustGrid.cpp:525)
+            if (bin) return fail(c, SKIRT_ERR_ARG, "Bookkeeping method is not compatible with binary tree");
+            father.assign(g->nnodes, -1);
+            for (int l = 0; l < g->nnodes; l++) {
+                const int fc = g->first_child[l];
+                if (fc < 0) continue;
+                if ((fc - 1) % 8 != 0) return fail(c, SKIRT_ERR_ARG, "octree not numbered breadth-first for the Bookkeeping search");
+                for (int k = 0; k < 8; k++) father[fc + k] = l;
+            }
+        }
         c->nnodes = g->nnodes;
         c->eps = g->eps;
         c->search = g->search;
@@ -2143,6 +2240,7 @@ int skirt_mcrt_upload_grid(SkirtMcrt* c, const SkirtGridDesc* g) {
         if ((rc = upload(c, c->dBox, g->box, 6 * (size_t)g->nnodes))) return rc;
         if ((rc = upload(c, c->dFirstChild, g->first_child, (size_t)g->nnodes))) return rc;
         c->binTree = bin;
+        if (!father.empty() && (rc = upload(c, c->dFather, father.data(), father.size()))) return rc;
         if (bin) {
             std::vector<signed char> dirs(g->split_dir, g->split_dir + g->nnodes);
             for (int l = 0; l < g->nnodes; l++)
@@ -2603,11 +2701,13 @@ int skirt_mcrt_run_phase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, 
     a.gx0 = c->gx0; a.gx1 = c->gx1; a.gy0 = c->gy0; a.gy1 = c->gy1; a.gz0 = c->gz0; a.gz1 = c->gz1;
     a.box = c->dBox; a.firstChild = c->dFirstChild; a.cellnumber = c->dCellnumber;
     a.splitDir = c->binTree ? c->dSplitDir : nullptr;
+    a.father = c->dFather;
     a.nbrOffset = c->dNbrOffset; a.nbrList = c->dNbrList; a.eps = c->eps; a.search = c->search;
     a.site = c->dSite; a.cellNbrOffset = c->dCellNbrOffset; a.cellNbr = c->dCellNbr; a.cellBbox = c->dCellBbox;
     a.devCell = c->dDevCell;
     a.vnb = c->vnb; a.blockOffset = c->dBlockOffset; a.blockList = c->dBlockList;
-    const bool leafMap = c->gridKind == SKIRT_GRID_OCTREE && c->mapL >= 0 && p->has_dust;
+    const bool bookkeeping = c->gridKind == SKIRT_GRID_OCTREE && c->search == SKIRT_TREE_BOOKKEEPING;
+    const bool leafMap = c->gridKind == SKIRT_GRID_OCTREE && c->mapL >= 0 && p->has_dust && !bookkeeping;
     if (leafMap) {
         if ((rc = ensureLeafMap(c))) return rc;
         a.leafMap = c->dLeafMap; a.treeT = c->dTreeT; a.mapL = c->mapL; a.mapN = c->mapN;
@@ -2657,10 +2757,12 @@ int skirt_mcrt_run_phase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, 
     if (lds > 64 * 1024) return fail(c, SKIRT_ERR_UNSUPPORTED, "tables do not fit in LDS (" + std::to_string(lds) + " bytes)");
     const int kind = c->gridKind == SKIRT_GRID_CARTESIAN ? SKIRT_GRID_CARTESIAN
                      : c->gridKind == SKIRT_GRID_VORONOI ? SKIRT_GRID_VORONOI
+                     : bookkeeping ? kOctreeBookkeeping
                      : (leafMap ? (c->binTree ? kBinTreeMap : SKIRT_GRID_OCTREE) : kOctreeNodes);
     c->lastWalk = kind == SKIRT_GRID_CARTESIAN ? SKIRT_WALK_CARTESIAN
                   : kind == SKIRT_GRID_OCTREE  ? SKIRT_WALK_OCTREE_MAP
                   : kind == kBinTreeMap        ? SKIRT_WALK_KDTREE_MAP
+                  : kind == kOctreeBookkeeping ? SKIRT_WALK_OCTREE_BOOKKEEPING
                   : kind == SKIRT_GRID_VORONOI ? SKIRT_WALK_VORONOI
                                                : SKIRT_WALK_TREE_NODES;
     const bool one = a.ncomp == 1;
@@ -2669,6 +2771,7 @@ int skirt_mcrt_run_phase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, 
     if (kind == SKIRT_GRID_CARTESIAN) pick(traceKernel<SKIRT_GRID_CARTESIAN, true>, traceKernel<SKIRT_GRID_CARTESIAN, false>);
     else if (kind == SKIRT_GRID_OCTREE) pick(traceKernel<SKIRT_GRID_OCTREE, true>, traceKernel<SKIRT_GRID_OCTREE, false>);
     else if (kind == kBinTreeMap) pick(traceKernel<kBinTreeMap, true>, traceKernel<kBinTreeMap, false>);
+    else if (kind == kOctreeBookkeeping) pick(traceKernel<kOctreeBookkeeping, true>, traceKernel<kOctreeBookkeeping, false>);
     else if (kind == SKIRT_GRID_VORONOI) pick(traceKernel<SKIRT_GRID_VORONOI, true>, traceKernel<SKIRT_GRID_VORONOI, false>);
     else pick(traceKernel<kOctreeNodes, true>, traceKernel<kOctreeNodes, false>);
     int tgrid = c->traceGrid;
@@ -2693,6 +2796,7 @@ int skirt_mcrt_run_phase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, 
         if (kind == SKIRT_GRID_CARTESIAN) { if (one) SKIRT_EVENT(SKIRT_GRID_CARTESIAN, true); else SKIRT_EVENT(SKIRT_GRID_CARTESIAN, false); }
         else if (kind == SKIRT_GRID_OCTREE) { if (one) SKIRT_EVENT(SKIRT_GRID_OCTREE, true); else SKIRT_EVENT(SKIRT_GRID_OCTREE, false); }
         else if (kind == kBinTreeMap) { if (one) SKIRT_EVENT(kBinTreeMap, true); else SKIRT_EVENT(kBinTreeMap, false); }
+        else if (kind == kOctreeBookkeeping) { if (one) SKIRT_EVENT(kOctreeBookkeeping, true); else SKIRT_EVENT(kOctreeBookkeeping, false); }
         else if (kind == SKIRT_GRID_VORONOI) { if (one) SKIRT_EVENT(SKIRT_GRID_VORONOI, true); else SKIRT_EVENT(SKIRT_GRID_VORONOI, false); }
         else { if (one) SKIRT_EVENT(kOctreeNodes, true); else SKIRT_EVENT(kOctreeNodes, false); }
 #undef SKIRT_EVENT
@@ -2702,6 +2806,7 @@ int skirt_mcrt_run_phase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, 
         if (kind == SKIRT_GRID_CARTESIAN) { if (one) SKIRT_TRACE(SKIRT_GRID_CARTESIAN, true); else SKIRT_TRACE(SKIRT_GRID_CARTESIAN, false); }
         else if (kind == SKIRT_GRID_OCTREE) { if (one) SKIRT_TRACE(SKIRT_GRID_OCTREE, true); else SKIRT_TRACE(SKIRT_GRID_OCTREE, false); }
         else if (kind == kBinTreeMap) { if (one) SKIRT_TRACE(kBinTreeMap, true); else SKIRT_TRACE(kBinTreeMap, false); }
+        else if (kind == kOctreeBookkeeping) { if (one) SKIRT_TRACE(kOctreeBookkeeping, true); else SKIRT_TRACE(kOctreeBookkeeping, false); }
         else if (kind == SKIRT_GRID_VORONOI) { if (one) SKIRT_TRACE(SKIRT_GRID_VORONOI, true); else SKIRT_TRACE(SKIRT_GRID_VORONOI, false); }
         else { if (one) SKIRT_TRACE(kOctreeNodes, true); else SKIRT_TRACE(kOctreeNodes, false); }
 #undef SKIRT_TRACE
@@ -2853,7 +2958,7 @@ void skirt_mcrt_destroy(SkirtMcrt* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    void* bufs[] = {c->dMesh, c->dBox, c->dFirstChild, c->dSplitDir, c->dCellnumber, c->dNbrOffset, c->dNbrList, c->dTreeT,
+    void* bufs[] = {c->dMesh, c->dBox, c->dFirstChild, c->dSplitDir, c->dFather, c->dCellnumber, c->dNbrOffset, c->dNbrList, c->dTreeT,
                     c->dLeafMap, c->dCellLv, c->dCellCdf, c->dCellLtot, c->dCellNode, c->dEmisVolume, c->dEmisKabs,
                     c->dEmisSigma, c->dEmisMu, c->dEmisTv, c->dEmisPlanck, c->dEmisLambda, c->dEmisDlambda,
                     c->dEmisScratch, c->dDevCell, c->dSite, c->dCellBbox, c->dCellNbrOffset, c->dCellNbr,

@@ -145,8 +145,7 @@ int skirt_sim_attach(SkirtSim* s, int device) {
             g.nbr_offset = t.nbrOffset.data();
             g.nbr_list = t.nbrList.data();
             g.eps = t.eps;
-            g.search = t.search == 0 ? SKIRT_TREE_TOPDOWN : SKIRT_TREE_NEIGHBOR;
-            if (t.search == 2) { g_err = "Bookkeeping tree search is not supported by the engine"; return SKIRT_ERR_UNSUPPORTED; }
+            g.search = t.search == 0 ? SKIRT_TREE_TOPDOWN : t.search == 2 ? SKIRT_TREE_BOOKKEEPING : SKIRT_TREE_NEIGHBOR;
         }
         if ((rc = check(s, skirt_mcrt_upload_grid(s->eng, &g)))) return rc;
         int nc = m.ncomp();

@@ -22,7 +22,9 @@ def run_gpu(path, packages):
 
 @pytest.mark.parametrize("name,walk", [("bin_pan", S.WALK_KDTREE_MAP), ("bin_pan_td", S.WALK_KDTREE_MAP),
                                        ("bin_full", S.WALK_KDTREE_MAP), ("bin_bary", None),
-                                       ("oct_bary", S.WALK_TREE_NODES), ("oct_pan_td", S.WALK_OCTREE_MAP)])
+                                       ("oct_bary", S.WALK_TREE_NODES), ("oct_pan_td", S.WALK_OCTREE_MAP),
+                                       ("oct_pan_bk", S.WALK_OCTREE_BOOKKEEPING),
+                                       ("oct_bary_bk", S.WALK_OCTREE_BOOKKEEPING)])
 def test_tree_engine_matches_oracle_same_streams(tmp_path, name, walk):
     path = T.write(name, str(tmp_path))
     packages = 2000
@@ -56,7 +58,8 @@ def test_kd_tree_leaf_map_walk_equals_node_walk(tmp_path, name, monkeypatch):
     assert sa["grid_walk"] == S.WALK_KDTREE_MAP and sb["grid_walk"] == S.WALK_TREE_NODES
     for k in ("packets", "segments_fill", "segments_walk", "segments_peel", "detects", "absorb_adds"):
         assert sa[k] == sb[k], (k, sa[k], sb[k])
-    np.testing.assert_allclose(a.labs(), b.labs(), rtol=1e-10, atol=1e-300)
+    if a.labs() is not None:
+        np.testing.assert_allclose(a.labs(), b.labs(), rtol=1e-10, atol=1e-300)
     fa, da = a.instrument(0)
     fb, db = b.instrument(0)
     np.testing.assert_allclose(da, db, rtol=1e-10, atol=1e-300)

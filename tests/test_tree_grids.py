@@ -114,3 +114,26 @@ def test_tree_variants_run_in_both_rng_modes(tmp_path, name):
         assert np.isfinite(res.labs).all() and res.labs.sum() > 0
     # the two streams estimate the same absorbed luminosity
     np.testing.assert_allclose(mt.labs.sum(), ph.labs.sum(), rtol=0.1)
+
+
+@pytest.mark.parametrize("nb,bk", [("pan_oct", "oct_pan_bk"), ("oct_bary", "oct_bary_bk")])
+def test_bookkeeping_search_crosses_the_neighbor_search_cells(tmp_path, nb, bk):
+    """The Bookkeeping search (TreeDustGrid.cpp:523-659) puts the position on each crossed wall instead of
+    eps beyond it, so its segments differ from the Neighbor search's by about eps; it crosses the same
+    cells in the same order (apart from rays through a cell edge or corner, where the two searches may
+    legitimately pick different cells) and covers the same chord."""
+    import os
+    r = rays(300, 13)
+    src = os.path.join(T.GOLD, "pan_oct.ski") if nb == "pan_oct" else T.write(nb, str(tmp_path))
+    a, na = O.grid_paths(src, r)
+    b, nb_ = O.grid_paths(T.write(bk, str(tmp_path)), r)
+    assert na == nb_
+    same = 0
+    eps = 1e-12 * np.sqrt(3) * 1000 * PC
+    for (ba, da), (bb, db) in zip(a, b):
+        if len(da) == len(db) and np.array_equal(ba, bb, equal_nan=True):
+            same += 1
+            np.testing.assert_allclose(da, db, rtol=0, atol=4 * eps)
+        if len(da):
+            np.testing.assert_allclose(da.sum(), db.sum(), rtol=1e-9)
+    assert same >= 0.99 * len(r)

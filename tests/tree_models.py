@@ -3,7 +3,7 @@
 The reference fixtures cover the OctTreeDustGrid with centre splits and the Neighbor search
 (pan_oct). Its other tree grids -- BinTreeDustGrid (the k-d tree, Alternating or Barycenter split
 directions, BinTreeDustGrid.cpp, BinTreeNode.cpp, BaryBinTreeNode.cpp), barycentric octrees
-(BaryOctTreeNode.cpp) and the TopDown search -- have no reference outputs here (the reference binary
+(BaryOctTreeNode.cpp), the TopDown and Bookkeeping searches -- have no reference outputs here (the reference binary
 cannot be built or run in this repository), so these variants swap only the <dustGrid> element of a
 pinned model and are checked against the pinned octree walk (geometric equivalence) and against the
 oracle on the same random streams.
@@ -39,6 +39,10 @@ GRIDS = {
                  'sampleCount="100" maxOpticalDepth="0" maxMassFraction="5e-4" maxDensDispFraction="0" barycentric="true"/>'),
     "oct_pan_td": ("pan_oct", '<OctTreeDustGrid writeGrid="false" %s minLevel="2" maxLevel="6" searchMethod="TopDown" '
                    'sampleCount="100" maxOpticalDepth="0" maxMassFraction="5e-4" maxDensDispFraction="0" barycentric="false"/>'),
+    "oct_pan_bk": ("pan_oct", '<OctTreeDustGrid writeGrid="false" %s minLevel="2" maxLevel="6" searchMethod="Bookkeeping" '
+                   'sampleCount="100" maxOpticalDepth="0" maxMassFraction="5e-4" maxDensDispFraction="0" barycentric="false"/>'),
+    "oct_bary_bk": ("pan_oct", '<OctTreeDustGrid writeGrid="false" %s minLevel="1" maxLevel="6" searchMethod="Bookkeeping" '
+                    'sampleCount="100" maxOpticalDepth="0" maxMassFraction="5e-4" maxDensDispFraction="0" barycentric="true"/>'),
 }
 
 
