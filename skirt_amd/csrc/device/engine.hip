@@ -55,7 +55,10 @@ constexpr int kStepsPerPull = SKIRT_STEPS_PER_PULL;  // grid steps between two r
 // The slot pool runs as kHalves independent pipelines on their own streams: while one half's trace
 // kernel drains its queue, the other half's event and detect kernels (and its trace kernel's first
 // waves) fill the CUs the finishing waves leave idle.
-constexpr int kHalves = 1;
+#ifndef SKIRT_HALVES
+#define SKIRT_HALVES 1
+#endif
+constexpr int kHalves = SKIRT_HALVES;
 constexpr int kPollEvery = 1;      // iterations between two counter copies of a half
 constexpr int kPollRing = 3;       // copies in flight per half (the host reads each kPollRing copies late)
 // occupancy attribute of the trace kernel (a build knob for tuning variants, tools/build_variant.sh)
