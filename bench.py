@@ -69,8 +69,9 @@ def cpu_baseline(ski, target_seconds=20.0):
     nl = probe.nlambda
     per = int(max(200, min(1e6, rate * target_seconds / nl)))
     r = oracle_lib.run(ski, rng=oracle_lib.RNG_PHILOX, threads=threads, packages=per)
-    return r.packets / r.seconds, threads, "%d packets/wavelength x %d wavelengths = %d packets in %.1f s" % (
-        per, nl, r.packets, r.seconds)
+    # counted like the GPU line: packages x wavelengths (wavelengths without source luminosity launch none)
+    return per * nl / r.seconds, threads, "%d packets/wavelength x %d wavelengths = %d packets (%d launched) in %.1f s" % (
+        per, nl, per * nl, r.packets, r.seconds)
 
 
 def main():
@@ -177,6 +178,11 @@ def main():
             dist.all_reduce(n)
         packets_all = float(n.item())
     value = packets_all / elapsed
+    launched = torch.tensor([float(sum(st["packets"] for st in per_step) if dust_phases else delta["packets"])],
+                            dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(launched)
+    launched_rate = float(launched.item()) / elapsed
     avg_kernel_s = sum(kernel_ms) / len(kernel_ms) / 1e3
     segs = delta["segments_fill"] + delta["segments_walk"] + delta["segments_peel"]
     # the dominant kernel: traceKernel. Its algorithmic bytes per launch (without the
@@ -207,6 +213,10 @@ def main():
             "octree_nodes": info.nnodes,
             "wavelengths": info.nlambda,
             "packets_per_step_per_gpu": share,
+            # BASELINE.md section 2 counts packages x wavelengths; the stellar SED emits nothing at the
+            # longest wavelengths, whose packets the reference (dostellaremissionchunk) and the engine
+            # skip alike. The rate of packets actually launched:
+            "launched_packets_per_s": launched_rate,
             "parallelism": "dp%d (packet sharding, RCCL all-reduce of Labs + instrument tallies per phase)" % world,
             "segments_per_packet": segs / max(1, delta["packets"]),
             "lane_use": (delta["segments_fill"] + delta["segments_walk"] + delta["segments_peel"]) / max(1, delta["lane_slots"]),
