@@ -165,9 +165,10 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    delta = {k: s1[k] - s0[k] for k in s1 if k not in ("kernel_ms", "iterations")}
+    delta = {k: s1[k] - s0[k] for k in s1 if k not in ("kernel_ms", "iterations", "device_cells")}
     if dust_phases:
-        for k in ("packets", "segments_fill", "segments_walk", "segments_peel", "detects", "absorb_adds", "lane_slots"):
+        for k in ("packets", "segments_fill", "segments_walk", "segments_peel", "detects", "absorb_adds", "lane_slots",
+                  "labs_requests"):
             delta[k] = sum(st[k] for st in per_step)
     trace_ms, trace_launches = delta["trace_ms"], delta["trace_launches"]
     packets_all = share * world * args.steps
@@ -211,6 +212,7 @@ def main():
             "ski": ski_rel,
             "cells": info.ncells,
             "octree_nodes": info.nnodes,
+            "device_cells": s1["device_cells"],
             "wavelengths": info.nlambda,
             "packets_per_step_per_gpu": share,
             # BASELINE.md section 2 counts packages x wavelengths; the stellar SED emits nothing at the
@@ -240,6 +242,8 @@ def main():
             # what actually bounds the kernel: Labs adds are scattered f64 atomics, executed memory-side
             # at a fixed chip-wide rate (tools/atomic_bench.hip, profiles/r01_atomic_bench.txt)
             "labs_atomic_adds_per_s": delta["absorb_adds"] / max(1e-9, trace_ms / 1e3),
+            # adds that shared a 64-byte request (same line, same wave instruction)
+            "labs_adds_per_request": delta["absorb_adds"] / max(1, delta["labs_requests"]),
             "labs_atomic_peak_measured": ATOMIC_PEAK_ADDS,
         },
         "phase_ms_avg": avg_kernel_s * 1e3,

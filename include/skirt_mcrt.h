@@ -171,6 +171,9 @@ typedef struct {
     uint64_t trace_launches;    /* trace-kernel launches timed so far, cumulative */
     int32_t grid_walk;          /* walk of the last run: SKIRT_WALK_* */
     int32_t map_level;          /* tree leaf-map depth (finest cells per axis = 2^map_level), -1 without */
+    uint64_t labs_requests;     /* 64-byte atomic requests carrying the Labs adds (adds sharing a line in
+                                   one wave instruction share a request) */
+    uint64_t device_cells;      /* device cell numbers, >= ncells (octree sibling groups start on a line) */
 } SkirtStats;
 
 /* grid walks of the trace kernel (SkirtStats::grid_walk) */
@@ -185,8 +188,8 @@ int skirt_mcrt_upload_grid(SkirtMcrt* ctx, const SkirtGridDesc* grid);
 int skirt_mcrt_upload_media(SkirtMcrt* ctx, const SkirtMediaDesc* media);
 int skirt_mcrt_upload_sources(SkirtMcrt* ctx, const SkirtSourceDesc* src);
 int skirt_mcrt_set_instruments(SkirtMcrt* ctx, const SkirtInstrDesc* instr, int n);
-/* device tally buffers: Labs (ncells*nlambda doubles, stored wavelength-major [nlambda][ncells] on the
- * device) and the concatenated instrument tallies. Optionally bind caller-owned device memory of the
+/* device tally buffers: Labs (stored wavelength-major [nlambda][row] on the device, rows of device cells
+ * padded to a 64-byte line; n_labs >= ncells*nlambda) and the concatenated instrument tallies. Optionally bind caller-owned device memory of the
  * sizes returned by skirt_mcrt_tally_sizes (e.g. torch tensors, so they can be all-reduced in place). */
 int skirt_mcrt_tally_sizes(SkirtMcrt* ctx, size_t* n_labs, size_t* n_instr);
 int skirt_mcrt_bind_tallies(SkirtMcrt* ctx, double* d_labs, double* d_instr);

@@ -37,7 +37,8 @@ class SkirtStats(ctypes.Structure):
                 ("segments_walk", ctypes.c_uint64), ("segments_peel", ctypes.c_uint64),
                 ("detects", ctypes.c_uint64), ("absorb_adds", ctypes.c_uint64), ("lane_slots", ctypes.c_uint64),
                 ("iterations", ctypes.c_uint64), ("kernel_ms", ctypes.c_double), ("trace_ms", ctypes.c_double),
-                ("trace_launches", ctypes.c_uint64), ("grid_walk", ctypes.c_int32), ("map_level", ctypes.c_int32)]
+                ("trace_launches", ctypes.c_uint64), ("grid_walk", ctypes.c_int32), ("map_level", ctypes.c_int32),
+                ("labs_requests", ctypes.c_uint64), ("device_cells", ctypes.c_uint64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

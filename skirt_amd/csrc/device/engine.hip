@@ -132,6 +132,7 @@ constexpr int kOctreeBookkeeping = 18;  // octree, Bookkeeping search (node arra
 struct Args {
     // grid
     int nx, ny, nz, ncells;
+    int labsStride;              // Labs row length (device cells, padded to a 64-byte line)
     const double* mesh;          // Cartesian borders x | y | z (staged in LDS)
     double gx0, gx1, gy0, gy1, gz0, gz1;
     const double* box;           // octree
@@ -185,7 +186,7 @@ struct Args {
     double xi;
     int store, hasDust;
     // tallies
-    double* labs;                // [nlambda][ncells]
+    double* labs;                // [nlambda][labsStride], device cell order
     double* tally;
     unsigned int* error;
     unsigned long long* stats;   // packets, seg_fill, seg_walk, seg_peel, detects, absorbs, lane slots
@@ -285,11 +286,11 @@ __device__ __forceinline__ constexpr int gridParts() {
 // The counters live in kStatCopies copies of one 64-byte line each (summed by the host): the waves of a
 // launch end together, and same-line atomics from all of them would queue on one L2 channel.
 constexpr int kStatCopies = 64;
-__device__ __forceinline__ void flushStats(const Args& a, const unsigned long long (&vals)[7]) {
+__device__ __forceinline__ void flushStats(const Args& a, const unsigned long long (&vals)[8]) {
     const int lane = threadIdx.x & 63;
     unsigned long long* dst = a.stats + 8 * ((blockIdx.x * (kBlock / 64) + threadIdx.x / 64) & (kStatCopies - 1));
 #pragma unroll
-    for (int q = 0; q < 7; q++) {
+    for (int q = 0; q < 8; q++) {
         unsigned long long v = vals[q];
         for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
         if (lane == 0 && v) atomicAdd(dst + q, v);
@@ -933,6 +934,7 @@ struct Tracer {
     const Args& a;
     const Shared& sh;
     unsigned int segFill = 0, segWalk = 0, segPeel = 0, absorbs = 0, laneSlots = 0;
+    unsigned int requests = 0;  // 64-byte atomic requests of the Labs adds (lane 0 of each wave counts)
     // Labs adds of this lane not yet issued. f64 atomics execute memory-side at a fixed chip-wide rate
     // of 64-byte requests; lanes of one wave instruction that hit the same 64-byte line share a
     // request. A lane's consecutive adds are consecutive cells of one ray -- spatial neighbours, and
@@ -955,10 +957,17 @@ struct Tracer {
             const int src = G * i + lane / kLabsBuf;
             const int n = __shfl(npend, src);
             const int q = j * kBlock + wbase + src;
+            const unsigned idx = pendIdx[q];
+            // the requests of this instruction: a lane starts one unless the lane before it (the same
+            // ray's previous add) hit the same 64-byte line
+            const unsigned line = (unsigned)(reinterpret_cast<size_t>(a.labs + idx) >> 6);
+            const unsigned prev = __shfl(line, lane - 1);
+            const unsigned long long starts = __ballot(j < n && (j == 0 || prev != line));
+            if (lane == 0) requests += (unsigned)__popcll(starts);
 #ifdef SKIRT_EXPERIMENT_NO_LABS_ATOMICS  // tuning experiment only: the cost of the Labs atomics
-            if (j < n && pendVal[q] == -1.0) atomicAddF64(a.labs + pendIdx[q], pendVal[q]);
+            if (j < n && pendVal[q] == -1.0) atomicAddF64(a.labs + idx, pendVal[q]);
 #else
-            if (j < n) atomicAddF64(a.labs + pendIdx[q], pendVal[q]);
+            if (j < n) atomicAddF64(a.labs + idx, pendVal[q]);
 #endif
         }
         npend = 0;
@@ -997,7 +1006,7 @@ struct Tracer {
                 }
                 if (a.store) {
                     pendVal[npend * kBlock + threadIdx.x] = (1.0 - albedo) * Lintm;
-                    pendIdx[npend * kBlock + threadIdx.x] = (unsigned)r.ell * (unsigned)a.ncells + (unsigned)m;
+                    pendIdx[npend * kBlock + threadIdx.x] = (unsigned)r.ell * (unsigned)a.labsStride + (unsigned)m;
                     npend++;
                     absorbs++;
                 }
@@ -1118,6 +1127,7 @@ struct EmisArgs {
     const double* planckabs;     // [ncomp][ntemp]
     const double* lambda;        // [nlambda]
     const double* dlambda;       // [nlambda]
+    int labsStride;              // Labs row length
     double* lv;                  // out [nlambda][ncells]
     double* cdf;                 // out [nlambda][ncells + 1]
     double* ltot;                // out [nlambda]
@@ -1134,19 +1144,20 @@ __device__ __forceinline__ double planckB(double T, double lambda) {  // PlanckF
 __global__ void __launch_bounds__(kBlock) cellSpectraKernel(const EmisArgs e) {
     const int m = blockIdx.x * blockDim.x + threadIdx.x;
     if (m >= e.ncells) return;
-    const int N = e.ncells, Nl = e.nlambda;
+    const int Nl = e.nlambda;
+    const size_t S = e.labsStride;
     const int dm = e.devCell ? e.devCell[m] : m;
     // PanDustSystem::Labs(m): stellar sum, continued by the dust sum
     double Labsbol = 0;
-    for (int ell = 0; ell < Nl; ell++) Labsbol += e.labs[(size_t)ell * N + dm];
+    for (int ell = 0; ell < Nl; ell++) Labsbol += e.labs[ell * S + dm];
     if (e.labsDust)
-        for (int ell = 0; ell < Nl; ell++) Labsbol += e.labsDust[(size_t)ell * N + dm];
+        for (int ell = 0; ell < Nl; ell++) Labsbol += e.labsDust[ell * S + dm];
     double Jv[kMaxEmisLambda], Lv[kMaxEmisLambda];
     const double fac = 4.0 * M_PI * e.volume[m];
     for (int ell = 0; ell < Nl; ell++) {  // DustSystem::meanintensityv
         double L = 0;
-        L += e.labs[(size_t)ell * N + dm];
-        if (e.labsDust) L += e.labsDust[(size_t)ell * N + dm];
+        L += e.labs[ell * S + dm];
+        if (e.labsDust) L += e.labsDust[ell * S + dm];
         double kr = 0.0;
         for (int h = 0; h < e.ncomp; h++) kr += e.kabs[h * Nl + ell] * e.rho[(size_t)dm * e.ncomp + h];
         const double J = L / (kr * fac) / e.dlambda[ell];
@@ -1183,7 +1194,7 @@ __global__ void __launch_bounds__(kBlock) cellSpectraKernel(const EmisArgs e) {
     }
     for (int ell = 0; ell < Nl; ell++) {
         const double lum = total > 0 ? Lv[ell] / total : Lv[ell];
-        e.lv[(size_t)ell * N + m] = Labsbol > 0.0 ? Labsbol * lum : 0.0;
+        e.lv[(size_t)ell * e.ncells + m] = Labsbol > 0.0 ? Labsbol * lum : 0.0;
     }
 }
 
@@ -1347,7 +1358,7 @@ __global__ void __launch_bounds__(kBlock) SKIRT_TRACE_ATTR traceKernel(const Arg
         }
     }
     T.drain();
-    const unsigned long long vals[7] = {0, T.segFill, T.segWalk, T.segPeel, 0, T.absorbs, T.laneSlots};
+    const unsigned long long vals[8] = {0, T.segFill, T.segWalk, T.segPeel, 0, T.absorbs, T.laneSlots, T.requests};
     flushStats(a, vals);
 }
 
@@ -1379,7 +1390,7 @@ __global__ void __launch_bounds__(kBlock) detectKernel(const Args a) {
             atomicAddF64(a.tally + sh.instr[ii].sedBase + (q - sh.instr[ii].sedOff), v);
         }
     }
-    const unsigned long long vals[7] = {0, 0, 0, 0, detects, 0, 0};
+    const unsigned long long vals[8] = {0, 0, 0, 0, detects, 0, 0, 0};
     flushStats(a, vals);
 }
 
@@ -1904,7 +1915,7 @@ __global__ void __launch_bounds__(kBlock) SKIRT_EVENT_ATTR eventKernel(const Arg
         if (active) actOut[apos] = slot;
         if (valid) E.store(slot, p);
     }
-    const unsigned long long vals[7] = {E.packets, E.segFill, E.segWalk, E.segPeel, E.detects, 0, 0};
+    const unsigned long long vals[8] = {E.packets, E.segFill, E.segWalk, E.segPeel, E.detects, 0, 0, 0};
     flushStats(a, vals);
 }
 
@@ -1919,6 +1930,10 @@ struct SkirtMcrt {
     std::string err;
     // grid
     int gridKind = -1, ncells = 0, nx = 0, ny = 0, nz = 0, nnodes = 0, search = 1;
+    // device cell space: ndev >= ncells device cell numbers (octrees leave unused numbers so that every
+    // group of 8 sibling leaves starts on a 64-byte line), Labs rows of labsStride (ndev rounded up to 8)
+    int ndev = 0;
+    int labsStride = 0;
     double eps = 0, gx0 = 0, gx1 = 0, gy0 = 0, gy1 = 0, gz0 = 0, gz1 = 0;
     double* dMesh = nullptr;
     double* dBox = nullptr;
@@ -2053,7 +2068,7 @@ int planLeafMap(SkirtMcrt* c, const SkirtGridDesc* g) {
     const char* env = getenv("SKIRT_AMD_LEAFMAP");
     if (env && env[0] == '0') return SKIRT_OK;
     const bool bin = g->split_dir != nullptr;
-    if (g->ncells >= (int)(1u << (bin ? kBinCellBits : kLeafLevelShift))) return SKIRT_OK;
+    if (c->ndev >= (int)(1u << (bin ? kBinCellBits : kLeafLevelShift))) return SKIRT_OK;
     const int maxL = bin ? kMaxBinMapLevel : kMaxMapLevel;
     struct Item { int node, lv[3], idx[3]; };  // per-axis depth and integer coordinate
     std::vector<Item> stack{{0, {0, 0, 0}, {0, 0, 0}}};
@@ -2181,6 +2196,7 @@ int skirt_mcrt_upload_grid(SkirtMcrt* c, const SkirtGridDesc* g) {
     if (!c || !g) return SKIRT_ERR_ARG;
     HIPCHECK(c, hipSetDevice(c->device));
     c->ncells = g->ncells;
+    c->ndev = g->ncells;
     c->devCell.clear();
     if (g->kind == SKIRT_GRID_CARTESIAN) {
         if (g->nx < 1 || g->ny < 1 || g->nz < 1 || !g->xv || !g->yv || !g->zv) return fail(c, SKIRT_ERR_ARG, "bad Cartesian grid");
@@ -2250,23 +2266,42 @@ int skirt_mcrt_upload_grid(SkirtMcrt* c, const SkirtGridDesc* g) {
                 if (g->first_child[l] < 0) dirs[l] = 0;
             if ((rc = upload(c, c->dSplitDir, dirs.data(), dirs.size()))) return rc;
         }
-        // Morton order of the leaves: depth-first, children in octant order (x, y, z bits)
+        // Morton order of the leaves: depth-first, children in octant order (x, y, z bits). A ray crosses
+        // about 2.5 of the 8 children of a node it enters, so 8 sibling leaves are numbered from a
+        // multiple of 8 (one 64-byte line of every Labs row), leaving unused device cells before them:
+        // the ray's Labs adds into them then share one atomic request (SKIRT_AMD_CELL_ALIGN=0: no gaps).
         c->devCell.assign(g->ncells, -1);
         {
+            const char* alignEnv = getenv("SKIRT_AMD_CELL_ALIGN");
+            const bool align = arity == 8 && !(alignEnv && alignEnv[0] == '0');
             std::vector<int> stack{0};
-            int next = 0;
+            int next = 0, used = 0;
+            auto number = [&](int l) -> bool {
+                if (c->devCell[g->cellnumber[l]] >= 0) return false;
+                c->devCell[g->cellnumber[l]] = next++;
+                used++;
+                return true;
+            };
             while (!stack.empty()) {
                 const int l = stack.back();
                 stack.pop_back();
                 const int fc = g->first_child[l];
                 if (fc < 0) {
-                    if (c->devCell[g->cellnumber[l]] >= 0) return fail(c, SKIRT_ERR_ARG, "octree cell number used twice");
-                    c->devCell[g->cellnumber[l]] = next++;
+                    if (!number(l)) return fail(c, SKIRT_ERR_ARG, "octree cell number used twice");
+                    continue;
+                }
+                bool leaves = align;
+                for (int k = 0; k < arity && leaves; k++) leaves = g->first_child[fc + k] < 0;
+                if (leaves) {  // the sibling leaves, aligned: the same depth-first order
+                    next = (next + 7) & ~7;
+                    for (int k = 0; k < arity; k++)
+                        if (!number(fc + k)) return fail(c, SKIRT_ERR_ARG, "octree cell number used twice");
                 } else {
                     for (int k = arity - 1; k >= 0; k--) stack.push_back(fc + k);
                 }
             }
-            if (next != g->ncells) return fail(c, SKIRT_ERR_ARG, "octree leaves do not cover the cells");
+            if (used != g->ncells) return fail(c, SKIRT_ERR_ARG, "octree leaves do not cover the cells");
+            c->ndev = next;
         }
         std::vector<int> cellNode(g->ncells, 0);
         for (int l = 0; l < g->nnodes; l++)
@@ -2362,6 +2397,7 @@ int skirt_mcrt_upload_grid(SkirtMcrt* c, const SkirtGridDesc* g) {
     } else {
         return fail(c, SKIRT_ERR_UNSUPPORTED, "unsupported grid kind");
     }
+    c->labsStride = (c->ndev + 7) & ~7;
     c->gridKind = g->kind;
     return SKIRT_OK;
 }
@@ -2386,7 +2422,7 @@ int skirt_mcrt_upload_media(SkirtMcrt* c, const SkirtMediaDesc* m) {
     if (c->devCell.empty()) {
         if ((rc = upload(c, c->dRho, m->rho, (size_t)m->ncells * m->ncomp))) return rc;
     } else {
-        std::vector<double> rho((size_t)m->ncells * m->ncomp);
+        std::vector<double> rho((size_t)c->ndev * m->ncomp, 0.0);  // unused device cells: no dust
         for (int q = 0; q < m->ncells; q++)
             for (int h = 0; h < m->ncomp; h++) rho[(size_t)c->devCell[q] * m->ncomp + h] = m->rho[(size_t)q * m->ncomp + h];
         if ((rc = upload(c, c->dRho, rho.data(), rho.size()))) return rc;
@@ -2458,13 +2494,13 @@ int skirt_mcrt_set_instruments(SkirtMcrt* c, const SkirtInstrDesc* in, int n) {
 
 int skirt_mcrt_tally_sizes(SkirtMcrt* c, size_t* nl, size_t* ni) {
     if (!c) return SKIRT_ERR_ARG;
-    if (nl) *nl = (size_t)c->ncells * c->nlambda;
+    if (nl) *nl = (size_t)c->labsStride * c->nlambda;
     if (ni) *ni = c->nInstrTally;
     return SKIRT_OK;
 }
 
 static int ensureTallies(SkirtMcrt* c) {
-    const size_t nl = (size_t)c->ncells * c->nlambda;
+    const size_t nl = (size_t)c->labsStride * c->nlambda;
     if (!c->dLabs && nl) {
         HIPCHECK(c, hipMalloc(&c->dLabs, nl * sizeof(double)));
         HIPCHECK(c, hipMemsetAsync(c->dLabs, 0, nl * sizeof(double), c->stream));
@@ -2498,7 +2534,7 @@ int skirt_mcrt_zero_tallies(SkirtMcrt* c) {
     HIPCHECK(c, hipSetDevice(c->device));
     int rc = ensureTallies(c);
     if (rc) return rc;
-    const size_t nl = (size_t)c->ncells * c->nlambda;
+    const size_t nl = (size_t)c->labsStride * c->nlambda;
     if (c->dLabs && nl) HIPCHECK(c, hipMemsetAsync(c->dLabs, 0, nl * sizeof(double), c->stream));
     if (c->dTally && c->nInstrTally) HIPCHECK(c, hipMemsetAsync(c->dTally, 0, c->nInstrTally * sizeof(double), c->stream));
     HIPCHECK(c, hipMemsetAsync(c->dStats, 0, 8 * kStatCopies * sizeof(unsigned long long), c->stream));
@@ -2534,7 +2570,7 @@ static int ensureDustLabs(SkirtMcrt* c);
 static int ensureEmisScratch(SkirtMcrt* c) {
     if (c->dEmisScratch) return SKIRT_OK;
     const size_t nb = (size_t)c->nlambda * (((size_t)c->ncells + kBlock - 1) / kBlock);
-    const size_t nbAll = ((size_t)c->ncells * c->nlambda + kBlock - 1) / kBlock;
+    const size_t nbAll = ((size_t)c->labsStride * c->nlambda + kBlock - 1) / kBlock;
     HIPCHECK(c, hipMalloc(&c->dEmisScratch, (std::max(nb, nbAll) + 2) * sizeof(double)));
     return SKIRT_OK;
 }
@@ -2582,7 +2618,7 @@ int skirt_mcrt_compute_cell_sources(SkirtMcrt* c, int include_dust) {
         (rc = alloc(c->dCellLtot, (size_t)Nl)) || (rc = ensureEmisScratch(c)))
         return rc;
     EmisArgs e{};
-    e.ncells = N; e.nlambda = Nl; e.ncomp = c->ncomp; e.ntemp = c->emisNtemp;
+    e.ncells = N; e.nlambda = Nl; e.ncomp = c->ncomp; e.ntemp = c->emisNtemp; e.labsStride = c->labsStride;
     e.devCell = c->devCell.empty() ? nullptr : c->dDevCell;
     e.labs = c->dLabs; e.labsDust = include_dust ? c->dLabsDust : nullptr;
     e.rho = c->dRho; e.volume = c->dEmisVolume; e.kabs = c->dEmisKabs; e.sigmaabs = c->dEmisSigma; e.mu = c->dEmisMu;
@@ -2601,7 +2637,7 @@ int skirt_mcrt_dust_labs_total(SkirtMcrt* c, double* total) {
     HIPCHECK(c, hipSetDevice(c->device));
     int rc = ensureDustLabs(c);
     if (rc) return rc;
-    const size_t n = (size_t)c->ncells * c->nlambda;
+    const size_t n = (size_t)c->labsStride * c->nlambda;  // unused device cells hold zeros
     if ((rc = ensureEmisScratch(c))) return rc;
     // reuse the cell-sum kernels on the dust table viewed as one "wavelength" of n cells
     EmisArgs e{};
@@ -2617,7 +2653,7 @@ int skirt_mcrt_dust_labs_total(SkirtMcrt* c, double* total) {
 }
 
 static int ensureDustLabs(SkirtMcrt* c) {
-    const size_t nl = (size_t)c->ncells * c->nlambda;
+    const size_t nl = (size_t)c->labsStride * c->nlambda;
     if (!c->dLabsDust && nl) {
         HIPCHECK(c, hipMalloc(&c->dLabsDust, nl * sizeof(double)));
         HIPCHECK(c, hipMemsetAsync(c->dLabsDust, 0, nl * sizeof(double), c->stream));
@@ -2639,7 +2675,7 @@ int skirt_mcrt_zero_dust_labs(SkirtMcrt* c) {
     HIPCHECK(c, hipSetDevice(c->device));
     int rc = ensureDustLabs(c);
     if (rc) return rc;
-    const size_t nl = (size_t)c->ncells * c->nlambda;
+    const size_t nl = (size_t)c->labsStride * c->nlambda;
     if (nl) HIPCHECK(c, hipMemsetAsync(c->dLabsDust, 0, nl * sizeof(double), c->stream));
     return SKIRT_OK;
 }
@@ -2648,14 +2684,14 @@ int skirt_mcrt_download_dust_labs(SkirtMcrt* c, double* labs) {
     if (!c || !labs) return SKIRT_ERR_ARG;
     int rc = skirt_mcrt_synchronize(c);
     if (rc) return rc;
-    const size_t nl = (size_t)c->ncells * c->nlambda;
+    const size_t nl = (size_t)c->labsStride * c->nlambda;
     if (!c->dLabsDust) { std::fill(labs, labs + nl, 0.0); return SKIRT_OK; }
     std::vector<double> t(nl);
     HIPCHECK(c, hipMemcpy(t.data(), c->dLabsDust, nl * sizeof(double), hipMemcpyDeviceToHost));
     const bool perm = !c->devCell.empty();
     for (int ell = 0; ell < c->nlambda; ell++)
         for (int m = 0; m < c->ncells; m++)
-            labs[(size_t)m * c->nlambda + ell] = t[(size_t)ell * c->ncells + (perm ? c->devCell[m] : m)];
+            labs[(size_t)m * c->nlambda + ell] = t[(size_t)ell * c->labsStride + (perm ? c->devCell[m] : m)];
     return SKIRT_OK;
 }
 
@@ -2699,6 +2735,7 @@ int skirt_mcrt_run_phase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, 
 
     Args a{};
     a.ncells = c->ncells;
+    a.labsStride = c->labsStride;
     a.nx = c->nx; a.ny = c->ny; a.nz = c->nz;
     a.mesh = c->dMesh;
     a.gx0 = c->gx0; a.gx1 = c->gx1; a.gy0 = c->gy0; a.gy1 = c->gy1; a.gz0 = c->gz0; a.gz1 = c->gz1;
@@ -2734,7 +2771,7 @@ int skirt_mcrt_run_phase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, 
     a.store = phase == SKIRT_PHASE_STELLAR ? (p->store_absorption ? 1 : 0) : (phase == SKIRT_PHASE_DUST_SELFABS ? 1 : 0);
     a.hasDust = p->has_dust ? 1 : 0;
     if (a.store && !c->dLabs) return fail(c, SKIRT_ERR_STATE, "no Labs buffer");
-    if ((uint64_t)c->ncells * (uint64_t)c->nlambda >= (1ull << 32)) return fail(c, SKIRT_ERR_UNSUPPORTED, "Labs table exceeds 2^32 entries");
+    if ((uint64_t)c->labsStride * (uint64_t)c->nlambda >= (1ull << 32)) return fail(c, SKIRT_ERR_UNSUPPORTED, "Labs table exceeds 2^32 entries");
     a.labs = phase == SKIRT_PHASE_DUST_SELFABS ? c->dLabsDust : c->dLabs;
     a.tally = c->dTally;
     a.error = c->dError; a.stats = c->dStats;
@@ -2913,7 +2950,7 @@ int skirt_mcrt_download(SkirtMcrt* c, double* labs, double* instr) {
     if (!c) return SKIRT_ERR_ARG;
     int rc = skirt_mcrt_synchronize(c);
     if (rc) return rc;
-    const size_t nl = (size_t)c->ncells * c->nlambda;
+    const size_t nl = (size_t)c->labsStride * c->nlambda;
     if (labs && nl) {
         if (!c->dLabs) return fail(c, SKIRT_ERR_STATE, "no Labs buffer");
         std::vector<double> t(nl);
@@ -2921,7 +2958,7 @@ int skirt_mcrt_download(SkirtMcrt* c, double* labs, double* instr) {
         const bool perm = !c->devCell.empty();
         for (int ell = 0; ell < c->nlambda; ell++)
             for (int m = 0; m < c->ncells; m++)
-                labs[(size_t)m * c->nlambda + ell] = t[(size_t)ell * c->ncells + (perm ? c->devCell[m] : m)];
+                labs[(size_t)m * c->nlambda + ell] = t[(size_t)ell * c->labsStride + (perm ? c->devCell[m] : m)];
     }
     if (instr && c->nInstrTally) {
         if (!c->dTally) return fail(c, SKIRT_ERR_STATE, "no instrument buffer");
@@ -2952,6 +2989,8 @@ int skirt_mcrt_stats(SkirtMcrt* c, SkirtStats* out) {
     out->trace_launches = c->traceLaunchesTotal;
     out->grid_walk = c->lastWalk;
     out->map_level = c->mapL;
+    out->labs_requests = v[7];
+    out->device_cells = c->ndev;
     return SKIRT_OK;
 }
 
