@@ -696,6 +696,7 @@ struct LeafMapGrid {
         const double lo = T[j], hi = T[j + 1];
         if (v < lo) {
             do j--; while (j > 0 && v < T[j]);
+            j = max(j, 0);  // v below T[0]: a point outside the grid, whose entry is fetched but not used
         } else if (v >= hi && j < N - 1) {
             do j++; while (j < N - 1 && v >= T[j + 1]);
         }
@@ -706,15 +707,19 @@ struct LeafMapGrid {
         return x >= a.gx0 && x <= a.gx1 && y >= a.gy0 && y <= a.gy1 && z >= a.gz0 && z <= a.gz1;
     }
 
-    // leaf map entry of the point (inside the grid); fx, fy, fz its finest-level indices
-    __device__ static __forceinline__ LeafEntry lookup(const Args& a, const Shared& sh, double x, double y, double z,
-                                                       int& fx, int& fy, int& fz) {
+    // issues the load of the leaf map entry of the point (clamped into the grid, so any point -- even
+    // NaN -- reads a valid entry); fx, fy, fz its finest-level indices
+    __device__ static __forceinline__ int4 fetch(const Args& a, const Shared& sh, double x, double y, double z,
+                                                 int& fx, int& fy, int& fz) {
         const int N = a.mapN;
         const double* tx = sh.mesh;
         fx = finest(tx, N, a.mapInvX, x);
         fy = finest(tx + (N + 1), N, a.mapInvY, y);
         fz = finest(tx + 2 * (N + 1), N, a.mapInvZ, z);
-        int4 v = *reinterpret_cast<const int4*>(a.leafMap + morton3(fx, fy, fz));
+        return *reinterpret_cast<const int4*>(a.leafMap + morton3(fx, fy, fz));
+    }
+
+    __device__ static __forceinline__ LeafEntry decode(int4 v) {
         // one 16-byte load: keep the compiler from splitting off the density into a later second load
         asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w));
         LeafEntry e;
@@ -723,6 +728,12 @@ struct LeafMapGrid {
         const long long bits = ((long long)(unsigned)v.w << 32) | (unsigned)v.z;
         e.rho0 = __longlong_as_double(bits);
         return e;
+    }
+
+    // leaf map entry of the point (inside the grid); fx, fy, fz its finest-level indices
+    __device__ static __forceinline__ LeafEntry lookup(const Args& a, const Shared& sh, double x, double y, double z,
+                                                       int& fx, int& fy, int& fz) {
+        return decode(fetch(a, sh, x, y, z, fx, fy, fz));
     }
 
     // r.ck: the leaf's size in finest cells (octree) or its packed shifts (k-d tree)
@@ -772,13 +783,16 @@ struct LeafMapGrid {
         if (dsx <= dsy && dsx <= dsz) { ds = dsx; wall = (r.dx < 0.0) ? 0 : 1; }
         else if (dsy <= dsx && dsy <= dsz) { ds = dsy; wall = (r.dy < 0.0) ? 2 : 3; }
         else { ds = dsz; wall = (r.dz < 0.0) ? 4 : 5; }
-        if (!seg(r.cj, r.rho0, ds)) return false;
         double x = r.x + (ds + a.eps) * r.dx;
         double y = r.y + (ds + a.eps) * r.dy;
         double z = r.z + (ds + a.eps) * r.dz;
-        if (!inside(a, x, y, z)) return false;  // no neighbour and no root descent contains it
+        // the next leaf's entry is requested first; the segment's own work (optical depth, absorption)
+        // runs while the load is in flight
         int fx, fy, fz;
-        LeafEntry e = lookup(a, sh, x, y, z, fx, fy, fz);
+        const int4 raw = fetch(a, sh, x, y, z, fx, fy, fz);
+        if (!seg(r.cj, r.rho0, ds)) return false;
+        if (!inside(a, x, y, z)) return false;  // no neighbour and no root descent contains it
+        LeafEntry e = decode(raw);
         int lx, ly, lz;
         shifts(a, e.cl, lx, ly, lz);
         if (e.node == r.ci || x == tx[(fx >> lx) << lx] || y == ty[(fy >> ly) << ly] || z == tz[(fz >> lz) << lz]) {
