@@ -132,6 +132,7 @@ constexpr int kOctreeBookkeeping = 18;  // octree, Bookkeeping search (node arra
 struct Args {
     // grid
     int nx, ny, nz, ncells;
+    int brick;                   // Cartesian: device cells numbered in 2x2x2 bricks (see Grid<CARTESIAN>::dev)
     int labsStride;              // Labs row length (device cells, padded to a 64-byte line)
     const double* mesh;          // Cartesian borders x | y | z (staged in LDS)
     double gx0, gx1, gy0, gy1, gz0, gz1;
@@ -390,6 +391,16 @@ struct Grid<SKIRT_GRID_CARTESIAN> {
         return true;
     }
 
+    // device number of cell (i, j, k). Bricked: the 8 cells of each 2x2x2 brick are consecutive and
+    // start on a 64-byte line of every Labs row (a ray crosses about 2.5 cells of a brick it enters,
+    // whose Labs adds then share one atomic request); bricks in the reference's (i, j, k) order.
+    // Unbricked: the reference's index k + Nz j + Nz Ny i (CartesianDustGrid.cpp:305-308).
+    __device__ static __forceinline__ int dev(const Args& a, int i, int j, int k) {
+        if (!a.brick) return k + a.nz * j + a.nz * a.ny * i;
+        const int by = (a.ny + 1) >> 1, bz = (a.nz + 1) >> 1;
+        return ((((i >> 1) * by + (j >> 1)) * bz + (k >> 1)) << 3) | ((i & 1) << 2) | ((j & 1) << 1) | (k & 1);
+    }
+
     // one grid step: emits (m, ds); false when the ray ends (left the grid or stopped by seg)
     template <class SegFn>
     __device__ static __forceinline__ bool step(const Args& a, const Shared& sh, Ray& r, SegFn seg) {
@@ -397,7 +408,7 @@ struct Grid<SKIRT_GRID_CARTESIAN> {
         const double* yv = xv + a.nx + 1;
         const double* zv = yv + a.ny + 1;
         const int i = r.ci, j = r.cj, k = r.ck;
-        const int m = k + a.nz * j + a.nz * a.ny * i;
+        const int m = dev(a, i, j, k);
         const double rho0 = a.rho[(size_t)m * a.ncomp];
         const double xE = (r.dx < 0.0) ? xv[i] : xv[i + 1];
         const double yE = (r.dy < 0.0) ? yv[j] : yv[j + 1];
@@ -434,7 +445,7 @@ struct Grid<SKIRT_GRID_CARTESIAN> {
         const double* zv = yv + a.ny + 1;
         const int i = locateFail(xv, a.nx + 1, x), j = locateFail(yv, a.ny + 1, y), k = locateFail(zv, a.nz + 1, z);
         if (i < 0 || j < 0 || k < 0) return -1;
-        return k + a.nz * j + a.nz * a.ny * i;
+        return dev(a, i, j, k);
     }
 };
 
@@ -1948,6 +1959,7 @@ struct SkirtMcrt {
     // group of 8 sibling leaves starts on a 64-byte line), Labs rows of labsStride (ndev rounded up to 8)
     int ndev = 0;
     int labsStride = 0;
+    bool brick = false;  // Cartesian cells numbered in 2x2x2 bricks
     double eps = 0, gx0 = 0, gx1 = 0, gy0 = 0, gy1 = 0, gz0 = 0, gz1 = 0;
     double* dMesh = nullptr;
     double* dBox = nullptr;
@@ -2211,6 +2223,7 @@ int skirt_mcrt_upload_grid(SkirtMcrt* c, const SkirtGridDesc* g) {
     HIPCHECK(c, hipSetDevice(c->device));
     c->ncells = g->ncells;
     c->ndev = g->ncells;
+    c->brick = false;
     c->devCell.clear();
     if (g->kind == SKIRT_GRID_CARTESIAN) {
         if (g->nx < 1 || g->ny < 1 || g->nz < 1 || !g->xv || !g->yv || !g->zv) return fail(c, SKIRT_ERR_ARG, "bad Cartesian grid");
@@ -2223,6 +2236,21 @@ int skirt_mcrt_upload_grid(SkirtMcrt* c, const SkirtGridDesc* g) {
         for (int i = 0; i < g->ny; i++) if (!(g->yv[i] < g->yv[i + 1])) return fail(c, SKIRT_ERR_ARG, "y mesh not increasing");
         for (int i = 0; i < g->nz; i++) if (!(g->zv[i] < g->zv[i + 1])) return fail(c, SKIRT_ERR_ARG, "z mesh not increasing");
         c->nx = g->nx; c->ny = g->ny; c->nz = g->nz;
+        // device numbers in 2x2x2 bricks (Grid<SKIRT_GRID_CARTESIAN>::dev); SKIRT_AMD_CELL_ALIGN=0: the
+        // reference's numbering
+        const char* alignEnv = getenv("SKIRT_AMD_CELL_ALIGN");
+        c->brick = !(alignEnv && alignEnv[0] == '0');
+        if (c->brick) {
+            const long long bx = (g->nx + 1) / 2, by = (g->ny + 1) / 2, bz = (g->nz + 1) / 2;
+            if (8 * bx * by * bz >= (1ll << 31)) return fail(c, SKIRT_ERR_UNSUPPORTED, "Cartesian grid too large");
+            c->devCell.assign(g->ncells, 0);
+            for (int i = 0; i < g->nx; i++)
+                for (int j = 0; j < g->ny; j++)
+                    for (int k = 0; k < g->nz; k++)
+                        c->devCell[k + g->nz * j + g->nz * g->ny * i] =
+                            (int)((((i >> 1) * by + (j >> 1)) * bz + (k >> 1)) << 3) | ((i & 1) << 2) | ((j & 1) << 1) | (k & 1);
+            c->ndev = (int)(8 * bx * by * bz);
+        }
         c->gx0 = g->xv[0]; c->gx1 = g->xv[g->nx];
         c->gy0 = g->yv[0]; c->gy1 = g->yv[g->ny];
         c->gz0 = g->zv[0]; c->gz1 = g->zv[g->nz];
@@ -2751,6 +2779,7 @@ int skirt_mcrt_run_phase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, 
     a.ncells = c->ncells;
     a.labsStride = c->labsStride;
     a.nx = c->nx; a.ny = c->ny; a.nz = c->nz;
+    a.brick = c->brick ? 1 : 0;
     a.mesh = c->dMesh;
     a.gx0 = c->gx0; a.gx1 = c->gx1; a.gy0 = c->gy0; a.gy1 = c->gy1; a.gz0 = c->gz0; a.gz1 = c->gz1;
     a.box = c->dBox; a.firstChild = c->dFirstChild; a.cellnumber = c->dCellnumber;
