@@ -157,6 +157,7 @@ struct Args {
     const double* treeT;         // octree split coordinates per axis, 3 x (mapN + 1) (staged in LDS)
     int mapL, mapN;              // leaf map depth and 2^depth
     double mapInvX, mapInvY, mapInvZ;
+    double mapX0, mapY0, mapZ0;  // T[0] of each axis (the root box's lower corner)
     // media
     int ncomp, nlambda;
     const double* rho;
@@ -702,8 +703,10 @@ struct LeafMapGrid {
     // finest-level index j with T[j] <= v < T[j+1] (the last cell also holds v == T[N]); v in [T[0], T[N]].
     // The split coordinates are uniform to rounding, so the estimate is off by one at most near a
     // split; the loops only run for that rare lane.
-    __device__ static __forceinline__ int finest(const double* T, int N, double inv, double v) {
-        int j = max(0, min(N - 1, (int)((v - T[0]) * inv)));
+    __device__ static __forceinline__ int estimate(int N, double t0, double inv, double v) {
+        return max(0, min(N - 1, (int)((v - t0) * inv)));
+    }
+    __device__ static __forceinline__ int correct(const double* T, int N, int j, double v) {
         const double lo = T[j], hi = T[j + 1];
         if (v < lo) {
             do j--; while (j > 0 && v < T[j]);
@@ -719,15 +722,22 @@ struct LeafMapGrid {
     }
 
     // issues the load of the leaf map entry of the point (clamped into the grid, so any point -- even
-    // NaN -- reads a valid entry); fx, fy, fz its finest-level indices
+    // NaN -- reads a valid entry); fx, fy, fz its finest-level indices. The entry of the estimated cell
+    // is requested before the estimate is checked against the T tables in LDS; the rare lane whose
+    // estimate was off by one requests the right entry again.
     __device__ static __forceinline__ int4 fetch(const Args& a, const Shared& sh, double x, double y, double z,
                                                  int& fx, int& fy, int& fz) {
         const int N = a.mapN;
         const double* tx = sh.mesh;
-        fx = finest(tx, N, a.mapInvX, x);
-        fy = finest(tx + (N + 1), N, a.mapInvY, y);
-        fz = finest(tx + 2 * (N + 1), N, a.mapInvZ, z);
-        return *reinterpret_cast<const int4*>(a.leafMap + morton3(fx, fy, fz));
+        const int ex = estimate(N, a.mapX0, a.mapInvX, x);
+        const int ey = estimate(N, a.mapY0, a.mapInvY, y);
+        const int ez = estimate(N, a.mapZ0, a.mapInvZ, z);
+        int4 v = *reinterpret_cast<const int4*>(a.leafMap + morton3(ex, ey, ez));
+        fx = correct(tx, N, ex, x);
+        fy = correct(tx + (N + 1), N, ey, y);
+        fz = correct(tx + 2 * (N + 1), N, ez, z);
+        if (fx != ex || fy != ey || fz != ez) v = *reinterpret_cast<const int4*>(a.leafMap + morton3(fx, fy, fz));
+        return v;
     }
 
     __device__ static __forceinline__ LeafEntry decode(int4 v) {
@@ -1975,6 +1985,7 @@ struct SkirtMcrt {
     // octree leaf map (mapL < 0: walk the node arrays)
     int mapL = -1, mapN = 0;
     double mapInv[3] = {0, 0, 0};
+    double mapOrigin[3] = {0, 0, 0};
     double* dTreeT = nullptr;
     LeafEntry* dLeafMap = nullptr;
     bool mapReady = false;
@@ -2155,6 +2166,7 @@ int planLeafMap(SkirtMcrt* c, const SkirtGridDesc* g) {
     c->mapL = L;
     c->mapN = N;
     for (int ax = 0; ax < 3; ax++) c->mapInv[ax] = N / (g->box[3 + ax] - g->box[ax]);
+    for (int ax = 0; ax < 3; ax++) c->mapOrigin[ax] = T[ax * (N + 1)];
     return SKIRT_OK;
 }
 
@@ -2795,6 +2807,7 @@ int skirt_mcrt_run_phase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, 
         if ((rc = ensureLeafMap(c))) return rc;
         a.leafMap = c->dLeafMap; a.treeT = c->dTreeT; a.mapL = c->mapL; a.mapN = c->mapN;
         a.mapInvX = c->mapInv[0]; a.mapInvY = c->mapInv[1]; a.mapInvZ = c->mapInv[2];
+        a.mapX0 = c->mapOrigin[0]; a.mapY0 = c->mapOrigin[1]; a.mapZ0 = c->mapOrigin[2];
     }
     a.ncomp = std::max(1, c->ncomp); a.nlambda = c->nlambda;
     a.rho = c->dRho;
