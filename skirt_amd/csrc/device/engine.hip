@@ -438,7 +438,7 @@ struct Grid<SKIRT_GRID_CARTESIAN> {
         return true;
     }
 
-    __device__ static __forceinline__ void resume(const Args&, Ray&) {}
+    __device__ static __forceinline__ void resume(const Args&, const Shared&, Ray&) {}
 
     __device__ static __forceinline__ int whichcell(const Args& a, const Shared& sh, double x, double y, double z) {
         const double* xv = sh.mesh;
@@ -581,7 +581,7 @@ struct Grid<kOctreeNodes> {
         return true;
     }
 
-    __device__ static __forceinline__ void resume(const Args& a, Ray& r) {
+    __device__ static __forceinline__ void resume(const Args& a, const Shared&, Ray& r) {
         loadBox(a, r.ci, r.bx0, r.by0, r.bz0, r.bx1, r.by1, r.bz1);
     }
 
@@ -604,7 +604,7 @@ struct Grid<kOctreeBookkeeping> {
     __device__ static __forceinline__ bool begin(const Args& a, const Shared& sh, Ray& r, SegFn seg) {
         return Nodes::begin(a, sh, r, seg);
     }
-    __device__ static __forceinline__ void resume(const Args& a, Ray& r) { Nodes::resume(a, r); }
+    __device__ static __forceinline__ void resume(const Args& a, const Shared& sh, Ray& r) { Nodes::resume(a, sh, r); }
     __device__ static __forceinline__ int whichcell(const Args& a, const Shared& sh, double x, double y, double z) {
         return Nodes::whichcell(a, sh, x, y, z);
     }
@@ -757,17 +757,31 @@ struct LeafMapGrid {
         return decode(fetch(a, sh, x, y, z, fx, fy, fz));
     }
 
-    // r.ck: the leaf's size in finest cells (octree) or its packed shifts (k-d tree)
-    __device__ static __forceinline__ void enter(const Args& a, Ray& r, int fx, int fy, int fz, const LeafEntry& e) {
-        int sx, sy, sz;
-        shifts(a, e.cl, sx, sy, sz);
+    // r.ck: the leaf's size in finest cells (octree) or its packed shifts (k-d tree); r.bx0, r.by0,
+    // r.bz0: the leaf's faces the ray leaves through along x, y, z (read from the T tables once, when
+    // the leaf is entered, so the next step starts without an LDS round trip)
+    __device__ static __forceinline__ void enterPlanes(Ray& r, int jx, int jy, int jz, const LeafEntry& e,
+                                                       double lox, double loy, double loz,
+                                                       double hix, double hiy, double hiz) {
         r.ci = e.node;
         r.cj = cellOf(e.cl);
-        r.ck = BIN ? (int)(e.cl >> kBinCellBits) : 1 << sx;
-        r.jx = (fx >> sx) << sx;
-        r.jy = (fy >> sy) << sy;
-        r.jz = (fz >> sz) << sz;
+        if (BIN) r.ck = (int)(e.cl >> kBinCellBits);
+        r.jx = jx; r.jy = jy; r.jz = jz;
         r.rho0 = e.rho0;
+        r.bx0 = (r.dx < 0.0) ? lox : hix;
+        r.by0 = (r.dy < 0.0) ? loy : hiy;
+        r.bz0 = (r.dz < 0.0) ? loz : hiz;
+    }
+    __device__ static __forceinline__ void enter(const Args& a, const Shared& sh, Ray& r, int fx, int fy, int fz,
+                                                 const LeafEntry& e) {
+        const int N1 = a.mapN + 1;
+        const double* tx = sh.mesh;
+        int sx, sy, sz;
+        shifts(a, e.cl, sx, sy, sz);
+        const int jx = (fx >> sx) << sx, jy = (fy >> sy) << sy, jz = (fz >> sz) << sz;
+        enterPlanes(r, jx, jy, jz, e, tx[jx], tx[N1 + jy], tx[2 * N1 + jz], tx[jx + (1 << sx)],
+                    tx[N1 + jy + (1 << sy)], tx[2 * N1 + jz + (1 << sz)]);
+        if (!BIN) r.ck = 1 << sx;
     }
 
     template <class SegFn>
@@ -780,7 +794,7 @@ struct LeafMapGrid {
         int fx, fy, fz;
         const LeafEntry e = lookup(a, sh, rx, ry, rz, fx, fy, fz);
         r.x = rx; r.y = ry; r.z = rz;
-        enter(a, r, fx, fy, fz, e);
+        enter(a, sh, r, fx, fy, fz, e);
         return true;
     }
 
@@ -790,12 +804,7 @@ struct LeafMapGrid {
         const double* tx = sh.mesh;
         const double* ty = tx + N1;
         const double* tz = ty + N1;
-        const int ex = BIN ? 1 << (r.ck & 7) : r.ck;
-        const int ey = BIN ? 1 << ((r.ck >> 3) & 7) : r.ck;
-        const int ez = BIN ? 1 << ((r.ck >> 6) & 7) : r.ck;
-        const double xnext = tx[(r.dx < 0.0) ? r.jx : r.jx + ex];
-        const double ynext = ty[(r.dy < 0.0) ? r.jy : r.jy + ey];
-        const double znext = tz[(r.dz < 0.0) ? r.jz : r.jz + ez];
+        const double xnext = r.bx0, ynext = r.by0, znext = r.bz0;
         const double dsx = (r.ix != 0.0) ? (xnext - r.x) * r.ix : kDblMax;
         const double dsy = (r.iy != 0.0) ? (ynext - r.y) * r.iy : kDblMax;
         const double dsz = (r.iz != 0.0) ? (znext - r.z) * r.iz : kDblMax;
@@ -816,19 +825,37 @@ struct LeafMapGrid {
         LeafEntry e = decode(raw);
         int lx, ly, lz;
         shifts(a, e.cl, lx, ly, lz);
-        if (e.node == r.ci || x == tx[(fx >> lx) << lx] || y == ty[(fy >> ly) << ly] || z == tz[(fz >> lz) << lz]) {
+        const int jx = (fx >> lx) << lx, jy = (fy >> ly) << ly, jz = (fz >> lz) << lz;
+        // the new leaf's six faces in one LDS round trip: the lower ones decide whether the exit point
+        // lies on a face, the ones ahead of the ray are the next step's exit planes
+        const double lox = tx[jx], loy = ty[jy], loz = tz[jz];
+        const double hix = tx[jx + (1 << lx)], hiy = ty[jy + (1 << ly)], hiz = tz[jz + (1 << lz)];
+        r.x = x; r.y = y; r.z = z;
+        if (e.node == r.ci || x == lox || y == loy || z == loz) {
             // on a face, or not out of the current leaf: the reference's own search decides
             const int next = Nodes::nextNode(a, r.ci, wall, x, y, z, r.dx, r.dy, r.dz);
             if (next < 0) return false;
             const double* b = a.box + 6 * (size_t)next;  // its lower corner is a finest cell of it
             e = lookup(a, sh, b[0], b[1], b[2], fx, fy, fz);
+            enter(a, sh, r, fx, fy, fz, e);
+            return true;
         }
-        r.x = x; r.y = y; r.z = z;
-        enter(a, r, fx, fy, fz, e);
+        enterPlanes(r, jx, jy, jz, e, lox, loy, loz, hix, hiy, hiz);
+        if (!BIN) r.ck = 1 << lx;
         return true;
     }
 
-    __device__ static __forceinline__ void resume(const Args&, Ray&) {}
+    // a ray record carries its entry leaf (ci, cj, ck, jx, jy, jz): its exit planes from the T tables
+    __device__ static __forceinline__ void resume(const Args& a, const Shared& sh, Ray& r) {
+        const int N1 = a.mapN + 1;
+        const double* tx = sh.mesh;
+        const int ex = BIN ? 1 << (r.ck & 7) : r.ck;
+        const int ey = BIN ? 1 << ((r.ck >> 3) & 7) : r.ck;
+        const int ez = BIN ? 1 << ((r.ck >> 6) & 7) : r.ck;
+        r.bx0 = tx[(r.dx < 0.0) ? r.jx : r.jx + ex];
+        r.by0 = tx[N1 + ((r.dy < 0.0) ? r.jy : r.jy + ey)];
+        r.bz0 = tx[2 * N1 + ((r.dz < 0.0) ? r.jz : r.jz + ez)];
+    }
 
     __device__ static __forceinline__ int whichcell(const Args& a, const Shared& sh, double x, double y, double z) {
         if (!inside(a, x, y, z)) return -1;
@@ -942,7 +969,7 @@ struct Grid<SKIRT_GRID_VORONOI> {
         return mq >= 0;
     }
 
-    __device__ static __forceinline__ void resume(const Args&, Ray&) {}
+    __device__ static __forceinline__ void resume(const Args&, const Shared&, Ray&) {}
 
     __device__ static __forceinline__ int whichcell(const Args& a, const Shared&, double x, double y, double z) {
         return cellIndex(a, x, y, z);
@@ -1081,7 +1108,7 @@ struct Tracer {
         // FILL: f1 = exp(-tau) = 1, f2 = scattered luminosity; WALK: tau and s at the last segment end
         r.f1 = (r.mode == RAY_FILL) ? 1.0 : 0.0;
         r.f2 = (r.mode == RAY_WALK) ? c4.y : 0.0;
-        if (r.mode != RAY_NONE) Grid<GRID>::resume(a, r);
+        if (r.mode != RAY_NONE) Grid<GRID>::resume(a, sh, r);
     }
 
     // the ray ended (grid edge or WALK target reached): deliver its result
