@@ -2808,8 +2808,11 @@ int skirt_mcrt_run_phase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, 
         std::vector<double> z(4 * (size_t)c->nlambda, 0.0);
         if ((rc = upload(c, c->dOptics, z.data(), z.size()))) return rc;
     }
-    // slot pool: enough packets in flight to fill the chip many times over, bounded by the phase size
-    int slots = c->slotsWanted > 0 ? c->slotsWanted : (1 << 21);
+    // slot pool: enough packets in flight to fill the chip many times over, bounded by the phase size.
+    // 2^23 slots (3.3 GB of packet state and ray queues with one instrument) make each iteration's trace
+    // launch long enough that its drain tail and the event kernel amortise (C3: 2^21 slots 1.87e8 pkt/s,
+    // 2^22 1.98e8, 2^23 2.04e8, 2^24 2.05e8; tools/gpu_sweep3.sh)
+    int slots = c->slotsWanted > 0 ? c->slotsWanted : (1 << 23);
     if ((uint64_t)slots > count) slots = (int)count;
     slots = std::max(slots, 64 * kHalves) / kHalves;  // per half
     if ((rc = ensurePool(c, slots))) return rc;
