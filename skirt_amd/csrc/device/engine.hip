@@ -237,6 +237,25 @@ __host__ __device__ __forceinline__ unsigned morton3(unsigned x, unsigned y, uns
     return spread3(x) | (spread3(y) << 1) | (spread3(z) << 2);
 }
 
+// Leaf map order of the finest-level cells of an N^3 map (N = 2^L): 2x2x2 bricks of 8 consecutive
+// 16-byte entries (one 128-byte line), the bricks in (x, y, z) row-major order. Per line the same
+// neighbourhood as Morton order, at a few integer operations instead of three bit spreads per step.
+// (SKIRT_LEAF_MORTON: full Morton order.)
+__host__ __device__ __forceinline__ unsigned leafBricks(int N) { return (unsigned)((N + 1) >> 1); }
+__host__ __device__ __forceinline__ unsigned leafIndex(int N, unsigned x, unsigned y, unsigned z) {
+#ifdef SKIRT_LEAF_MORTON
+    (void)N;
+    return morton3(x, y, z);
+#else
+    const unsigned nb = leafBricks(N);
+    return ((((x >> 1) * nb + (y >> 1)) * nb + (z >> 1)) << 3) | ((x & 1u) << 2) | ((y & 1u) << 1) | (z & 1u);
+#endif
+}
+__host__ __device__ __forceinline__ unsigned long long leafMapSize(int N) {
+    const unsigned long long nb = leafBricks(N);
+    return 8ull * nb * nb * nb;
+}
+
 __device__ __forceinline__ void atomicAddF64(double* p, double v) {
     // explicit global address space: global_atomic_add_f64 instead of a flat atomic
     __hip_atomic_fetch_add((__attribute__((address_space(1))) double*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -732,11 +751,11 @@ struct LeafMapGrid {
         const int ex = estimate(N, a.mapX0, a.mapInvX, x);
         const int ey = estimate(N, a.mapY0, a.mapInvY, y);
         const int ez = estimate(N, a.mapZ0, a.mapInvZ, z);
-        int4 v = *reinterpret_cast<const int4*>(a.leafMap + morton3(ex, ey, ez));
+        int4 v = *reinterpret_cast<const int4*>(a.leafMap + leafIndex(N, ex, ey, ez));
         fx = correct(tx, N, ex, x);
         fy = correct(tx + (N + 1), N, ey, y);
         fz = correct(tx + 2 * (N + 1), N, ez, z);
-        if (fx != ex || fy != ey || fz != ez) v = *reinterpret_cast<const int4*>(a.leafMap + morton3(fx, fy, fz));
+        if (fx != ex || fy != ey || fz != ez) v = *reinterpret_cast<const int4*>(a.leafMap + leafIndex(N, fx, fy, fz));
         return v;
     }
 
@@ -1310,15 +1329,26 @@ __global__ void __launch_bounds__(kBlock) cellCdfKernel(const EmisArgs e) {
 // (a k-d tree by the bit of its split axis at that axis' depth)
 __global__ void __launch_bounds__(kBlock) buildLeafMapKernel(LeafEntry* map, const int* firstChild, const signed char* splitDir,
                                                              const int* cellnumber, const double* rho, int ncomp, int L) {
-    const unsigned long long n = 1ull << (3 * L);
+    const int N = 1 << L;
+    const unsigned long long n = leafMapSize(N);
     for (unsigned long long q = blockIdx.x * (unsigned long long)blockDim.x + threadIdx.x; q < n;
          q += (unsigned long long)gridDim.x * blockDim.x) {
         unsigned fx = 0, fy = 0, fz = 0;
+#ifdef SKIRT_LEAF_MORTON
         for (int b = 0; b < L; b++) {  // inverse Morton
             fx |= (unsigned)((q >> (3 * b)) & 1u) << b;
             fy |= (unsigned)((q >> (3 * b + 1)) & 1u) << b;
             fz |= (unsigned)((q >> (3 * b + 2)) & 1u) << b;
         }
+#else
+        {  // inverse of leafIndex
+            const unsigned long long nb = leafBricks(N), br = q >> 3;
+            fx = (unsigned)(2 * (br / (nb * nb)) + ((q >> 2) & 1u));
+            fy = (unsigned)(2 * ((br / nb) % nb) + ((q >> 1) & 1u));
+            fz = (unsigned)(2 * (br % nb) + (q & 1u));
+            fx = min(fx, (unsigned)N - 1u); fy = min(fy, (unsigned)N - 1u); fz = min(fz, (unsigned)N - 1u);
+        }
+#endif
         int node = 0, level = 0;
         LeafEntry e;
         if (splitDir) {
@@ -2199,7 +2229,7 @@ int planLeafMap(SkirtMcrt* c, const SkirtGridDesc* g) {
 
 int ensureLeafMap(SkirtMcrt* c) {
     if (c->mapL < 0 || c->mapReady) return SKIRT_OK;
-    const size_t n = (size_t)1 << (3 * c->mapL);
+    const size_t n = (size_t)leafMapSize(1 << c->mapL);
     if (!c->dLeafMap) HIPCHECK(c, hipMalloc(&c->dLeafMap, n * sizeof(LeafEntry)));
     const int blocks = (int)std::min<size_t>((n + kBlock - 1) / kBlock, 65536);
     hipLaunchKernelGGL(buildLeafMapKernel, dim3(blocks), dim3(kBlock), 0, c->stream, c->dLeafMap, c->dFirstChild,
