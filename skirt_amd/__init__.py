@@ -185,7 +185,7 @@ class Simulation:
         self._check(lib().skirt_sim_run_dust_sharded(self._h, rank, world, fn, None))
 
     def bind_dust_labs(self, ptr):
-        """Make the engine accumulate the dust Labs in caller device memory (ncells*nlambda doubles)."""
+        """Make the engine accumulate the dust Labs in caller device memory (tally_sizes()[0] doubles)."""
         self._check_engine(lib().skirt_mcrt_bind_dust_labs(self.engine, ctypes.c_void_p(ptr)))
 
     def labs_dust(self):

@@ -1091,14 +1091,59 @@ Model loadSki(const std::string& path, UniformSource& rng, const std::string& da
             g.zmin = attr(c, ge, "minZ", "length", 0);
             g.zmax = attr(c, ge, "maxZ", "length", 0);
             if (g.xmax <= g.xmin || g.ymax <= g.ymin || g.zmax <= g.zmin) throw std::runtime_error("invalid grid extent");
+            // the MoveableMesh of each axis on [0,1] (LinMesh.cpp, PowMesh.cpp, SymPowMesh.cpp; NR::lingrid,
+            // NR::powgrid, NR::sympowgrid, Fundamentals/NR.hpp:171-261), then
+            // _xv = mesh*(xmax-xmin) + xmin (CartesianDustGrid.cpp:34-36)
             auto mesh = [&](const char* prop, int& N, std::vector<double>& v, double lo, double hi) {
                 const XmlElement* me = need(ge, prop);
-                if (me->name != "LinMesh") throw std::runtime_error("unsupported mesh " + me->name);
                 N = attrInt(me, "numBins", 100);
-                // LinMesh::mesh() = NR::lingrid(tv, 0, 1, N); _xv = mesh*(xmax-xmin) + xmin
-                double dx = (1.0 - 0.0) / N;
+                if (N < 1) throw std::runtime_error("the number of mesh bins should be positive");
+                std::vector<double> tv(N + 1);
+                auto lingrid = [&](int n) {
+                    const double dx = (1.0 - 0.0) / n;
+                    for (int i = 0; i <= n; i++) tv[i] = 0.0 + i * dx;
+                };
+                if (me->name == "LinMesh") {
+                    lingrid(N);
+                } else if (me->name == "PowMesh" || me->name == "SymPowMesh") {
+                    const double ratio = attr(c, me, "ratio", "", 1.0);
+                    if (!(ratio > 0)) throw std::runtime_error("the bin width ratio should be positive");
+                    const bool sym = me->name == "SymPowMesh";
+                    if (sym ? N <= 2 : N <= 1) lingrid(N);
+                    else if (std::fabs(ratio - 1.) < 1e-3) lingrid(N);
+                    else if (!sym) {
+                        const double range = 1.0 - 0.0;
+                        const double q = std::pow(ratio, 1. / (N - 1));
+                        const double qn = std::pow(q, N);
+                        for (int i = 0; i <= N; ++i) tv[i] = 0.0 + (1. - std::pow(q, i)) / (1. - qn) * range;
+                    } else {
+                        const double xc = 0.5 * (0.0 + 1.0);
+                        if (N % 2 == 0) {
+                            const int M = N / 2;
+                            const double q = std::pow(ratio, 1.0 / (M - 1.0));
+                            const double qM = std::pow(q, M);
+                            tv[M] = xc;
+                            for (int i = 1; i <= M; ++i) {
+                                const double dxi = (1.0 - std::pow(q, i)) / (1.0 - qM) * 0.5 * (1.0 - 0.0);
+                                tv[M + i] = xc + dxi;
+                                tv[M - i] = xc - dxi;
+                            }
+                        } else {
+                            const int M = (N + 1) / 2;
+                            const double q = std::pow(ratio, 1.0 / (M - 1.0));
+                            const double qM = std::pow(q, M);
+                            for (int i = 1; i <= M; ++i) {
+                                const double dxi = (0.5 + 0.5 * q - std::pow(q, i)) / (0.5 + 0.5 * q - qM) * 0.5 * (1.0 - 0.0);
+                                tv[M - 1 + i] = xc + dxi;
+                                tv[M - i] = xc - dxi;
+                            }
+                        }
+                    }
+                } else {
+                    throw std::runtime_error("unsupported mesh " + me->name);
+                }
                 v.resize(N + 1);
-                for (int i = 0; i <= N; i++) v[i] = (0.0 + i * dx) * (hi - lo) + lo;
+                for (int i = 0; i <= N; i++) v[i] = tv[i] * (hi - lo) + lo;
             };
             mesh("meshX", g.Nx, g.xv, g.xmin, g.xmax);
             mesh("meshY", g.Ny, g.yv, g.ymin, g.ymax);

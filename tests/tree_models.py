@@ -1,4 +1,4 @@
-"""Tree-grid variants of the golden models, written as .ski files for the tree tests.
+"""Grid variants of the golden models (tree grids, Cartesian meshes), written as .ski files for the tests.
 
 The reference fixtures cover the OctTreeDustGrid with centre splits and the Neighbor search
 (pan_oct). Its other tree grids -- BinTreeDustGrid (the k-d tree, Alternating or Barycenter split
@@ -43,6 +43,15 @@ GRIDS = {
                    'sampleCount="100" maxOpticalDepth="0" maxMassFraction="5e-4" maxDensDispFraction="0" barycentric="false"/>'),
     "oct_bary_bk": ("pan_oct", '<OctTreeDustGrid writeGrid="false" %s minLevel="1" maxLevel="6" searchMethod="Bookkeeping" '
                     'sampleCount="100" maxOpticalDepth="0" maxMassFraction="5e-4" maxDensDispFraction="0" barycentric="true"/>'),
+    # Cartesian grids on the Pan model of the pan_cart16 fixture: odd bin counts (the engine's 2x2x2
+    # device-cell bricks then have unused cells) and the power-law meshes (PowMesh, SymPowMesh with an
+    # odd and an even bin count)
+    "cart_odd": ("pan_cart16", '<CartesianDustGrid writeGrid="false" %s><meshX type="MoveableMesh"><LinMesh numBins="7"/></meshX>'
+                 '<meshY type="MoveableMesh"><LinMesh numBins="5"/></meshY><meshZ type="MoveableMesh"><LinMesh numBins="9"/></meshZ>'
+                 '</CartesianDustGrid>'),
+    "cart_pow": ("pan_cart16", '<CartesianDustGrid writeGrid="false" %s><meshX type="MoveableMesh"><PowMesh numBins="12" ratio="4"/></meshX>'
+                 '<meshY type="MoveableMesh"><SymPowMesh numBins="9" ratio="3"/></meshY>'
+                 '<meshZ type="MoveableMesh"><SymPowMesh numBins="10" ratio="0.2"/></meshZ></CartesianDustGrid>'),
 }
 
 
