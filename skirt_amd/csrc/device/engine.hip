@@ -61,9 +61,12 @@ constexpr int kStepsPerPull = SKIRT_STEPS_PER_PULL;  // grid steps between two r
 constexpr int kHalves = SKIRT_HALVES;
 constexpr int kPollEvery = 1;      // iterations between two counter copies of a half
 constexpr int kPollRing = 3;       // copies in flight per half (the host reads each kPollRing copies late)
-// occupancy attribute of the trace kernel (a build knob for tuning variants, tools/build_variant.sh)
+// occupancy attribute of the trace kernel (a build knob for tuning variants, tools/build_variant.sh):
+// 3 waves per SIMD, i.e. at most 168 VGPRs (the grid entry on the pull path would otherwise take the
+// octree kernel to 175 and 2 waves; C3 1.91e8 -> 2.15e8 pkt/s at 3). The Voronoi step needs 190 and
+// runs faster at 2 waves than spilling at 3.
 #ifndef SKIRT_TRACE_ATTR
-#define SKIRT_TRACE_ATTR
+#define SKIRT_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(GRID == SKIRT_GRID_VORONOI ? 2 : 3)))
 #endif
 #ifndef SKIRT_EVENT_ATTR
 #define SKIRT_EVENT_ATTR
@@ -84,21 +87,25 @@ enum State : int { S_NEW = 0, S_FILL = 2, S_WALK = 3 };
 // peel-off categories (which FullInstrument arrays a detection adds to, FullInstrument.cpp:115-171)
 enum PeelCat : unsigned { CAT_STAR_DIRECT = 0, CAT_STAR_SCATTERED = 1, CAT_DUST_DIRECT = 2, CAT_DUST_SCATTERED = 3 };
 
-// one queued ray, 128 bytes = 8 x 16-byte chunks. The event kernel writes it already entered into the
-// grid (the part of the path before the grid, the first cell and the reciprocal direction computed), so
-// the trace kernel starts stepping at once.
+// one queued ray, 112 bytes = 7 x 16-byte chunks, written by the event kernel with the reciprocal
+// direction computed. The trace kernel enters the grid when it pulls the ray (the path before the grid,
+// the first cell): that lookup then overlaps with the other lanes' steps instead of stalling the event
+// kernel, whose waves are few (2 per SIMD) and long. Voronoi rays are entered by the event kernel
+// (kEnterInEvent): s0 then holds the path length before the grid, ci/cj the first cell.
 struct __attribute__((aligned(16))) RayRec {
-    double x, y, z;        // c0-c1: entry point (inside the grid)
+    double x, y, z;        // c0-c1: start point
     double dx, dy, dz;     // c1-c2: direction
     double ix, iy, iz;     // c3-c4: 1/direction (0 where |k| <= 1e-15: that axis is never crossed)
-    double s0;             // c4: path length before the entry point; a finished PEEL ray: optical depth
-    double rho0;           // c5: density (component 0) of the entry cell
+    double s0;             // c4: path length before the grid (Voronoi) or 0; a finished PEEL ray: optical depth
+    double unused;         // c5
     double param;          // c5: FILL: packet luminosity L; WALK: optical depth to reach; PEEL: peel-off L
     int idx;               // c6: FILL/WALK: slot; PEEL: frame pixel (-1: none)
     unsigned flags;        // c6: mode | cat << 2 | instrument << 4 | scattering level << 10 | ell << 18
-    int ci, cj, ck, jx, jy, jz;  // c6-c7: grid position of the entry cell (see Ray)
+    int ci, cj;            // c6: Voronoi: first cell and where its neighbour list starts
 };
-static_assert(sizeof(RayRec) == 128, "ray record layout");
+static_assert(sizeof(RayRec) == 112, "ray record layout");
+template <int GRID>
+constexpr bool kEnterInEvent = GRID == SKIRT_GRID_VORONOI;
 __device__ __forceinline__ unsigned rayMode(unsigned f) { return f & 3u; }
 __device__ __forceinline__ unsigned rayCat(unsigned f) { return (f >> 2) & 3u; }
 __device__ __forceinline__ int rayInstr(unsigned f) { return (int)((f >> 4) & 63u); }
@@ -457,7 +464,6 @@ struct Grid<SKIRT_GRID_CARTESIAN> {
         return true;
     }
 
-    __device__ static __forceinline__ void resume(const Args&, const Shared&, Ray&) {}
 
     __device__ static __forceinline__ int whichcell(const Args& a, const Shared& sh, double x, double y, double z) {
         const double* xv = sh.mesh;
@@ -600,9 +606,6 @@ struct Grid<kOctreeNodes> {
         return true;
     }
 
-    __device__ static __forceinline__ void resume(const Args& a, const Shared&, Ray& r) {
-        loadBox(a, r.ci, r.bx0, r.by0, r.bz0, r.bx1, r.by1, r.bz1);
-    }
 
     __device__ static __forceinline__ int whichcell(const Args& a, const Shared&, double x, double y, double z) {
         const int l = descend(a, x, y, z);
@@ -623,7 +626,6 @@ struct Grid<kOctreeBookkeeping> {
     __device__ static __forceinline__ bool begin(const Args& a, const Shared& sh, Ray& r, SegFn seg) {
         return Nodes::begin(a, sh, r, seg);
     }
-    __device__ static __forceinline__ void resume(const Args& a, const Shared& sh, Ray& r) { Nodes::resume(a, sh, r); }
     __device__ static __forceinline__ int whichcell(const Args& a, const Shared& sh, double x, double y, double z) {
         return Nodes::whichcell(a, sh, x, y, z);
     }
@@ -864,18 +866,6 @@ struct LeafMapGrid {
         return true;
     }
 
-    // a ray record carries its entry leaf (ci, cj, ck, jx, jy, jz): its exit planes from the T tables
-    __device__ static __forceinline__ void resume(const Args& a, const Shared& sh, Ray& r) {
-        const int N1 = a.mapN + 1;
-        const double* tx = sh.mesh;
-        const int ex = BIN ? 1 << (r.ck & 7) : r.ck;
-        const int ey = BIN ? 1 << ((r.ck >> 3) & 7) : r.ck;
-        const int ez = BIN ? 1 << ((r.ck >> 6) & 7) : r.ck;
-        r.bx0 = tx[(r.dx < 0.0) ? r.jx : r.jx + ex];
-        r.by0 = tx[N1 + ((r.dy < 0.0) ? r.jy : r.jy + ey)];
-        r.bz0 = tx[2 * N1 + ((r.dz < 0.0) ? r.jz : r.jz + ez)];
-    }
-
     __device__ static __forceinline__ int whichcell(const Args& a, const Shared& sh, double x, double y, double z) {
         if (!inside(a, x, y, z)) return -1;
         int fx, fy, fz;
@@ -988,7 +978,6 @@ struct Grid<SKIRT_GRID_VORONOI> {
         return mq >= 0;
     }
 
-    __device__ static __forceinline__ void resume(const Args&, const Shared&, Ray&) {}
 
     __device__ static __forceinline__ int whichcell(const Args& a, const Shared&, double x, double y, double z) {
         return cellIndex(a, x, y, z);
@@ -1103,22 +1092,19 @@ struct Tracer {
         return true;
     }
 
-    // load queued ray `id` (already entered into the grid by the event kernel)
+    // load queued ray `id` and enter the grid: the part of the path before the grid (segments outside
+    // it, m = -1) and the first cell (DustGrid::path); an empty path finishes the ray at once
     __device__ __forceinline__ void load(Ray& r, unsigned id) {
         const double2* c = reinterpret_cast<const double2*>(a.rays + id);
         const double2 c0 = c[0], c1 = c[1], c2 = c[2], c3 = c[3], c4 = c[4], c5 = c[5];
         const int4 c6 = reinterpret_cast<const int4*>(c)[6];
-        const int4 c7 = reinterpret_cast<const int4*>(c)[7];
         r.id = id;
         r.x = c0.x; r.y = c0.y; r.z = c1.x;
         r.dx = c1.y; r.dy = c2.x; r.dz = c2.y;
         r.ix = c3.x; r.iy = c3.y; r.iz = c4.x;
-        r.rho0 = c5.x;
         r.param = c5.y;
         r.idx = c6.x;
         r.flags = (unsigned)c6.y;
-        r.ci = c6.z; r.cj = c6.w; r.ck = c7.x;
-        r.jx = c7.y; r.jy = c7.z; r.jz = c7.w;
         r.mode = rayMode(r.flags);
         r.ell = rayEll(r.flags);
         r.tau = 0;
@@ -1127,7 +1113,14 @@ struct Tracer {
         // FILL: f1 = exp(-tau) = 1, f2 = scattered luminosity; WALK: tau and s at the last segment end
         r.f1 = (r.mode == RAY_FILL) ? 1.0 : 0.0;
         r.f2 = (r.mode == RAY_WALK) ? c4.y : 0.0;
-        if (r.mode != RAY_NONE) Grid<GRID>::resume(a, sh, r);
+        if (kEnterInEvent<GRID>) {  // entered by the event kernel: the cell and its neighbour list
+            r.ci = c6.z;
+            r.cj = c6.w;
+        } else if (r.mode != RAY_NONE &&
+            !Grid<GRID>::begin(a, sh, r, [&](int m, double rho0, double ds) { return segment(r, m, rho0, ds); })) {
+            finish(r);  // FILL: tau = 0, no scattered luminosity; WALK: s = 0; PEEL: tau = 0
+            r.mode = RAY_NONE;
+        }
     }
 
     // the ray ended (grid edge or WALK target reached): deliver its result
@@ -1501,8 +1494,9 @@ struct Events {
 
     __device__ __forceinline__ double rho(int m, int h) const { return a.rho[(size_t)m * a.ncomp + h]; }
 
-    // queues ray `pos`: walks the part of the path before the grid (DustGrid::path up to the first
-    // cell) and stores the entered ray; an empty path is finished here and queued as RAY_NONE
+    // queues ray `pos`. The trace kernel enters the grid, except for Voronoi grids (kEnterInEvent): their
+    // cellIndex loops over a block's site list, which costs the trace kernel more than it costs here. A
+    // path found empty here (no dust system, or a Voronoi ray missing the grid) is finished here.
     __device__ __forceinline__ void emitRay(unsigned pos, const Packet& p, double dx, double dy, double dz, double prm,
                                             int idx, unsigned flags) {
         Ray r;
@@ -1512,18 +1506,20 @@ struct Events {
         r.iy = (fabs(dy) > 1e-15) ? 1.0 / dy : 0.0;
         r.iz = (fabs(dz) > 1e-15) ? 1.0 / dz : 0.0;
         r.s = 0;
-        r.rho0 = 0;
-        r.ci = r.cj = r.ck = r.jx = r.jy = r.jz = 0;
+        r.ci = r.cj = 0;
         const unsigned mode = rayMode(flags);
-        unsigned nseg = 0;
-        const bool entered = a.hasDust && Grid<GRID>::begin(a, sh, r, [&](int, double, double ds) {
-            if (ds > 0) { r.s += ds; nseg++; }  // outside the grid: no optical depth
-            return true;
-        });
-        if (mode == RAY_FILL) segFill += nseg;
-        else if (mode == RAY_WALK) segWalk += nseg;
-        else segPeel += nseg;
         int4* dst = reinterpret_cast<int4*>(a.rays + pos);
+        bool entered = a.hasDust;
+        if (kEnterInEvent<GRID> && entered) {
+            unsigned nseg = 0;
+            entered = Grid<GRID>::begin(a, sh, r, [&](int, double, double ds) {
+                if (ds > 0) { r.s += ds; nseg++; }  // outside the grid: no optical depth
+                return true;
+            });
+            if (mode == RAY_FILL) segFill += nseg;
+            else if (mode == RAY_WALK) segWalk += nseg;
+            else segPeel += nseg;
+        }
         if (!entered) {
             if (mode == RAY_PEEL) {
                 detectPeel(a, sh.instr[rayInstr(flags)], flags, idx, prm, 0.0, nullptr);
@@ -1541,9 +1537,8 @@ struct Events {
         d2[2] = make_double2(dy, dz);
         d2[3] = make_double2(r.ix, r.iy);
         d2[4] = make_double2(r.iz, r.s);
-        d2[5] = make_double2(r.rho0, prm);
+        d2[5] = make_double2(0.0, prm);
         dst[6] = make_int4(idx, (int)flags, r.ci, r.cj);
-        dst[7] = make_int4(r.ck, r.jx, r.jy, r.jz);
     }
 
     __device__ __forceinline__ void load(int s, Packet& p) const {
