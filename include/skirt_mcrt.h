@@ -17,9 +17,11 @@
  * Run calls are asynchronous on the engine's HIP stream; skirt_mcrt_synchronize or any download
  * waits for completion. One context per simulation per GPU; a context is not reentrant.
  * Layouts: Labs is row-major (cell, wavelength) like DustSystem::_Labs*vv (Table.hpp:104-105).
- * Instrument tallies are per instrument [nslots][nlambda][nframe] frames followed by
+ * Instrument tallies (as downloaded) are per instrument [nslots][nlambda][nframe] frames followed by
  * [nslots][nlambda] SEDs, slots as in FullInstrument (trav, strdir, strsca, dusdir, dussca,
- * scattering levels...) or a single "total" slot for Simple/SED/Frame instruments.
+ * scattering levels...) or a single "total" slot for Simple/SED/Frame instruments. These are host
+ * layouts: the device buffers (skirt_mcrt_tally_sizes, bind_tallies) are wavelength-major with padded
+ * rows and are converted by the downloads.
  */
 #ifndef SKIRT_MCRT_H
 #define SKIRT_MCRT_H

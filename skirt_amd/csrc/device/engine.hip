@@ -59,6 +59,7 @@ constexpr int kStepsPerPull = SKIRT_STEPS_PER_PULL;  // grid steps between two r
 #define SKIRT_HALVES 1
 #endif
 constexpr int kHalves = SKIRT_HALVES;
+constexpr int kDetectCopies = 8;   // LDS copies of the SED sums in the detect kernel (one per 8 lanes)
 constexpr int kPollEvery = 1;      // iterations between two counter copies of a half
 constexpr int kPollRing = 3;       // copies in flight per half (the host reads each kPollRing copies late)
 // occupancy attribute of the trace kernel (a build knob for tuning variants, tools/build_variant.sh):
@@ -75,6 +76,7 @@ constexpr int kPollRing = 3;       // copies in flight per half (the host reads 
 // ------------------------------------------------------------------ descriptors
 struct DevInstr {
     int kind, nx, ny, nslots, levels, sedOff;  // sedOff: offset of this instrument's SEDs in the LDS sums
+    int slotStride, pad;                        // frames: slots per pixel, padded (see frameAt)
     long long frameBase;                        // offset of the frames in the global instrument tally
     long long sedBase;                          // offset of the SEDs in the global instrument tally
     double kobs[3];
@@ -106,6 +108,17 @@ struct __attribute__((aligned(16))) RayRec {
 static_assert(sizeof(RayRec) == 112, "ray record layout");
 template <int GRID>
 constexpr bool kEnterInEvent = GRID == SKIRT_GRID_VORONOI;
+
+// the detection of one peel-off ray, in a compact array of its own (the detect kernel reads only these,
+// contiguously, instead of scanning every ray record): written by the event kernel, tau by the trace
+// kernel
+struct __attribute__((aligned(16))) DetRec {
+    double Lp;             // peel-off luminosity
+    double tau;            // optical depth to the grid edge
+    int l;                 // frame pixel (-1: none)
+    unsigned flags;        // as the ray's flags
+};
+static_assert(sizeof(DetRec) == 24 || sizeof(DetRec) == 32, "detection record layout");
 __device__ __forceinline__ unsigned rayMode(unsigned f) { return f & 3u; }
 __device__ __forceinline__ unsigned rayCat(unsigned f) { return (f >> 2) & 3u; }
 __device__ __forceinline__ int rayInstr(unsigned f) { return (int)((f >> 4) & 63u); }
@@ -206,9 +219,11 @@ struct Args {
     uint32_t *splo, *sphi, *sblock, *sw2, *sw3, *shave;
     double *resA, *resB;         // per slot: FILL -> tau, Lsca | WALK -> distance
     RayRec* rays;
+    DetRec* det;                 // detection records of the peel-off rays
     int* act[2];                 // active slot lists (double buffered)
     unsigned long long* claim;   // next packet index (relative to first)
-    unsigned int* ctr;           // [0,1] ray counts, [2,3] active counts, [4] trace pull counter
+    unsigned int* ctr;           // [0,1] ray counts, [2,3] active counts, [4] trace pull counter,
+                                 // [5,6] detection record counts
     int parity, init, threshold;
     int ldsMeshOff, ldsOptOff, ldsInstrOff, ldsSedOff;  // in doubles
 };
@@ -1126,7 +1141,7 @@ struct Tracer {
     // the ray ended (grid edge or WALK target reached): deliver its result
     __device__ __forceinline__ void finish(const Ray& r) {
         if (r.mode == RAY_PEEL) {
-            a.rays[r.id].s0 = r.tau;  // detectKernel turns it into a detection
+            a.det[r.idx].tau = r.tau;  // detectKernel turns it into a detection
         } else if (r.mode == RAY_FILL) {
             a.resA[r.idx] = r.tau;
             if (!ONECOMP) a.resB[r.idx] = r.f2;
@@ -1144,37 +1159,48 @@ struct Tracer {
     }
 };
 
-// Instrument::detect of one peel-off ray with optical depth tau (FullInstrument.cpp:107-174 and the
-// Simple/SED/Frame variants): SEDs into `sed` (LDS sums of the workgroup) or, when null, the global
-// tally; frames with f64 atomics
+// Instrument::detect of one peel-off ray (FullInstrument.cpp:107-174 and the Simple/SED/Frame
+// variants): what it adds to instrument slot `slot` (FullInstrument: 0 transparent, 1 direct stellar,
+// 2 scattered stellar, 3 direct dust, 4 scattered dust, 5.. per scattering level); false if nothing.
+// Lextf = L e^{-tau}.
+__device__ __forceinline__ bool detectSlot(const DevInstr& ins, unsigned flags, int slot, double Lp, double Lextf,
+                                           double& v) {
+    v = Lextf;
+    if (ins.kind != SKIRT_INSTR_FULL) return slot == 0;
+    switch (rayCat(flags)) {
+    case CAT_STAR_DIRECT:
+        if (slot == 0) v = Lp;
+        return slot <= 1;
+    case CAT_STAR_SCATTERED: {
+        const int lev = rayLevel(flags);
+        return slot == 2 || (lev >= 1 && lev <= ins.levels && slot == 5 + lev - 1);
+    }
+    case CAT_DUST_DIRECT: return slot == 3;
+    default: return slot == 4;
+    }
+}
+
+// frame tally of an instrument: [lambda][pixel][slot] with the slots padded to slotStride (8 for a
+// FullInstrument with up to 3 scattering levels), so that one detection's adds fall in one 64-byte line
+__device__ __forceinline__ double* frameAt(const Args& a, const DevInstr& ins, int ell, int l, int slot) {
+    return a.tally + ins.frameBase + ((long long)ell * ins.nx * ins.ny + l) * ins.slotStride + slot;
+}
+
+// Instrument::detect of one peel-off ray with optical depth tau by one lane: SEDs into `sed` (LDS sums
+// of the workgroup) or, when null, the global tally; frames with f64 atomics
 __device__ __forceinline__ void detectPeel(const Args& a, const DevInstr& ins, unsigned flags, int l, double Lp,
                                            double tau, double* sed) {
     const double Lextf = Lp * exp(-tau);
     const int nl = a.nlambda;
     const int ell = rayEll(flags);
-    const long long nframe = (long long)ins.nx * ins.ny;
-    auto add = [&](int slot, double v) {
+    for (int slot = 0; slot < ins.nslots; slot++) {
+        double v;
+        if (!detectSlot(ins, flags, slot, Lp, Lextf, v)) continue;
         if (ins.kind != SKIRT_INSTR_FRAME) {
             if (sed) atomicAdd(&sed[ins.sedOff + slot * nl + ell], v);
             else atomicAddF64(a.tally + ins.sedBase + slot * nl + ell, v);
         }
-        if (l >= 0 && ins.kind != SKIRT_INSTR_SED)
-            atomicAddF64(a.tally + ins.frameBase + ((long long)slot * nl + ell) * nframe + l, v);
-    };
-    if (ins.kind != SKIRT_INSTR_FULL) { add(0, Lextf); return; }
-    switch (rayCat(flags)) {
-    case CAT_STAR_DIRECT:
-        add(0, Lp);
-        add(1, Lextf);
-        break;
-    case CAT_STAR_SCATTERED: {
-        add(2, Lextf);
-        const int lev = rayLevel(flags);
-        if (lev >= 1 && lev <= ins.levels) add(5 + lev - 1, Lextf);
-        break;
-    }
-    case CAT_DUST_DIRECT: add(3, Lextf); break;
-    default: add(4, Lextf); break;
+        if (l >= 0 && ins.kind != SKIRT_INSTR_SED) atomicAddF64(frameAt(a, ins, ell, l, slot), v);
     }
 }
 
@@ -1376,6 +1402,7 @@ __global__ void __launch_bounds__(kBlock) SKIRT_TRACE_ATTR traceKernel(const Arg
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         // reset the counters the next event iteration appends to (nobody else uses them now)
         a.ctr[1 - a.parity] = 0;  // ray count of the next iteration
+        a.ctr[5 + (1 - a.parity)] = 0;  // and its detection records (the last ones were detected already)
         a.ctr[2 + a.parity] = 0;  // active list just consumed by the event kernel
     }
     if (a.ctr[a.parity] == 0) return;  // an iteration after the end of the phase
@@ -1450,25 +1477,41 @@ __global__ void __launch_bounds__(kBlock) SKIRT_TRACE_ATTR traceKernel(const Arg
 // the detections of this iteration's peel-off rays (their optical depths are in the queue now)
 __global__ void __launch_bounds__(kBlock) detectKernel(const Args a) {
     extern __shared__ __attribute__((aligned(16))) double lds[];
-    if (a.ctr[a.parity] == 0) return;
+    const unsigned int nrays = a.ctr[5 + a.parity];  // this iteration's detection records
+    if (nrays == 0) return;
     Shared sh = stageTables(a, lds, STAGE_INSTR);
-    for (int q = threadIdx.x; q < a.nsed; q += blockDim.x) sh.sed[q] = 0.0;
+    for (int q = threadIdx.x; q < kDetectCopies * a.nsed; q += blockDim.x) sh.sed[q] = 0.0;
     __syncthreads();
-    const unsigned int nrays = a.ctr[a.parity];
     unsigned int detects = 0;
-    for (unsigned int id = blockIdx.x * blockDim.x + threadIdx.x; id < nrays; id += gridDim.x * blockDim.x) {
-        const int4 c6 = reinterpret_cast<const int4*>(a.rays + id)[6];
-        const unsigned flags = (unsigned)c6.y;
-        if (rayMode(flags) != RAY_PEEL) continue;
-        const double2 c4 = reinterpret_cast<const double2*>(a.rays + id)[4];
-        const double2 c5 = reinterpret_cast<const double2*>(a.rays + id)[5];
-        detectPeel(a, sh.instr[rayInstr(flags)], flags, c6.x, c5.y, c4.y, sh.sed);
-        detects++;
+    // eight lanes per ray, one per instrument slot (mod 8): the frame adds of one detection fall in one
+    // 64-byte line (frameAt) and leave in one wave instruction, so they share one atomic request. Each
+    // group of 8 lanes sums SEDs into its own LDS copy: the 8 rays of an instruction mostly hit the same
+    // few (slot, wavelength) sums, which one copy would serialize.
+    const int lane = threadIdx.x & 63, sub = lane & 7;
+    double* sed = sh.sed + (lane >> 3) * a.nsed;
+    const unsigned int waves = gridDim.x * (blockDim.x / 64);
+    const unsigned int wave = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
+    for (unsigned int base = wave * 8; base < nrays; base += waves * 8) {
+        const unsigned int id = base + (lane >> 3);
+        if (id >= nrays) continue;
+        const DetRec d = a.det[id];
+        const unsigned flags = d.flags;
+        const DevInstr& ins = sh.instr[rayInstr(flags)];
+        const int l = d.l, ell = rayEll(flags);
+        const double Lp = d.Lp, Lextf = Lp * exp(-d.tau);
+        for (int slot = sub; slot < ins.nslots; slot += 8) {
+            double v;
+            if (!detectSlot(ins, flags, slot, Lp, Lextf, v)) continue;
+            if (ins.kind != SKIRT_INSTR_FRAME) atomicAdd(&sed[ins.sedOff + slot * a.nlambda + ell], v);
+            if (l >= 0 && ins.kind != SKIRT_INSTR_SED) atomicAddF64(frameAt(a, ins, ell, l, slot), v);
+        }
+        if (sub == 0) detects++;
     }
     // flush the per-workgroup SED sums
     __syncthreads();
     for (int q = threadIdx.x; q < a.nsed; q += blockDim.x) {
-        const double v = sh.sed[q];
+        double v = 0.0;
+        for (int g = 0; g < kDetectCopies; g++) v += sh.sed[g * a.nsed + q];
         if (v != 0.0) {
             int ii = 0;
             while (ii + 1 < a.ninstr && sh.instr[ii + 1].sedOff <= q) ii++;
@@ -1521,10 +1564,7 @@ struct Events {
             else segPeel += nseg;
         }
         if (!entered) {
-            if (mode == RAY_PEEL) {
-                detectPeel(a, sh.instr[rayInstr(flags)], flags, idx, prm, 0.0, nullptr);
-                detects++;
-            } else {
+            if (mode != RAY_PEEL) {  // a peel-off's detection record already holds tau = 0
                 a.resA[idx] = 0.0;  // FILL: tau = 0 (and no scattered luminosity); WALK: s = 0
                 if (!ONECOMP) a.resB[idx] = 0.0;
             }
@@ -1599,12 +1639,9 @@ struct Events {
     // Instrument::detect without a dust system (tau = 0): FullInstrument then holds only the
     // transparent arrays (FullInstrument.cpp:58-60, 115-120)
     __device__ __forceinline__ void detectNow(const DevInstr& ins, const Packet& p, double Lp, int l) {
-        const int nl = a.nlambda;
-        const long long nframe = (long long)ins.nx * ins.ny;
         detects++;
         if (ins.kind != SKIRT_INSTR_FRAME) atomicAddF64(a.tally + ins.sedBase + p.ell, Lp);
-        if (l >= 0 && ins.kind != SKIRT_INSTR_SED) atomicAddF64(a.tally + ins.frameBase + (long long)p.ell * nframe + l, Lp);
-        (void)nl;
+        if (l >= 0 && ins.kind != SKIRT_INSTR_SED) atomicAddF64(frameAt(a, ins, p.ell, l, 0), Lp);
     }
 
     // Random::direction() (Random.cpp:179-184): theta = acos(2u-1), phi = 2 pi u', evaluated as
@@ -1851,9 +1888,40 @@ __device__ __forceinline__ void blockReserve(T0* ctr0, T0 c0, T0& r0, T1* ctr1, 
     __syncthreads();  // the scratch words are reused by the next call
 }
 
+// three counters at once (scratch: 3 * (kBlock / 64) + 3 words)
+__device__ __forceinline__ void blockReserve3(unsigned* ctr0, unsigned c0, unsigned& r0, unsigned* ctr1, unsigned c1,
+                                              unsigned& r1, unsigned* ctr2, unsigned c2, unsigned& r2,
+                                              unsigned long long* scratch) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    constexpr int W = kBlock / 64;
+    unsigned i0 = c0, i1 = c1, i2 = c2;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const unsigned v0 = __shfl_up(i0, off), v1 = __shfl_up(i1, off), v2 = __shfl_up(i2, off);
+        if (lane >= off) { i0 += v0; i1 += v1; i2 += v2; }
+    }
+    if (lane == 63) { scratch[wave] = i0; scratch[W + wave] = i1; scratch[2 * W + wave] = i2; }
+    __syncthreads();
+    unsigned w0 = 0, w1 = 0, w2 = 0, t0 = 0, t1 = 0, t2 = 0;
+#pragma unroll
+    for (int w = 0; w < W; w++) {
+        const unsigned s0 = (unsigned)scratch[w], s1 = (unsigned)scratch[W + w], s2 = (unsigned)scratch[2 * W + w];
+        if (w < wave) { w0 += s0; w1 += s1; w2 += s2; }
+        t0 += s0; t1 += s1; t2 += s2;
+    }
+    if (threadIdx.x == 0) scratch[3 * W] = t0 ? atomicAdd(ctr0, t0) : 0u;
+    if (threadIdx.x == 64) scratch[3 * W + 1] = t1 ? atomicAdd(ctr1, t1) : 0u;
+    if (threadIdx.x == 128) scratch[3 * W + 2] = t2 ? atomicAdd(ctr2, t2) : 0u;
+    __syncthreads();
+    r0 = (unsigned)scratch[3 * W] + w0 + i0 - c0;
+    r1 = (unsigned)scratch[3 * W + 1] + w1 + i1 - c1;
+    r2 = (unsigned)scratch[3 * W + 2] + w2 + i2 - c2;
+    __syncthreads();  // the scratch words are reused by the next call
+}
+
 template <int GRID, bool ONECOMP>
 __global__ void __launch_bounds__(kBlock) SKIRT_EVENT_ATTR eventKernel(const Args a) {
-    __shared__ unsigned long long resv[2 * (kBlock / 64) + 2];
+    __shared__ unsigned long long resv[3 * (kBlock / 64) + 3];
     extern __shared__ __attribute__((aligned(16))) double lds[];
     if (blockIdx.x == 0 && threadIdx.x == 0) a.ctr[4] = 0;  // the trace kernel's pull counter
     if (!a.init && a.ctr[2 + a.parity] == 0) return;  // an iteration after the end of the phase
@@ -1954,12 +2022,13 @@ __global__ void __launch_bounds__(kBlock) SKIRT_EVENT_ATTR eventKernel(const Arg
             }
         }
         if (mainMode != RAY_NONE) nray++;
-        // the queue space of the block's rays and the slots staying active: one atomic each per block
+        // the queue space of the block's rays, the slots staying active and the detection records of
+        // the peel-offs: one atomic each per block
         const bool active = mainMode != RAY_NONE;
-        unsigned int pos = 0, apos = 0;
-        blockReserve<unsigned int, unsigned int>(a.ctr + a.parity, (unsigned)nray, pos, a.ctr + 2 + (1 - a.parity),
-                                                 active ? 1u : 0u, apos, resv);
         const int npeel = nray - (mainMode != RAY_NONE ? 1 : 0);
+        unsigned int pos = 0, apos = 0, dpos = 0;
+        blockReserve3(a.ctr + a.parity, (unsigned)nray, pos, a.ctr + 2 + (1 - a.parity), active ? 1u : 0u, apos,
+                      a.ctr + 5 + a.parity, (unsigned)npeel, dpos, resv);
         int inext = 0;  // next instrument to consider for a peel-off
         for (int k = 0; k < nray; k++) {
             double dx, dy, dz, prm;
@@ -1988,8 +2057,11 @@ __global__ void __launch_bounds__(kBlock) SKIRT_EVENT_ATTR eventKernel(const Arg
                 }
                 dx = ins.kobs[0]; dy = ins.kobs[1]; dz = ins.kobs[2];
                 prm = Lp;
-                idx = l;
                 flags = RAY_PEEL | (cat << 2) | ((unsigned)i << 4) | (level << 10) | ((unsigned)p.ell << 18);
+                // its detection record (the trace kernel adds the optical depth; a path that misses the
+                // grid leaves tau = 0)
+                idx = (int)(dpos + k);
+                a.det[idx] = DetRec{Lp, 0.0, l, flags};
             } else {
                 dx = p.kx; dy = p.ky; dz = p.kz;
                 prm = mainParam;
@@ -2119,7 +2191,8 @@ int upload(SkirtMcrt* c, T*& dst, const T* src, size_t n) {
 // results and two active lists; nslots counts the slots of one half
 int ensurePool(SkirtMcrt* c, int nslots) {
     const int rayCap = nslots * (1 + (int)c->instr.size());
-    const size_t half = (size_t)rayCap * sizeof(RayRec) + (size_t)nslots * (10 * 8 + 4 * 4 + 6 * 4 + 2 * 4) + 4096;
+    const size_t half = (size_t)rayCap * sizeof(RayRec) + (size_t)(rayCap - nslots) * sizeof(DetRec) +
+                        (size_t)nslots * (10 * 8 + 4 * 4 + 6 * 4 + 2 * 4) + 4096;
     if (c->dPool && c->nslots == nslots && c->rayCap == rayCap) return SKIRT_OK;
     if (c->dPool) { (void)hipFree(c->dPool); c->dPool = nullptr; }
     HIPCHECK(c, hipMalloc(&c->dPool, kHalves * half));
@@ -2137,6 +2210,8 @@ void carvePool(SkirtMcrt* c, Args& a, int h) {
     auto takeU = [&](uint32_t*& d) { d = reinterpret_cast<uint32_t*>(p); p += n * 4; };
     a.rays = reinterpret_cast<RayRec*>(p);
     p += (size_t)c->rayCap * sizeof(RayRec);
+    a.det = reinterpret_cast<DetRec*>(p);  // at most one peel-off per instrument and slot per iteration
+    p += (size_t)(c->rayCap - c->nslots) * sizeof(DetRec);
     takeD(a.srx); takeD(a.sry); takeD(a.srz); takeD(a.skx); takeD(a.sky); takeD(a.skz); takeD(a.sL); takeD(a.sLth);
     takeD(a.resA); takeD(a.resB);
     takeI(a.sell); takeI(a.snscatt); takeI(a.sstellar); takeI(a.sstate);
@@ -2579,8 +2654,9 @@ int skirt_mcrt_set_instruments(SkirtMcrt* c, const SkirtInstrDesc* in, int n) {
         d.sinphi = in[i].sinphi; d.cosphi = in[i].cosphi; d.sintheta = in[i].sintheta; d.costheta = in[i].costheta;
         d.sinpa = in[i].sinpa; d.cospa = in[i].cospa;
         d.xpmin = in[i].xpmin; d.xpsiz = in[i].xpsiz; d.ypmin = in[i].ypmin; d.ypsiz = in[i].ypsiz;
+        d.slotStride = d.nslots == 1 ? 1 : (d.nslots + 7) / 8 * 8;
         d.frameBase = off;
-        const long long nframes = (d.kind == SKIRT_INSTR_SED) ? 0 : (long long)d.nslots * c->nlambda * d.nx * d.ny;
+        const long long nframes = (d.kind == SKIRT_INSTR_SED) ? 0 : (long long)d.slotStride * c->nlambda * d.nx * d.ny;
         off += nframes;
         d.sedBase = off;
         const long long nseds = (d.kind == SKIRT_INSTR_FRAME) ? 0 : (long long)d.nslots * c->nlambda;
@@ -2906,6 +2982,9 @@ int skirt_mcrt_run_phase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, 
                             + (size_t)kLabsBuf * kBlock * (sizeof(double) + sizeof(unsigned));  // + Labs buffers
     const size_t ldsEvent = (size_t)a.ldsSedOff * sizeof(double);           // + instruments
     if (lds > 64 * 1024) return fail(c, SKIRT_ERR_UNSUPPORTED, "tables do not fit in LDS (" + std::to_string(lds) + " bytes)");
+    // detect kernel: kDetectCopies copies of the SED sums (one per group of 8 lanes, see detectKernel)
+    const size_t ldsDetect = lds + (size_t)(kDetectCopies - 1) * c->nsed * sizeof(double);
+    if (ldsDetect > 64 * 1024) return fail(c, SKIRT_ERR_UNSUPPORTED, "instrument SEDs do not fit in LDS");
     const int kind = c->gridKind == SKIRT_GRID_CARTESIAN ? SKIRT_GRID_CARTESIAN
                      : c->gridKind == SKIRT_GRID_VORONOI ? SKIRT_GRID_VORONOI
                      : bookkeeping ? kOctreeBookkeeping
@@ -3010,7 +3089,7 @@ int skirt_mcrt_run_phase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, 
             HIPCHECK(c, hipEventRecord(c->traceEv[2 * c->traceLaunches + 1], st));
             c->traceLaunches++;
             if (a.ninstr > 0) {
-                hipLaunchKernelGGL(detectKernel, dim3(dgrid), dim3(kBlock), lds, st, aa);
+                hipLaunchKernelGGL(detectKernel, dim3(dgrid), dim3(kBlock), ldsDetect, st, aa);
                 HIPCHECK(c, hipGetLastError());
             }
             its[h]++;
@@ -3073,7 +3152,21 @@ int skirt_mcrt_download(SkirtMcrt* c, double* labs, double* instr) {
     }
     if (instr && c->nInstrTally) {
         if (!c->dTally) return fail(c, SKIRT_ERR_STATE, "no instrument buffer");
-        HIPCHECK(c, hipMemcpy(instr, c->dTally, c->nInstrTally * sizeof(double), hipMemcpyDeviceToHost));
+        std::vector<double> t(c->nInstrTally);
+        HIPCHECK(c, hipMemcpy(t.data(), c->dTally, c->nInstrTally * sizeof(double), hipMemcpyDeviceToHost));
+        // per instrument, the reference's order: frames [slot][lambda][pixel], then SEDs [slot][lambda]
+        size_t o = 0;
+        const size_t nl = (size_t)c->nlambda;
+        for (const DevInstr& d : c->instr) {
+            const size_t npix = (size_t)d.nx * d.ny;
+            if (d.kind != SKIRT_INSTR_SED)
+                for (int slot = 0; slot < d.nslots; slot++)
+                    for (size_t ell = 0; ell < nl; ell++)
+                        for (size_t l = 0; l < npix; l++)
+                            instr[o++] = t[d.frameBase + (ell * npix + l) * d.slotStride + slot];
+            if (d.kind != SKIRT_INSTR_FRAME)
+                for (size_t q = 0; q < (size_t)d.nslots * nl; q++) instr[o++] = t[d.sedBase + q];
+        }
     }
     return SKIRT_OK;
 }

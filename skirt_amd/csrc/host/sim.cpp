@@ -26,7 +26,7 @@ struct SkirtSim {
     std::vector<double> labs;                 // Ncells x Nlambda (stellar)
     std::vector<double> labsDust;             // Ncells x Nlambda (last self-absorption cycle)
     std::vector<double> dustTotals;           // Labsdusttot after every self-absorption cycle
-    std::vector<double> instrAll;             // concatenated device layout
+    std::vector<double> instrAll;             // concatenated, per instrument frames [slot][lambda][pixel] + SEDs
     std::vector<size_t> instrOff;             // per instrument offset into instrAll
     std::vector<std::vector<double>> frames, seds;
     ~SkirtSim() {
@@ -187,7 +187,8 @@ int skirt_sim_attach(SkirtSim* s, int device) {
     if ((rc = check(s, skirt_mcrt_set_instruments(s->eng, ids.data(), (int)ids.size())))) return rc;
     size_t nl = 0, ni = 0;
     skirt_mcrt_tally_sizes(s->eng, &nl, &ni);
-    if (ni != s->instrAll.size()) { g_err = "instrument tally size mismatch"; return SKIRT_ERR_STATE; }
+    // the device tally pads each frame pixel's slots to a 64-byte line; downloads restore this layout
+    if (ni < s->instrAll.size()) { g_err = "instrument tally size mismatch"; return SKIRT_ERR_STATE; }
     return check(s, skirt_mcrt_zero_tallies(s->eng));
 }
 
