@@ -745,11 +745,17 @@ public:
             }
         }
         const Geometry& geo = M.starGeom[h];
-        // PlummerGeometry::randomradius then SpheGeometry::generatePosition
-        double t = pow(rng.uniform(), 1.0 / 3.0);
-        double r = geo.c * t / sqrt((1.0 - t) * (1.0 + t));
-        Vec3 d = isotropic(rng);
-        Vec3 pos{r * d.x, r * d.y, r * d.z};
+        Vec3 pos;
+        if (geo.kind == GeometryKind::ExpDisk) {
+            // ExpDiskGeometry::randomR / randomz, SepAxGeometry::generatePosition
+            expDiskPosition(geo, rng, pos.x, pos.y, pos.z);
+        } else {
+            // PlummerGeometry::randomradius then SpheGeometry::generatePosition
+            double t = pow(rng.uniform(), 1.0 / 3.0);
+            double r = geo.c * t / sqrt((1.0 - t) * (1.0 + t));
+            Vec3 d = isotropic(rng);
+            pos = Vec3{r * d.x, r * d.y, r * d.z};
+        }
         Vec3 k = isotropic(rng);
         pp = Packet{Lw, ell, pos, k, 0, h};
     }
@@ -1027,6 +1033,35 @@ int oracle_grid_paths(const char* ski, const char* datadir, int n, const double*
                 else for (int k = 0; k < 6; k++) o[k] = NAN;
                 o[6] = p.v[j].ds;
             }
+        }
+        return 0;
+    } catch (const std::exception& e) {
+        g_error = e.what();
+        return -1;
+    }
+}
+
+int oracle_star_positions(const char* ski, const char* datadir, int comp, int n, uint64_t seed, double* out,
+                          double* density) {
+    try {
+        std::string dd = datadir && *datadir ? datadir : defaultDataDir();
+        MTRandom mt(readSkiSeed(ski));
+        Model M = loadSki(ski, mt, dd);
+        if (comp < 0 || comp >= (int)M.starGeom.size()) throw std::runtime_error("no such stellar component");
+        const Geometry& geo = M.starGeom[comp];
+        MTRandom mtr((unsigned long)seed);
+        MTRng rng(&mtr);
+        for (int i = 0; i < n; i++) {
+            double* o = out + 3 * (size_t)i;
+            if (geo.kind == GeometryKind::ExpDisk) {
+                expDiskPosition(geo, rng, o[0], o[1], o[2]);
+            } else {
+                const double t = pow(rng.uniform(), 1.0 / 3.0);
+                const double r = geo.c * t / sqrt((1.0 - t) * (1.0 + t));
+                const Vec3 d = isotropic(rng);
+                o[0] = r * d.x; o[1] = r * d.y; o[2] = r * d.z;
+            }
+            if (density) density[i] = geo.density(o[0], o[1], o[2]);
         }
         return 0;
     } catch (const std::exception& e) {

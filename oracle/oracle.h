@@ -69,6 +69,10 @@ int oracle_num_instruments(OracleRun* r);
  * the ray's segment count (capped at maxseg), *ncells the grid's cell count. Returns 0, -1 on failure. */
 int oracle_grid_paths(const char* ski, const char* datadir, int n, const double* rays, int maxseg, double* out,
                       int* nseg, int* ncells);
+/* n random positions of stellar component `comp` (its geometry's generatePosition on an MT19937 stream
+ * seeded with `seed`), 3 doubles each, and the geometry's density there (density may be NULL) */
+int oracle_star_positions(const char* ski, const char* datadir, int comp, int n, uint64_t seed, double* out,
+                          double* density);
 /* statistics: number of packets launched, path segments traversed, wall seconds of the photon phases */
 double oracle_seconds(OracleRun* r);
 uint64_t oracle_packets(OracleRun* r);

@@ -1644,6 +1644,63 @@ struct Events {
         if (l >= 0 && ins.kind != SKIRT_INSTR_SED) atomicAddF64(frameAt(a, ins, p.ell, l, 0), Lp);
     }
 
+    // SpecialFunctions::LambertW1 (SpecialFunctions.cpp:579-626), the W_{-1} branch; as the host's
+    // lambertW1 (host/build.cpp), whose argument checks the callers here never fail
+    __device__ static double lambertW1(double z) {
+        const double eps = 1.0e-12;
+        const double em1 = 0.3678794411714423215955237701614608;
+        if (z == 0.0) return -kDblMax;
+        const double q = z + em1;
+        const double r = -sqrt(q);
+        const double t8 = -8.401032217523977370984161688514 +
+                          r * (12.250753501314460424 + r * (-18.100697012472442755 + r * 27.029044799010561650));
+        const double t5 = 3.066858901050631912893148922704 +
+                          r * (-4.175335600258177138854984177460 + r * (5.858023729874774148815053846119 + r * t8));
+        const double t1 = 2.331643981597124203363536062168 +
+                          r * (-1.812187885639363490240191647568 +
+                               r * (1.936631114492359755363277457668 + r * (-2.353551201881614516821543561516 + r * t5)));
+        const double w0 = -1.0 + r * t1;
+        if (q < 3.0e-3) return w0;
+        double w;
+        if (z < -1e-6) {
+            w = w0;
+        } else {
+            const double l1 = log(-z);
+            const double l2 = log(-l1);
+            w = l1 - l2 + l2 / l1;
+        }
+        for (int i = 0; i < 10; i++) {  // Halley iteration
+            const double e = exp(w);
+            double t = w * e - z;
+            const double p = w + 1.0;
+            t /= e * p - 0.5 * (p + 1.0) * t / p;
+            w -= t;
+            if (fabs(t) < eps * (1.0 + fabs(w))) break;
+        }
+        return w;
+    }
+
+    // ExpDiskGeometry::randomR / randomz and SepAxGeometry::generatePosition (R, phi = 2 pi u, z;
+    // Position(R, phi, z, CYLINDRICAL)); gp = {hR, hz, Rmax, zmax, Rmin, rho0, 0, kind}
+    __device__ __forceinline__ void expDiskPosition(PacketRng& rng, const double* gp, double& x, double& y,
+                                                    double& z) const {
+        const double hR = gp[0], hz = gp[1], Rmax = gp[2], zmax = gp[3], Rmin = gp[4];
+        double R, X;
+        do {
+            X = rng.uniform();
+            R = hR * (-1.0 - lambertW1((X - 1.0) / M_E));
+        } while ((Rmax > 0.0 && R >= Rmax) || R <= Rmin);
+        const double phi = 2.0 * M_PI * rng.uniform();
+        double zz;
+        do {
+            X = rng.uniform();
+            zz = (X <= 0.5) ? hz * log(2.0 * X) : -hz * log(2.0 * (1.0 - X));
+        } while (zmax > 0.0 && fabs(zz) >= zmax);
+        x = R * cos(phi);
+        y = R * sin(phi);
+        z = zz;
+    }
+
     // Random::direction() (Random.cpp:179-184): theta = acos(2u-1), phi = 2 pi u', evaluated as
     // cos(theta) = 2u-1, sin(theta) = sqrt(1-cos^2) and sin/cos(2 pi u') = sinpi/cospi(2u') -- the
     // same values to rounding, without acos or a large-argument reduction. The reference's 1e-8
@@ -1809,14 +1866,19 @@ struct Events {
             const double Lmean = a.lumtot[ell] / N;
             L = L0 * (1.0 / (1.0 - xi + xi * Lmean / Lh));
         }
-        // PlummerGeometry::randomradius (t = u^(1/3)) and SpheGeometry::generatePosition, then the
-        // emission direction Random::direction()
-        const double c = a.geomParam[4 * h];
-        const double t = cbrt(p.rng.uniform());
-        const double rr = c * t / sqrt((1.0 - t) * (1.0 + t));
-        double ux, uy, uz;
-        isotropic(p.rng, ux, uy, uz);
-        p.rx = rr * ux; p.ry = rr * uy; p.rz = rr * uz;
+        const double* gp = a.geomParam + 8 * h;
+        if ((int)gp[7] == SKIRT_GEOM_EXPDISK) {
+            expDiskPosition(p.rng, gp, p.rx, p.ry, p.rz);
+        } else {
+            // PlummerGeometry::randomradius (t = u^(1/3)) and SpheGeometry::generatePosition
+            const double c = gp[0];
+            const double t = cbrt(p.rng.uniform());
+            const double rr = c * t / sqrt((1.0 - t) * (1.0 + t));
+            double ux, uy, uz;
+            isotropic(p.rng, ux, uy, uz);
+            p.rx = rr * ux; p.ry = rr * uy; p.rz = rr * uz;
+        }
+        // the emission direction Random::direction()
         isotropic(p.rng, p.kx, p.ky, p.kz);
         p.L = L;
         p.nscatt = 0;
@@ -2615,8 +2677,14 @@ int skirt_mcrt_upload_media(SkirtMcrt* c, const SkirtMediaDesc* m) {
 int skirt_mcrt_upload_sources(SkirtMcrt* c, const SkirtSourceDesc* s) {
     if (!c || !s) return SKIRT_ERR_ARG;
     if (s->ncomp < 1 || s->nlambda < 1) return fail(c, SKIRT_ERR_ARG, "bad source sizes");
-    for (int h = 0; h < s->ncomp; h++)
-        if (s->geom_kind[h] != SKIRT_GEOM_PLUMMER) return fail(c, SKIRT_ERR_UNSUPPORTED, "unsupported source geometry");
+    // device geometry table: the 8 parameters of each component with its kind in the last word
+    std::vector<double> gp(8 * (size_t)s->ncomp);
+    for (int h = 0; h < s->ncomp; h++) {
+        if (s->geom_kind[h] != SKIRT_GEOM_PLUMMER && s->geom_kind[h] != SKIRT_GEOM_EXPDISK)
+            return fail(c, SKIRT_ERR_UNSUPPORTED, "unsupported source geometry");
+        for (int q = 0; q < 7; q++) gp[8 * h + q] = s->geom_param[8 * h + q];
+        gp[8 * h + 7] = (double)s->geom_kind[h];
+    }
     HIPCHECK(c, hipSetDevice(c->device));
     if (c->nlambda && c->nlambda != s->nlambda) return fail(c, SKIRT_ERR_ARG, "sources and media disagree on nlambda");
     if (s->nlambda >= (1 << 14)) return fail(c, SKIRT_ERR_ARG, "at most 16383 wavelengths");
@@ -2624,7 +2692,7 @@ int skirt_mcrt_upload_sources(SkirtMcrt* c, const SkirtSourceDesc* s) {
     c->emissionBias = s->emission_bias;
     c->nlambda = s->nlambda;
     int rc;
-    if ((rc = upload(c, c->dGeomParam, s->geom_param, 4 * (size_t)s->ncomp))) return rc;
+    if ((rc = upload(c, c->dGeomParam, gp.data(), gp.size()))) return rc;
     if ((rc = upload(c, c->dLum, s->lum, (size_t)s->ncomp * s->nlambda))) return rc;
     if ((rc = upload(c, c->dLumtot, s->lumtot, (size_t)s->nlambda))) return rc;
     if ((rc = upload(c, c->dCdf, s->cdf, (size_t)s->nlambda * (s->ncomp + 1)))) return rc;

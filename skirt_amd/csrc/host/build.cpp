@@ -14,6 +14,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <cfloat>
 #include <cstring>
 #include <dlfcn.h>
 #include <fstream>
@@ -182,8 +183,53 @@ double Geometry::density(double x, double y, double z) const {
         double s = r / c;
         return rho0 * std::pow(1.0 + s * s, -2.5);
     }
+    case GeometryKind::ExpDisk: {
+        // AxGeometry::density(Position) -> ExpDiskGeometry::density(R, z) (Position::cylradius)
+        const double R = std::sqrt(x * x + y * y);
+        const double absz = std::fabs(z);
+        if (Rmax > 0.0 && R > Rmax) return 0.0;
+        else if (zmax > 0.0 && absz > zmax) return 0.0;
+        else if (R < Rmin) return 0.0;
+        return rho0 * std::exp(-R / hR) * std::exp(-absz / hz);
+    }
     }
     return 0;
+}
+
+double lambertW1(double z) {
+    const double eps = 1.0e-12;
+    const double em1 = 0.3678794411714423215955237701614608;
+    static const double c[12] = {-1.0, 2.331643981597124203363536062168, -1.812187885639363490240191647568,
+                                 1.936631114492359755363277457668, -2.353551201881614516821543561516,
+                                 3.066858901050631912893148922704, -4.175335600258177138854984177460,
+                                 5.858023729874774148815053846119, -8.401032217523977370984161688514,
+                                 12.250753501314460424, -18.100697012472442755, 27.029044799010561650};
+    if (z < -em1 || z > 0.0 || std::isinf(z) || std::isnan(z)) throw std::runtime_error("LambertW1: bad argument");
+    if (z == 0.0) return -DBL_MAX;
+    const double q = z + em1;
+    const double r = -std::sqrt(q);
+    const double t8 = c[8] + r * (c[9] + r * (c[10] + r * c[11]));
+    const double t5 = c[5] + r * (c[6] + r * (c[7] + r * t8));
+    const double t1 = c[1] + r * (c[2] + r * (c[3] + r * (c[4] + r * t5)));
+    const double w0 = c[0] + r * t1;
+    if (q < 3.0e-3) return w0;
+    double w;
+    if (z < -1e-6) {
+        w = w0;
+    } else {
+        const double l1 = std::log(-z);
+        const double l2 = std::log(-l1);
+        w = l1 - l2 + l2 / l1;
+    }
+    for (int i = 0; i < 10; i++) {  // Halley iteration
+        const double e = std::exp(w);
+        double t = w * e - z;
+        const double p = w + 1.0;
+        t /= e * p - 0.5 * (p + 1.0) * t / p;
+        w -= t;
+        if (std::fabs(t) < eps * (1.0 + std::fabs(w))) return w;
+    }
+    throw std::runtime_error("LambertW1: no convergence");
 }
 
 double WavelengthGrid::lambdamin(int ell) const {
@@ -329,6 +375,27 @@ Geometry parseGeometry(const Ctx& c, const XmlElement* g) {
         geo.c = attr(c, g, "scale", "length", 0);
         if (geo.c <= 0) throw std::runtime_error("the scale length c should be positive");
         geo.rho0 = 0.75 / std::pow(geo.c, 3) / M_PI;
+    } else if (g->name == "ExpDiskGeometry") {
+        // ExpDiskGeometry::setupSelfBefore (ExpDiskGeometry.cpp): checks and the normalization rho0
+        geo.kind = GeometryKind::ExpDisk;
+        geo.hR = attr(c, g, "radialScale", "length", 0);
+        geo.hz = attr(c, g, "axialScale", "length", 0);
+        geo.Rmax = attr(c, g, "radialTrunc", "length", 0);
+        geo.zmax = attr(c, g, "axialTrunc", "length", 0);
+        geo.Rmin = attr(c, g, "innerRadius", "length", 0);
+        if (geo.hR <= 0) throw std::runtime_error("The radial scale length hR should be positive");
+        if (geo.hz <= 0) throw std::runtime_error("The axial scale height hz should be positive");
+        if (geo.Rmax < 0) throw std::runtime_error("The radial truncation length Rmax should be zero or positive");
+        if (geo.zmax < 0) throw std::runtime_error("The axial truncation length zmax should be zero or positive");
+        if (geo.Rmin < 0) throw std::runtime_error("The minimum radius Rmax should be zero or positive");
+        else if (geo.Rmin > geo.Rmax && geo.Rmax > 0)
+            throw std::runtime_error("The minimum radius Rmin should be larger than the truncation radius Rmax");
+        const double intphi = 2.0 * M_PI;
+        const double intz = (geo.zmax > 0) ? -2.0 * geo.hz * std::expm1(-geo.zmax / geo.hz) : 2.0 * geo.hz;
+        const double tmin = (geo.Rmin > 0) ? std::exp(-geo.Rmin / geo.hR) * (1.0 + geo.Rmin / geo.hR) : 1.0;
+        const double tmax = (geo.Rmax > 0) ? std::exp(-geo.Rmax / geo.hR) * (1.0 + geo.Rmax / geo.hR) : 0.0;
+        const double intR = geo.hR * geo.hR * (tmin - tmax);
+        geo.rho0 = 1.0 / (intR * intphi * intz);
     } else {
         throw std::runtime_error("unsupported geometry " + g->name);
     }
@@ -952,6 +1019,15 @@ static void buildVoronoiGrid(const Ctx& c, const XmlElement* ge, Model& m, Unifo
                 if (X < cum[0]) h = 0;
                 else h = nr::locateBasic(cum, X, (int)cum.size() - 1);
                 const Geometry& geo = m.dust[h].geom;
+                if (geo.kind == GeometryKind::ExpDisk) {
+                    double x, y, z;
+                    expDiskPosition(geo, rng, x, y, z);
+                    if (contains(x, y, z)) {
+                        sites[3 * q] = x; sites[3 * q + 1] = y; sites[3 * q + 2] = z;
+                        break;
+                    }
+                    continue;
+                }
                 // PlummerGeometry::randomradius, then SpheGeometry::generatePosition (Random::direction)
                 double t = std::pow(rng.uniform(), 1.0 / 3.0);
                 double r = geo.c * t / std::sqrt((1.0 - t) * (1.0 + t));

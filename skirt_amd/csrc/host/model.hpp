@@ -6,6 +6,7 @@
 // (include/skirt_mcrt.h) or to the CPU checker in oracle/.
 #pragma once
 
+#include <cmath>
 #include <cstdint>
 #include <string>
 #include <vector>
@@ -18,16 +19,42 @@ namespace skirt {
 
 // ---------------------------------------------------------------- geometries
 // Reference: SKIRTcore/PlummerGeometry.cpp (density 49-54, randomradius 57-63), SpheGeometry.cpp
-// (generatePosition = randomradius then isotropic direction).
-enum class GeometryKind : int { Plummer = 0 };
+// (generatePosition = randomradius then isotropic direction); ExpDiskGeometry.cpp (setupSelfBefore:
+// rho0; density; randomR with SpecialFunctions::LambertW1; randomz) and SepAxGeometry::generatePosition
+// (R, then phi = 2 pi u, then z; Position(R, phi, z, CYLINDRICAL), Position.cpp:23-31).
+// The kind values are the engine's (skirt_mcrt.h SKIRT_GEOM_*).
+enum class GeometryKind : int { Plummer = 0, ExpDisk = 1 };
 
 struct Geometry {
     GeometryKind kind = GeometryKind::Plummer;
     double c = 0;     // Plummer scale length
-    double rho0 = 0;  // 0.75/c^3/pi (PlummerGeometry.cpp setupSelfBefore)
+    double rho0 = 0;  // Plummer: 0.75/c^3/pi (PlummerGeometry.cpp setupSelfBefore); ExpDisk: its rho0
+    double hR = 0, hz = 0, Rmax = 0, zmax = 0, Rmin = 0;  // ExpDisk scales and truncations (0: none)
 
     double density(double x, double y, double z) const;
 };
+
+// SpecialFunctions::LambertW1 (SKIRTcore/SpecialFunctions.cpp:579-626): the W_{-1} branch
+double lambertW1(double z);
+
+// ExpDiskGeometry::randomR / randomz and SepAxGeometry::generatePosition, in the reference's draw order
+template <class R>
+void expDiskPosition(const Geometry& g, R& rng, double& x, double& y, double& z) {
+    double Rc, X;
+    do {
+        X = rng.uniform();
+        Rc = g.hR * (-1.0 - lambertW1((X - 1.0) / M_E));
+    } while ((g.Rmax > 0.0 && Rc >= g.Rmax) || Rc <= g.Rmin);
+    const double phi = 2.0 * M_PI * rng.uniform();
+    double zc;
+    do {
+        X = rng.uniform();
+        zc = (X <= 0.5) ? g.hz * std::log(2.0 * X) : -g.hz * std::log(2.0 * (1.0 - X));
+    } while (g.zmax > 0.0 && std::fabs(zc) >= g.zmax);
+    x = Rc * std::cos(phi);
+    y = Rc * std::sin(phi);
+    z = zc;
+}
 
 // ---------------------------------------------------------------- wavelength grid
 struct WavelengthGrid {

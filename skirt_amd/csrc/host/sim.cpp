@@ -162,10 +162,17 @@ int skirt_sim_attach(SkirtSim* s, int device) {
     }
     int ns = (int)m.starL.size();
     std::vector<int> gk(ns, SKIRT_GEOM_PLUMMER);
-    std::vector<double> gp(4 * ns, 0.0), lum(ns * Nl), cdf(Nl * (ns + 1));
+    std::vector<double> gp(8 * ns, 0.0), lum(ns * Nl), cdf(Nl * (ns + 1));
     for (int h = 0; h < ns; h++) {
-        gp[4 * h] = m.starGeom[h].c;
-        gp[4 * h + 1] = m.starGeom[h].rho0;
+        const Geometry& g = m.starGeom[h];
+        if (g.kind == GeometryKind::ExpDisk) {
+            gk[h] = SKIRT_GEOM_EXPDISK;
+            const double v[6] = {g.hR, g.hz, g.Rmax, g.zmax, g.Rmin, g.rho0};
+            for (int q = 0; q < 6; q++) gp[8 * h + q] = v[q];
+        } else {
+            gp[8 * h] = g.c;
+            gp[8 * h + 1] = g.rho0;
+        }
         for (int ell = 0; ell < Nl; ell++) lum[h * Nl + ell] = m.starL[h][ell];
     }
     for (int ell = 0; ell < Nl; ell++)

@@ -104,6 +104,22 @@ def philox(ctr, key):
     return list(o)
 
 
+def star_positions(ski, comp, n, seed=1):
+    """n random positions of stellar component `comp` ([n, 3]) and the geometry's density there."""
+    L = lib()
+    L.oracle_star_positions.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int, ctypes.c_int,
+                                        ctypes.c_uint64, ctypes.POINTER(ctypes.c_double),
+                                        ctypes.POINTER(ctypes.c_double)]
+    out = np.zeros((n, 3))
+    dens = np.zeros(n)
+    rc = L.oracle_star_positions(ski.encode(), DATA_DIR.encode(), comp, n, seed,
+                                 out.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
+                                 dens.ctypes.data_as(ctypes.POINTER(ctypes.c_double)))
+    if rc:
+        raise RuntimeError("oracle failed: " + L.oracle_last_error().decode())
+    return out, dens
+
+
 def grid_paths(ski, rays, maxseg=4096):
     """DustGrid::path of the ski's dust grid for rays [n, 6] (position, direction): a list of
     (boxes [nseg, 6] (NaN rows before the grid), ds [nseg]) per ray, and the grid's cell count."""

@@ -55,6 +55,30 @@ GRIDS = {
 }
 
 
+# ExpDiskGeometry variants: stars and dust in exponential disks (the first PlummerGeometry of a model is
+# its stellar component's, the second its dust component's)
+STAR_DISK = '<ExpDiskGeometry radialScale="120 pc" axialScale="25 pc" radialTrunc="0 pc" axialTrunc="0 pc" innerRadius="0 pc"/>'
+DUST_DISK = ('<ExpDiskGeometry radialScale="150 pc" axialScale="40 pc" radialTrunc="450 pc" axialTrunc="300 pc" '
+             'innerRadius="20 pc"/>')
+GEOMETRIES = {
+    "disk_cart": ("pan_cart16", STAR_DISK, DUST_DISK),
+    "disk_oct": ("pan_oct", STAR_DISK, DUST_DISK),
+}
+
+
+def write_geometry(name, directory):
+    """Writes geometry variant `name` into `directory` and returns its path."""
+    base, star, dust = GEOMETRIES[name]
+    text = open(os.path.join(GOLD, base + ".ski")).read()
+    parts = text.split('<PlummerGeometry scale="100 pc"/>')
+    assert len(parts) == 3, name
+    text = parts[0] + star + parts[1] + dust + parts[2]
+    path = os.path.join(directory, name + ".ski")
+    with open(path, "w") as f:
+        f.write(text)
+    return path
+
+
 def write(name, directory):
     """Writes variant `name` into `directory` and returns its path."""
     base, grid = GRIDS[name]
