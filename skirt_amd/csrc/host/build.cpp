@@ -23,6 +23,7 @@
 #include <stdexcept>
 #include <thread>
 
+#include "dustemission.hpp"
 #include "model.hpp"
 #include "mt_random.hpp"
 #include "xml.hpp"
@@ -561,6 +562,56 @@ std::vector<double> sunSedNormalized(const Ctx& c, const WavelengthGrid& wl) {
     return Lv;
 }
 
+// SED::setluminosities (SED.cpp): normalized to unit sum
+static std::vector<double> normalizedSed(std::vector<double> Lv) {
+    const double s = nr::sum(Lv);
+    if (s <= 0) throw std::runtime_error("the total luminosity in the SED is zero or negative");
+    for (auto& v : Lv) v /= s;
+    return Lv;
+}
+
+std::vector<double> blackBodySedNormalized(double T, const WavelengthGrid& wl) {
+    // BlackBodySED.cpp setupSelfBefore: per wavelength bin, the 101-point trapezoid rule of B(lambda)
+    // lambda over log10(lambda) between lambdamin and lambdamax, times ln 10 dloglambda
+    if (T <= 0) throw std::runtime_error("the black body temperature T should be positive");
+    std::vector<double> Lv(wl.n());
+    for (int ell = 0; ell < wl.n(); ell++) {
+        const int N = 100;
+        const double loglambdamin = std::log10(wl.lambdamin(ell));
+        const double loglambdamax = std::log10(wl.lambdamax(ell));
+        const double dloglambda = (loglambdamax - loglambdamin) / N;
+        double sum = 0;
+        for (int i = 0; i <= N; i++) {
+            double weight = 1.0;
+            if (i == 0 || i == N) weight = 0.5;
+            const double loglambda = loglambdamin + i * dloglambda;
+            const double lambda = std::pow(10, loglambda);
+            sum += weight * planckFunction(T, lambda) * lambda;
+        }
+        Lv[ell] = sum * M_LN10 * dloglambda;
+    }
+    return normalizedSed(Lv);
+}
+
+std::vector<double> quasarSedNormalized(const WavelengthGrid& wl) {
+    // QuasarSED.cpp setupSelfBefore: a broken power law in micron, then SED::setemissivities
+    std::vector<double> Lv(wl.n());
+    for (int ell = 0; ell < wl.n(); ell++) {
+        double lambda = wl.lambda[ell];
+        lambda *= 1e6;
+        double j = 0.0;
+        const double a = 1.0, b = 0.003981072, cq = 0.001258926, d = 0.070376103;
+        if (lambda < 0.001) j = 0.0;
+        else if (lambda < 0.01) j = a * std::pow(lambda, 0.2);
+        else if (lambda < 0.1) j = b * std::pow(lambda, -1.0);
+        else if (lambda < 5.0) j = cq * std::pow(lambda, -1.5);
+        else if (lambda < 1000.0) j = d * std::pow(lambda, -4.0);
+        else j = 0.0;
+        Lv[ell] = j * wl.dlambda[ell];
+    }
+    return normalizedSed(Lv);
+}
+
 // ------------------------------------------------------------ octree
 // TreeDustGrid::setupSelfBefore / subdivide (TreeDustGrid.cpp:50-233), OctTreeNode (OctTreeNode.cpp),
 // TreeNode neighbor bookkeeping (TreeNode.cpp). Nodes are kept as indices into flat arrays; the
@@ -1094,13 +1145,16 @@ Model loadSki(const std::string& path, UniformSource& rng, const std::string& da
         } else if (sc->name == "PanStellarComp") {
             const XmlElement* sed = need(sc, "sed");
             const XmlElement* norm = need(sc, "normalization");
-            if (sed->name != "SunSED") throw std::runtime_error("unsupported stellar SED " + sed->name);
             if (norm->name != "BolLuminosityStellarCompNormalization")
                 throw std::runtime_error("unsupported stellar normalization " + norm->name);
             double Lsunits = attr(c, norm, "luminosity", "", 0);
             if (Lsunits <= 0) throw std::runtime_error("the bolometric luminosity should be positive");
             double Ltot = Lsunits * constants::Lsun;
-            std::vector<double> sedL = sunSedNormalized(c, m.wl);
+            std::vector<double> sedL;
+            if (sed->name == "SunSED") sedL = sunSedNormalized(c, m.wl);
+            else if (sed->name == "BlackBodySED") sedL = blackBodySedNormalized(attr(c, sed, "temperature", "temperature", 0), m.wl);
+            else if (sed->name == "QuasarSED") sedL = quasarSedNormalized(m.wl);
+            else throw std::runtime_error("unsupported stellar SED " + sed->name);
             std::vector<double> Lv(Nlambda);
             for (int ell = 0; ell < Nlambda; ell++) Lv[ell] = Ltot * sedL[ell];
             m.starL.push_back(Lv);

@@ -31,3 +31,31 @@ def test_exp_disk_engine_matches_oracle_same_streams(tmp_path, name):
     np.testing.assert_allclose(seds, orc.seds[0], rtol=1e-9, atol=1e-300)
     np.testing.assert_allclose(frames.sum(axis=2), orc.frames[0].sum(axis=2), rtol=1e-9, atol=1e-300)
     assert close_fraction(frames, orc.frames[0], 1e-9) > 0.999
+
+
+def test_dust_free_blackbody_engine_matches_oracle(tmp_path):
+    """A dust-free model (every packet ends at its emission peel-off, detected by the event kernel)
+    with a BlackBodySED, a FullInstrument and an SEDInstrument: the engine's tallies equal the oracle's
+    on the same streams."""
+    from test_seds import SKI
+    full = ('<FullInstrument instrumentName="f" distance="10 Mpc" inclination="60 deg" azimuth="0 deg" '
+            'positionAngle="0 deg" fieldOfViewX="1000 pc" pixelsX="24" centerX="0 pc" fieldOfViewY="1000 pc" '
+            'pixelsY="20" centerY="0 pc" scatteringLevels="2"/>')
+    text = SKI % {"N": 12, "SED": '<BlackBodySED temperature="8000 K"/>'}
+    text = text.replace("<SEDInstrument", full + "\n            <SEDInstrument")
+    path = str(tmp_path / "bb_free.ski")
+    with open(path, "w") as f:
+        f.write(text)
+    packages = 20000
+    sim = S.Simulation(path, packages=packages)
+    sim.attach(0)
+    sim.run_stellar()
+    sim.fetch()
+    orc = O.run(path, rng=O.RNG_PHILOX, threads=16, packages=packages)
+    assert sim.stats()["packets"] == orc.packets
+    for i in range(2):
+        frames, seds = sim.instrument(i)
+        np.testing.assert_allclose(seds, orc.seds[i], rtol=1e-12, atol=1e-300)
+        if orc.frames[i] is not None and orc.frames[i].size:
+            np.testing.assert_allclose(frames.sum(axis=2), orc.frames[i].sum(axis=2), rtol=1e-9, atol=1e-300)
+            assert close_fraction(frames, orc.frames[i], 1e-9) > 0.999
