@@ -46,7 +46,7 @@ enum {
 
 enum { SKIRT_GRID_CARTESIAN = 0, SKIRT_GRID_OCTREE = 1, SKIRT_GRID_VORONOI = 2 };
 enum { SKIRT_TREE_TOPDOWN = 0, SKIRT_TREE_NEIGHBOR = 1, SKIRT_TREE_BOOKKEEPING = 2 /* octrees only */ };
-enum { SKIRT_GEOM_PLUMMER = 0, SKIRT_GEOM_EXPDISK = 1 };
+enum { SKIRT_GEOM_PLUMMER = 0, SKIRT_GEOM_EXPDISK = 1, SKIRT_GEOM_SERSIC = 2 };
 enum { SKIRT_INSTR_FULL = 0, SKIRT_INSTR_SIMPLE = 1, SKIRT_INSTR_SED = 2, SKIRT_INSTR_FRAME = 3 };
 enum { SKIRT_PHASE_STELLAR = 0, SKIRT_PHASE_DUST_EMISSION = 1, SKIRT_PHASE_DUST_SELFABS = 2 };
 
@@ -105,11 +105,14 @@ typedef struct {
     int ncomp, nlambda;
     const int* geom_kind;       /* ncomp, SKIRT_GEOM_* */
     const double* geom_param;   /* ncomp x 8: PlummerGeometry {c, rho0, 0...};
-                                   ExpDiskGeometry {hR, hz, Rmax, zmax, Rmin, rho0, 0, 0} */
+                                   ExpDiskGeometry {hR, hz, Rmax, zmax, Rmin, rho0, 0, 0};
+                                   SersicGeometry {reff, n, rho0, 0...} (tables in geom_table) */
     const double* lum;          /* ncomp x nlambda, W */
     const double* lumtot;       /* nlambda, sum over components */
     const double* cdf;          /* nlambda x (ncomp+1) normalized cumulative luminosity */
     double emission_bias;
+    const double* geom_table;   /* ncomp x 202 (NULL if no component needs it): SersicGeometry's
+                                   SersicFunction tables {s_0..s_100, M_0..M_100} */
 } SkirtSourceDesc;
 
 /* Distant instruments (DistantInstrument.cpp:27-50, SingleFrameInstrument.cpp:24-38, 130-147). */

@@ -749,6 +749,9 @@ public:
         if (geo.kind == GeometryKind::ExpDisk) {
             // ExpDiskGeometry::randomR / randomz, SepAxGeometry::generatePosition
             expDiskPosition(geo, rng, pos.x, pos.y, pos.z);
+        } else if (geo.kind == GeometryKind::Sersic) {
+            // SersicGeometry::randomradius, SpheGeometry::generatePosition
+            sersicPosition(geo, rng, pos.x, pos.y, pos.z);
         } else {
             // PlummerGeometry::randomradius then SpheGeometry::generatePosition
             double t = pow(rng.uniform(), 1.0 / 3.0);
@@ -1055,6 +1058,8 @@ int oracle_star_positions(const char* ski, const char* datadir, int comp, int n,
             double* o = out + 3 * (size_t)i;
             if (geo.kind == GeometryKind::ExpDisk) {
                 expDiskPosition(geo, rng, o[0], o[1], o[2]);
+            } else if (geo.kind == GeometryKind::Sersic) {
+                sersicPosition(geo, rng, o[0], o[1], o[2]);
             } else {
                 const double t = pow(rng.uniform(), 1.0 / 3.0);
                 const double r = geo.c * t / sqrt((1.0 - t) * (1.0 + t));

@@ -59,6 +59,7 @@ constexpr int kStepsPerPull = SKIRT_STEPS_PER_PULL;  // grid steps between two r
 #define SKIRT_HALVES 1
 #endif
 constexpr int kHalves = SKIRT_HALVES;
+constexpr int kSersicTable = 202;  // SersicFunction: 101 radii, then 101 cumulative masses
 constexpr int kDetectCopies = 8;   // LDS copies of the SED sums in the detect kernel (one per 8 lanes)
 constexpr int kPollEvery = 1;      // iterations between two counter copies of a half
 constexpr int kPollRing = 3;       // copies in flight per half (the host reads each kPollRing copies late)
@@ -185,6 +186,7 @@ struct Args {
     // sources
     int nstar;
     const double* geomParam;
+    const double* geomTable;     // per component kSersicTable words: SersicFunction s_i, then M_i
     const double* lum;
     const double* lumtot;
     const double* cdf;
@@ -276,6 +278,21 @@ __host__ __device__ __forceinline__ unsigned leafIndex(int N, unsigned x, unsign
 __host__ __device__ __forceinline__ unsigned long long leafMapSize(int N) {
     const unsigned long long nb = leafBricks(N);
     return 8ull * nb * nb * nb;
+}
+
+// NR::interpolate_loglog (Fundamentals/NR.hpp:321-345): logarithmic in x, and in f when both f > 0
+__device__ __forceinline__ double interpolateLogLog(double x, double x1, double x2, double f1, double f2) {
+    x = log10(x);
+    x1 = log10(x1);
+    x2 = log10(x2);
+    const bool logf = f1 > 0 && f2 > 0;
+    if (logf) {
+        f1 = log10(f1);
+        f2 = log10(f2);
+    }
+    double fx = f1 + ((x - x1) / (x2 - x1)) * (f2 - f1);
+    if (logf) fx = pow(10.0, fx);
+    return fx;
 }
 
 __device__ __forceinline__ void atomicAddF64(double* p, double v) {
@@ -1869,6 +1886,25 @@ struct Events {
         const double* gp = a.geomParam + 8 * h;
         if ((int)gp[7] == SKIRT_GEOM_EXPDISK) {
             expDiskPosition(p.rng, gp, p.rx, p.ry, p.rz);
+        } else if ((int)gp[7] == SKIRT_GEOM_SERSIC) {
+            // SersicGeometry::randomradius (SersicFunction::inversemass: locate_clip + log-log
+            // interpolation of the cumulative mass table) and SpheGeometry::generatePosition
+            const double* sv = a.geomTable + (size_t)kSersicTable * h;
+            const double* Mv = sv + kSersicTable / 2;
+            constexpr int Ns = kSersicTable / 2;
+            const double M = p.rng.uniform();
+            double sr;
+            if (M <= Mv[0]) sr = sv[0];
+            else if (M >= Mv[Ns - 1]) sr = sv[Ns - 1];
+            else {
+                int jl = -1, ju = Ns - 1;  // NR::locate_clip
+                while (ju - jl > 1) { const int jm = (ju + jl) >> 1; if (M < Mv[jm]) ju = jm; else jl = jm; }
+                sr = interpolateLogLog(M, Mv[jl], Mv[jl + 1], sv[jl], sv[jl + 1]);
+            }
+            const double rr = gp[0] * sr;
+            double ux, uy, uz;
+            isotropic(p.rng, ux, uy, uz);
+            p.rx = rr * ux; p.ry = rr * uy; p.rz = rr * uz;
         } else {
             // PlummerGeometry::randomradius (t = u^(1/3)) and SpheGeometry::generatePosition
             const double c = gp[0];
@@ -2186,6 +2222,7 @@ struct SkirtMcrt {
     // sources
     int nstar = 0;
     double *dGeomParam = nullptr, *dLum = nullptr, *dLumtot = nullptr, *dCdf = nullptr;
+    double* dGeomTable = nullptr;  // SersicGeometry tables, kSersicTable per component
     double emissionBias = 0.5;
     // dust-phase cell sources and the dust Labs tally
     double *dCellLv = nullptr, *dCellCdf = nullptr, *dCellLtot = nullptr;
@@ -2679,9 +2716,15 @@ int skirt_mcrt_upload_sources(SkirtMcrt* c, const SkirtSourceDesc* s) {
     if (s->ncomp < 1 || s->nlambda < 1) return fail(c, SKIRT_ERR_ARG, "bad source sizes");
     // device geometry table: the 8 parameters of each component with its kind in the last word
     std::vector<double> gp(8 * (size_t)s->ncomp);
+    bool tables = false;
     for (int h = 0; h < s->ncomp; h++) {
-        if (s->geom_kind[h] != SKIRT_GEOM_PLUMMER && s->geom_kind[h] != SKIRT_GEOM_EXPDISK)
+        if (s->geom_kind[h] != SKIRT_GEOM_PLUMMER && s->geom_kind[h] != SKIRT_GEOM_EXPDISK &&
+            s->geom_kind[h] != SKIRT_GEOM_SERSIC)
             return fail(c, SKIRT_ERR_UNSUPPORTED, "unsupported source geometry");
+        if (s->geom_kind[h] == SKIRT_GEOM_SERSIC) {
+            if (!s->geom_table) return fail(c, SKIRT_ERR_ARG, "SersicGeometry without its tables");
+            tables = true;
+        }
         for (int q = 0; q < 7; q++) gp[8 * h + q] = s->geom_param[8 * h + q];
         gp[8 * h + 7] = (double)s->geom_kind[h];
     }
@@ -2693,6 +2736,12 @@ int skirt_mcrt_upload_sources(SkirtMcrt* c, const SkirtSourceDesc* s) {
     c->nlambda = s->nlambda;
     int rc;
     if ((rc = upload(c, c->dGeomParam, gp.data(), gp.size()))) return rc;
+    if (tables) {
+        if ((rc = upload(c, c->dGeomTable, s->geom_table, (size_t)kSersicTable * s->ncomp))) return rc;
+    } else if (c->dGeomTable) {
+        (void)hipFree(c->dGeomTable);
+        c->dGeomTable = nullptr;
+    }
     if ((rc = upload(c, c->dLum, s->lum, (size_t)s->ncomp * s->nlambda))) return rc;
     if ((rc = upload(c, c->dLumtot, s->lumtot, (size_t)s->nlambda))) return rc;
     if ((rc = upload(c, c->dCdf, s->cdf, (size_t)s->nlambda * (s->ncomp + 1)))) return rc;
@@ -3011,7 +3060,7 @@ int skirt_mcrt_run_phase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, 
     a.ncomp = std::max(1, c->ncomp); a.nlambda = c->nlambda;
     a.rho = c->dRho;
     a.optics = c->dOptics;
-    a.nstar = c->nstar; a.geomParam = c->dGeomParam; a.lum = c->dLum;
+    a.nstar = c->nstar; a.geomParam = c->dGeomParam; a.geomTable = c->dGeomTable; a.lum = c->dLum;
     a.lumtot = c->dLumtot; a.cdf = c->dCdf; a.emissionBias = c->emissionBias;
     a.ninstr = (int)c->instr.size(); a.instr = c->dInstr; a.nsed = c->nsed;
     a.npp = npp; a.first = first; a.end = first + count; a.seed = seed;
@@ -3277,7 +3326,7 @@ void skirt_mcrt_destroy(SkirtMcrt* c) {
                     c->dEmisSigma, c->dEmisMu, c->dEmisTv, c->dEmisPlanck, c->dEmisLambda, c->dEmisDlambda,
                     c->dEmisScratch, c->dDevCell, c->dSite, c->dCellBbox, c->dCellNbrOffset, c->dCellNbr,
                     c->dBlockOffset, c->dBlockList, c->dRho,
-                    c->dOptics, c->dGeomParam, c->dLum, c->dLumtot, c->dCdf, c->dInstr,
+                    c->dOptics, c->dGeomParam, c->dGeomTable, c->dLum, c->dLumtot, c->dCdf, c->dInstr,
                     c->dClaim, c->dStats, c->dError, c->dCtr, c->dPool};
     for (void* b : bufs)
         if (b) (void)hipFree(b);

@@ -117,6 +117,10 @@ static int locate(const std::vector<double>& xv, double x) {
     if (x == xv[n - 1]) return n - 2;
     return locateBasic(xv, x, n);
 }
+static int locateClip(const std::vector<double>& xv, double x) {
+    if (x < xv[0]) return 0;
+    return locateBasic(xv, x, (int)xv.size() - 1);
+}
 static int locateFail(const std::vector<double>& xv, double x) {
     int n = (int)xv.size();
     if (x > xv[n - 1]) return -1;
@@ -184,6 +188,16 @@ double Geometry::density(double x, double y, double z) const {
         double s = r / c;
         return rho0 * std::pow(1.0 + s * s, -2.5);
     }
+    case GeometryKind::Sersic: {
+        // SpheGeometry::density(Position) -> SersicGeometry::density(r) = rho0 S(r/reff)
+        const double r = std::sqrt(x * x + y * y + z * z);
+        const double s = r / reff;
+        const int Ns = (int)sv.size();
+        if (s <= sv[0]) return rho0 * Sv[0];
+        if (s >= sv[Ns - 1]) return rho0 * Sv[Ns - 1];
+        const int i = nr::locateClip(sv, s);
+        return rho0 * nr::interpolateLogLog(s, sv[i], sv[i + 1], Sv[i], Sv[i + 1]);
+    }
     case GeometryKind::ExpDisk: {
         // AxGeometry::density(Position) -> ExpDiskGeometry::density(R, z) (Position::cylradius)
         const double R = std::sqrt(x * x + y * y);
@@ -195,6 +209,84 @@ double Geometry::density(double x, double y, double z) const {
     }
     }
     return 0;
+}
+
+double Geometry::sersicInverseMass(double M) const {
+    const int Ns = (int)sv.size();
+    if (M <= Mv[0]) return sv[0];
+    if (M >= Mv[Ns - 1]) return sv[Ns - 1];
+    const int i = nr::locateClip(Mv, M);
+    return nr::interpolateLogLog(M, Mv[i], Mv[i + 1], sv[i], sv[i + 1]);
+}
+
+// SpecialFunctions::lngamma / gamma (SpecialFunctions.cpp:16-40)
+static double lngamma(double a) {
+    static const double cof[6] = {76.18009172947146, -86.50532032941677, 24.01409824083091, -1.231739572450155,
+                                  0.1208650973866179e-2, -0.5395239384953e-5};
+    double y, xx, tmp, ser;
+    y = xx = a;
+    tmp = xx + 5.5;
+    tmp -= (xx + 0.5) * std::log(tmp);
+    ser = 1.000000000190015;
+    for (int j = 0; j < 6; j++) ser += cof[j] / ++y;
+    return -tmp + std::log(2.5066282746310005 * ser / xx);
+}
+
+// SersicFunction::SersicFunction(n) (SersicFunction.cpp): S(s) by the Abel-type integral on a
+// 10001-point trapezoid, M(s) by a 33-point trapezoid per table interval, normalized
+static void buildSersicTables(Geometry& g) {
+    const double n = g.n;
+    if (n < 0.5 || n > 10.0) throw std::runtime_error("The Sersic parameter should be between 0.5 and 10");
+    const double b = 2.0 * n - 1.0 / 3.0 + 4.0 / 405.0 / n + 46.0 / 25515.0 / (n * n) + 131.0 / 1148175.0 / (n * n * n);
+    const double I0 = std::pow(b, 2.0 * n) / (M_PI * std::exp(lngamma(2.0 * n + 1)));
+    const int Ns = 101;
+    g.sv.assign(Ns, 0.0);
+    g.Sv.assign(Ns, 0.0);
+    g.Mv.assign(Ns, 0.0);
+    const double logsmin = -6.0, logsmax = 4.0;
+    const double dlogs = (logsmax - logsmin) / (Ns - 1.0);
+    for (int i = 0; i < Ns; i++) {
+        const double logs = logsmin + i * dlogs;
+        const double s = std::pow(10.0, logs);
+        g.sv[i] = s;
+        const double alpha = b * std::pow(s, 1.0 / n);
+        double sum = 0.0;
+        const int Nu = 10000;
+        const double tmax = 100.0;
+        const double umax = std::sqrt((tmax + 1.0) * (tmax - 1.0));
+        const double du = umax / Nu;
+        for (int j = 0; j <= Nu; j++) {
+            double weight = 1.0;
+            if (j == 0 || j == Nu) weight = 0.5;
+            const double u = j * du;
+            const double u2 = u * u;
+            double w;
+            if (u > 1e-3) w = (std::pow(1.0 + u2, 2.0 * n) - 1.0) / u2;
+            else w = 2.0 * n + n * (2.0 * n - 1.0) * u2 + 2.0 / 3.0 * n * (2.0 * n - 1.0) * (n - 1.0) * u2 * u2;
+            const double integrandum = 2.0 * std::exp(-alpha * (1.0 + u2)) / std::sqrt(w);
+            sum += weight * integrandum;
+        }
+        g.Sv[i] = I0 * std::pow(b, n) * std::pow(alpha, 1.0 - n) / M_PI * du * sum;
+    }
+    auto S = [&](double s) {  // SersicFunction::operator()
+        if (s <= g.sv[0]) return g.Sv[0];
+        if (s >= g.sv[Ns - 1]) return g.Sv[Ns - 1];
+        const int i = nr::locateClip(g.sv, s);
+        return nr::interpolateLogLog(s, g.sv[i], g.sv[i + 1], g.Sv[i], g.Sv[i + 1]);
+    };
+    for (int i = 1; i < Ns; i++) {
+        double sum = 0.0;
+        for (int j = 0; j <= 32; j++) {
+            double weight = 1.0;
+            if (j == 0 || j == 32) weight = 0.5;
+            const double ds = (g.sv[i] - g.sv[i - 1]) / 32.0;
+            const double s = g.sv[i - 1] + j * ds;
+            sum += weight * S(s) * s * s * ds;
+        }
+        const double dM = 4.0 * M_PI * sum;
+        g.Mv[i] = g.Mv[i - 1] + dM;
+    }
+    for (int i = 0; i < Ns; i++) g.Mv[i] /= g.Mv[Ns - 1];
 }
 
 double lambertW1(double z) {
@@ -376,6 +468,15 @@ Geometry parseGeometry(const Ctx& c, const XmlElement* g) {
         geo.c = attr(c, g, "scale", "length", 0);
         if (geo.c <= 0) throw std::runtime_error("the scale length c should be positive");
         geo.rho0 = 0.75 / std::pow(geo.c, 3) / M_PI;
+    } else if (g->name == "SersicGeometry") {
+        // SersicGeometry::setupSelfBefore
+        geo.kind = GeometryKind::Sersic;
+        geo.n = attr(c, g, "index", "", 0);
+        geo.reff = attr(c, g, "radius", "length", 0);
+        if (geo.n <= 0.5 || geo.n > 10) throw std::runtime_error("the Sersic index n should be between 0.5 and 10");
+        if (geo.reff <= 0) throw std::runtime_error("the effective radius should be positive");
+        geo.rho0 = 1.0 / (geo.reff * geo.reff * geo.reff);
+        buildSersicTables(geo);
     } else if (g->name == "ExpDiskGeometry") {
         // ExpDiskGeometry::setupSelfBefore (ExpDiskGeometry.cpp): checks and the normalization rho0
         geo.kind = GeometryKind::ExpDisk;
@@ -1070,9 +1171,10 @@ static void buildVoronoiGrid(const Ctx& c, const XmlElement* ge, Model& m, Unifo
                 if (X < cum[0]) h = 0;
                 else h = nr::locateBasic(cum, X, (int)cum.size() - 1);
                 const Geometry& geo = m.dust[h].geom;
-                if (geo.kind == GeometryKind::ExpDisk) {
+                if (geo.kind != GeometryKind::Plummer) {
                     double x, y, z;
-                    expDiskPosition(geo, rng, x, y, z);
+                    if (geo.kind == GeometryKind::ExpDisk) expDiskPosition(geo, rng, x, y, z);
+                    else sersicPosition(geo, rng, x, y, z);
                     if (contains(x, y, z)) {
                         sites[3 * q] = x; sites[3 * q + 1] = y; sites[3 * q + 2] = z;
                         break;

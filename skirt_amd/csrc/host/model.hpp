@@ -23,15 +23,21 @@ namespace skirt {
 // rho0; density; randomR with SpecialFunctions::LambertW1; randomz) and SepAxGeometry::generatePosition
 // (R, then phi = 2 pi u, then z; Position(R, phi, z, CYLINDRICAL), Position.cpp:23-31).
 // The kind values are the engine's (skirt_mcrt.h SKIRT_GEOM_*).
-enum class GeometryKind : int { Plummer = 0, ExpDisk = 1 };
+// SersicGeometry.cpp (setupSelfBefore, density, randomradius) with SersicFunction.cpp (its 101-point
+// tables of the deprojected profile S(s) and the cumulative mass M(s), log-log interpolated) and
+// SpheGeometry::generatePosition (radius, then Random::direction).
+enum class GeometryKind : int { Plummer = 0, ExpDisk = 1, Sersic = 2 };
 
 struct Geometry {
     GeometryKind kind = GeometryKind::Plummer;
     double c = 0;     // Plummer scale length
-    double rho0 = 0;  // Plummer: 0.75/c^3/pi (PlummerGeometry.cpp setupSelfBefore); ExpDisk: its rho0
+    double rho0 = 0;  // Plummer: 0.75/c^3/pi (PlummerGeometry.cpp setupSelfBefore); ExpDisk, Sersic: theirs
     double hR = 0, hz = 0, Rmax = 0, zmax = 0, Rmin = 0;  // ExpDisk scales and truncations (0: none)
+    double n = 0, reff = 0;                    // Sersic index and effective radius
+    std::vector<double> sv, Sv, Mv;            // SersicFunction tables
 
     double density(double x, double y, double z) const;
+    double sersicInverseMass(double M) const;  // SersicFunction::inversemass
 };
 
 // SpecialFunctions::LambertW1 (SKIRTcore/SpecialFunctions.cpp:579-626): the W_{-1} branch
@@ -54,6 +60,23 @@ void expDiskPosition(const Geometry& g, R& rng, double& x, double& y, double& z)
     x = Rc * std::cos(phi);
     y = Rc * std::sin(phi);
     z = zc;
+}
+
+// SersicGeometry::randomradius then SpheGeometry::generatePosition: Random::direction() as
+// Direction(theta, phi) with theta = acos(2u-1), phi = 2 pi u' (Random.cpp:179-184, Direction.cpp)
+template <class R>
+void sersicPosition(const Geometry& g, R& rng, double& x, double& y, double& z) {
+    const double r = g.reff * g.sersicInverseMass(rng.uniform());
+    const double theta = std::acos(2.0 * rng.uniform() - 1.0);
+    const double phi = 2.0 * M_PI * rng.uniform();
+    double kx, ky, kz;
+    if (theta <= 1e-8) { kx = 0; ky = 0; kz = 1; }
+    else if (theta >= M_PI - 1e-8) { kx = 0; ky = 0; kz = -1; }
+    else {
+        const double st = std::sin(theta);
+        kx = st * std::cos(phi); ky = st * std::sin(phi); kz = std::cos(theta);
+    }
+    x = r * kx; y = r * ky; z = r * kz;
 }
 
 // ---------------------------------------------------------------- wavelength grid

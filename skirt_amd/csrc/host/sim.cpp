@@ -162,10 +162,18 @@ int skirt_sim_attach(SkirtSim* s, int device) {
     }
     int ns = (int)m.starL.size();
     std::vector<int> gk(ns, SKIRT_GEOM_PLUMMER);
-    std::vector<double> gp(8 * ns, 0.0), lum(ns * Nl), cdf(Nl * (ns + 1));
+    std::vector<double> gp(8 * ns, 0.0), lum(ns * Nl), cdf(Nl * (ns + 1)), gt;
     for (int h = 0; h < ns; h++) {
         const Geometry& g = m.starGeom[h];
-        if (g.kind == GeometryKind::ExpDisk) {
+        if (g.kind == GeometryKind::Sersic) {
+            gk[h] = SKIRT_GEOM_SERSIC;
+            gp[8 * h] = g.reff; gp[8 * h + 1] = g.n; gp[8 * h + 2] = g.rho0;
+            gt.resize(202 * (size_t)ns, 0.0);
+            for (int q = 0; q < 101; q++) {
+                gt[202 * (size_t)h + q] = g.sv[q];
+                gt[202 * (size_t)h + 101 + q] = g.Mv[q];
+            }
+        } else if (g.kind == GeometryKind::ExpDisk) {
             gk[h] = SKIRT_GEOM_EXPDISK;
             const double v[6] = {g.hR, g.hz, g.Rmax, g.zmax, g.Rmin, g.rho0};
             for (int q = 0; q < 6; q++) gp[8 * h + q] = v[q];
@@ -177,7 +185,8 @@ int skirt_sim_attach(SkirtSim* s, int device) {
     }
     for (int ell = 0; ell < Nl; ell++)
         for (int q = 0; q <= ns; q++) cdf[ell * (ns + 1) + q] = m.starX[ell][q];
-    SkirtSourceDesc sd{ns, Nl, gk.data(), gp.data(), lum.data(), m.starLtot.data(), cdf.data(), m.starEmissionBias};
+    SkirtSourceDesc sd{ns, Nl, gk.data(), gp.data(), lum.data(), m.starLtot.data(), cdf.data(), m.starEmissionBias,
+                       gt.empty() ? nullptr : gt.data()};
     if ((rc = check(s, skirt_mcrt_upload_sources(s->eng, &sd)))) return rc;
     std::vector<SkirtInstrDesc> ids;
     for (const Instrument& ins : m.instruments) {

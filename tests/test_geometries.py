@@ -75,8 +75,8 @@ def test_exp_disk_positions_follow_the_density(tmp_path, comp_geom):
     assert np.all(np.abs(chi) < 6) and np.mean(chi ** 2) < 2.0, chi
 
 
-@pytest.mark.parametrize("name", ["disk_cart", "disk_oct"])
-def test_exp_disk_models_run_deterministically(tmp_path, name):
+@pytest.mark.parametrize("name", ["disk_cart", "disk_oct", "bulge_oct", "sersic_cart"])
+def test_geometry_models_run_deterministically(tmp_path, name):
     """The oracle's MT mode (the reference's -t 1 draw order) runs the disk models; two runs agree bit
     for bit and the tallies are positive and finite."""
     path = T.write_geometry(name, str(tmp_path))
@@ -86,3 +86,28 @@ def test_exp_disk_models_run_deterministically(tmp_path, name):
     np.testing.assert_array_equal(a.labs, b.labs)
     assert np.isfinite(a.labs).all() and a.labs.sum() > 0
     np.testing.assert_array_equal(a.seds[0], b.seds[0])
+
+
+@pytest.mark.parametrize("geom,n,reff_pc", [("SERSIC4", 4.0, 60.0), ("SERSIC1", 1.5, 120.0)])
+def test_sersic_positions_have_the_effective_radius(tmp_path, geom, n, reff_pc):
+    """SersicGeometry: the deprojected profile (SersicFunction's tables) sampled by inverse mass and an
+    isotropic direction puts half of the projected light inside reff -- the defining property of the
+    effective radius, independent of the tables' construction. Also rho = rho0 S(r/reff) > 0."""
+    base = "pan_cart16"
+    T.GEOMETRIES["_probe"] = (base, getattr(T, geom), T.DUST_DISK)
+    try:
+        path = T.write_geometry("_probe", str(tmp_path))
+    finally:
+        del T.GEOMETRIES["_probe"]
+    N = 400000
+    pos, dens = O.star_positions(path, 0, N, seed=777)
+    reff = reff_pc * PC
+    Rproj = np.hypot(pos[:, 0], pos[:, 1])
+    frac = np.mean(Rproj < reff)
+    assert abs(frac - 0.5) < 0.005, frac
+    assert np.all(dens > 0)
+    r = np.linalg.norm(pos, axis=1)
+    # isotropy and a density decreasing with radius
+    assert abs(np.mean(pos[:, 2] / r)) < 0.01
+    order = np.argsort(r)
+    assert np.all(np.diff(dens[order][:: N // 50]) <= 0)

@@ -1,6 +1,6 @@
-"""ExpDiskGeometry stars and dust on the GPU against the CPU oracle on the same Philox streams (the
-geometry's restatement is checked on its own in tests/test_geometries.py; parity unpinned against the
-reference itself, which has no fixture for it)."""
+"""ExpDiskGeometry and SersicGeometry stars and dust on the GPU against the CPU oracle on the same Philox
+streams (the geometries' restatements are checked on their own in tests/test_geometries.py; parity
+unpinned against the reference itself, which has no fixture for them)."""
 import numpy as np
 import pytest
 
@@ -12,8 +12,8 @@ from test_gpu_parity import close_fraction
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("name", ["disk_cart", "disk_oct"])
-def test_exp_disk_engine_matches_oracle_same_streams(tmp_path, name):
+@pytest.mark.parametrize("name", ["disk_cart", "disk_oct", "bulge_oct", "sersic_cart"])
+def test_geometry_engine_matches_oracle_same_streams(tmp_path, name):
     path = T.write_geometry(name, str(tmp_path))
     packages = 3000
     sim = S.Simulation(path, packages=packages)

@@ -60,9 +60,14 @@ GRIDS = {
 STAR_DISK = '<ExpDiskGeometry radialScale="120 pc" axialScale="25 pc" radialTrunc="0 pc" axialTrunc="0 pc" innerRadius="0 pc"/>'
 DUST_DISK = ('<ExpDiskGeometry radialScale="150 pc" axialScale="40 pc" radialTrunc="450 pc" axialTrunc="300 pc" '
              'innerRadius="20 pc"/>')
+SERSIC4 = '<SersicGeometry index="4" radius="60 pc"/>'
+SERSIC1 = '<SersicGeometry index="1.5" radius="120 pc"/>'
 GEOMETRIES = {
     "disk_cart": ("pan_cart16", STAR_DISK, DUST_DISK),
     "disk_oct": ("pan_oct", STAR_DISK, DUST_DISK),
+    # a Sersic bulge in a dust disk, and Sersic dust (density sampling of the host setup)
+    "bulge_oct": ("pan_oct", SERSIC4, DUST_DISK),
+    "sersic_cart": ("pan_cart16", SERSIC1, SERSIC4),
 }
 
 
