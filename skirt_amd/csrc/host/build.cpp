@@ -617,6 +617,35 @@ DustMix parseMix(const Ctx& c, const XmlElement* e, const WavelengthGrid& wl) {
         sabs.push_back(nr::resample<nr::interpolateLogLog>(wl.lambda, lambdav, kabsv));
         ssca.push_back(nr::resample<nr::interpolateLogLog>(wl.lambda, lambdav, kscav));
         gv.push_back(nr::resample<nr::interpolateLogLin>(wl.lambda, lambdav, gvv));
+    } else if (e->name == "MeanZubkoDustMix" || e->name == "DraineLiDustMix") {
+        // MeanZubkoDustMix.cpp / DraineLiDustMix.cpp setupSelfBefore: cross sections per H atom, then
+        // DustMix::addpopulation(mu, ...) (DustMix.cpp:300-321) with its wavelength check and resampling
+        const bool zubko = e->name == "MeanZubkoDustMix";
+        Table t = readTable(c.datadir, zubko ? "MeanZubkoDustMix.bin" : "DraineLiDustMix.bin");
+        const int N = zubko ? 1201 : 800;
+        if (t.nrows != N || t.ncols != 6) throw std::runtime_error("unexpected " + e->name + " table shape");
+        std::vector<double> lambdav(N), sabsv(N), sscav(N), gvv(N);
+        for (int k = 0; k < N; k++) {
+            lambdav[k] = t.at(k, 0) * 1e-6;
+            if (zubko) {
+                const double sigmaext = t.at(k, 3) * 1e-4;
+                const double albedo = t.at(k, 4);
+                sabsv[k] = (1. - albedo) * sigmaext;
+                sscav[k] = albedo * sigmaext;
+            } else {
+                sabsv[k] = t.at(k, 1) * 1e-4;
+                sscav[k] = t.at(k, 2) * 1e-4;
+            }
+            gvv[k] = t.at(k, 5);
+        }
+        double eps = 0.5e-5;
+        if (wl.lambda[0] < lambdav[0] * (1 - eps) || wl.lambda[Nlambda - 1] > lambdav[N - 1] * (1 + eps))
+            throw std::runtime_error("dust properties not defined over the simulation's wavelength range");
+        const double MdustoverMH = 5.4e-4 + 5.4e-4 + 1.8e-4 + 2.33e-3 + 8.27e-3;
+        muv.push_back(zubko ? 1.44e-29 : MdustoverMH * constants::mproton);
+        sabs.push_back(nr::resample<nr::interpolateLogLog>(wl.lambda, lambdav, sabsv));
+        ssca.push_back(nr::resample<nr::interpolateLogLog>(wl.lambda, lambdav, sscav));
+        gv.push_back(nr::resample<nr::interpolateLogLin>(wl.lambda, lambdav, gvv));
     } else {
         throw std::runtime_error("unsupported dust mix " + e->name);
     }

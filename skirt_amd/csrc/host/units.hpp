@@ -21,6 +21,7 @@ constexpr double AU = 1.49597871e11;
 constexpr double pc = 3.08567758e16;
 constexpr double Msun = 1.9891e30;
 constexpr double Lsun = 3.839e26;
+constexpr double mproton = 1.67262178e-27;  // Units.cpp _Mproton
 constexpr double lambdaV = 550e-9;
 constexpr double kappaV = 2600.;
 }  // namespace constants

@@ -59,3 +59,20 @@ def test_dust_free_blackbody_engine_matches_oracle(tmp_path):
         if orc.frames[i] is not None and orc.frames[i].size:
             np.testing.assert_allclose(frames.sum(axis=2), orc.frames[i].sum(axis=2), rtol=1e-9, atol=1e-300)
             assert close_fraction(frames, orc.frames[i], 1e-9) > 0.999
+
+
+@pytest.mark.parametrize("name", ["zubko_cart", "draineli_cart"])
+def test_dust_mix_engine_matches_oracle_same_streams(tmp_path, name):
+    path = T.write_mix(name, str(tmp_path))
+    packages = 3000
+    sim = S.Simulation(path, packages=packages)
+    sim.attach(0)
+    sim.run_stellar()
+    sim.fetch()
+    orc = O.run(path, rng=O.RNG_PHILOX, threads=16, packages=packages)
+    assert sim.stats()["packets"] == orc.packets
+    labs = sim.labs()
+    np.testing.assert_allclose(labs.sum(axis=0), orc.labs.sum(axis=0), rtol=1e-9)
+    assert close_fraction(labs, orc.labs, 1e-9) > 0.999
+    frames, seds = sim.instrument(0)
+    np.testing.assert_allclose(seds, orc.seds[0], rtol=1e-9, atol=1e-300)

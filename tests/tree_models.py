@@ -84,6 +84,25 @@ def write_geometry(name, directory):
     return path
 
 
+# dust mixes besides InterstellarDustMix, on the Pan Cartesian model
+MIXES = {
+    "zubko_cart": ("pan_cart16", '<MeanZubkoDustMix writeMix="false" writeMeanMix="false"/>'),
+    "draineli_cart": ("pan_cart16", '<DraineLiDustMix writeMix="false" writeMeanMix="false"/>'),
+}
+
+
+def write_mix(name, directory):
+    """Writes dust-mix variant `name` into `directory` and returns its path."""
+    base, mix = MIXES[name]
+    text = open(os.path.join(GOLD, base + ".ski")).read()
+    old = '<InterstellarDustMix writeMix="false" writeMeanMix="false"/>'
+    assert text.count(old) == 1, name
+    path = os.path.join(directory, name + ".ski")
+    with open(path, "w") as f:
+        f.write(text.replace(old, mix))
+    return path
+
+
 def write(name, directory):
     """Writes variant `name` into `directory` and returns its path."""
     base, grid = GRIDS[name]

@@ -57,6 +57,18 @@ def main():
     rows = read_rows(os.path.join(src, "DustMix/InterstellarDustMix.dat"))
     assert len(rows) == 1064, len(rows)
     write_bin(os.path.join(dst, "InterstellarDustMix.bin"), rows)
+
+    # MeanZubkoDustMix.dat: '#' header lines, then rows of lambda [micron], Cabs, Csca, tau [cm2/H], albedo,
+    # g; MeanZubkoDustMix.cpp reads the first 1201 of them
+    rows = read_rows(os.path.join(src, "DustMix/MeanZubkoDustMix.dat"))
+    assert len(rows) >= 1201, len(rows)
+    write_bin(os.path.join(dst, "MeanZubkoDustMix.bin"), rows[:1201])
+
+    # DraineLiDustMix.dat: '#' header lines, then 800 rows of lambda [micron], Cabs, Csca [cm2/H], emission,
+    # albedo, g (DraineLiDustMix.cpp)
+    rows = read_rows(os.path.join(src, "DustMix/DraineLiDustMix.dat"))
+    assert len(rows) >= 800, len(rows)
+    write_bin(os.path.join(dst, "DraineLiDustMix.bin"), rows[:800])
     print("wrote", dst)
 
 
