@@ -1044,6 +1044,27 @@ int oracle_grid_paths(const char* ski, const char* datadir, int n, const double*
     }
 }
 
+int oracle_dust_component(const char* ski, const char* datadir, int comp, double* nf, double* kext, double* lambda,
+                          int* nlambda) {
+    try {
+        std::string dd = datadir && *datadir ? datadir : defaultDataDir();
+        MTRandom mt(readSkiSeed(ski));
+        Model M = loadSki(ski, mt, dd);
+        if (comp < 0 || comp >= (int)M.dust.size()) throw std::runtime_error("no such dust component");
+        const DustComp& d = M.dust[comp];
+        *nf = d.nf;
+        *nlambda = M.wl.n();
+        for (int ell = 0; ell < M.wl.n(); ell++) {
+            if (kext) kext[ell] = d.mix.kext[ell];
+            if (lambda) lambda[ell] = M.wl.lambda[ell];
+        }
+        return 0;
+    } catch (const std::exception& e) {
+        g_error = e.what();
+        return -1;
+    }
+}
+
 int oracle_star_positions(const char* ski, const char* datadir, int comp, int n, uint64_t seed, double* out,
                           double* density) {
     try {

@@ -69,6 +69,10 @@ int oracle_num_instruments(OracleRun* r);
  * the ray's segment count (capped at maxseg), *ncells the grid's cell count. Returns 0, -1 on failure. */
 int oracle_grid_paths(const char* ski, const char* datadir, int n, const double* rays, int maxseg, double* out,
                       int* nseg, int* ncells);
+/* dust component `comp` of the model: its normalization factor (the dust mass of a normalized geometry)
+ * and the mix's kappa_ext and the wavelengths (nlambda each, either may be NULL) */
+int oracle_dust_component(const char* ski, const char* datadir, int comp, double* nf, double* kext, double* lambda,
+                          int* nlambda);
 /* n random positions of stellar component `comp` (its geometry's generatePosition on an MT19937 stream
  * seeded with `seed`), 3 doubles each, and the geometry's density there (density may be NULL) */
 int oracle_star_positions(const char* ski, const char* datadir, int comp, int n, uint64_t seed, double* out,

@@ -211,6 +211,25 @@ double Geometry::density(double x, double y, double z) const {
     return 0;
 }
 
+double Geometry::SigmaR() const {
+    if (kind != GeometryKind::ExpDisk) throw std::runtime_error("Geometry is not axisymmetric");
+    if (Rmax > 0.0) return rho0 * hR * (std::exp(-Rmin / hR) - std::exp(-Rmax / hR));
+    return rho0 * hR * std::exp(-Rmin / hR);
+}
+double Geometry::SigmaZ() const {
+    if (kind != GeometryKind::ExpDisk) throw std::runtime_error("Geometry is not axisymmetric");
+    if (Rmin > 0.0) return 0.0;
+    if (zmax > 0.0) return -2.0 * rho0 * hz * std::expm1(-zmax / hz);
+    return 2.0 * rho0 * hz;
+}
+static double lngamma(double a);
+double Geometry::Sigmar() const {
+    if (kind == GeometryKind::Plummer) return 0.5 / (M_PI * c * c);
+    if (kind == GeometryKind::Sersic)
+        return 1.0 / (reff * reff) * std::pow(b, 2.0 * n) / (2.0 * M_PI * std::exp(lngamma(2.0 * n + 1.0)));
+    throw std::runtime_error("Geometry is not spherically symmetric");
+}
+
 double Geometry::sersicInverseMass(double M) const {
     const int Ns = (int)sv.size();
     if (M <= Mv[0]) return sv[0];
@@ -238,7 +257,8 @@ static void buildSersicTables(Geometry& g) {
     const double n = g.n;
     if (n < 0.5 || n > 10.0) throw std::runtime_error("The Sersic parameter should be between 0.5 and 10");
     const double b = 2.0 * n - 1.0 / 3.0 + 4.0 / 405.0 / n + 46.0 / 25515.0 / (n * n) + 131.0 / 1148175.0 / (n * n * n);
-    const double I0 = std::pow(b, 2.0 * n) / (M_PI * std::exp(lngamma(2.0 * n + 1)));
+    g.b = b;  // SersicGeometry::setupSelfBefore computes the same expression
+    const double I0 =std::pow(b, 2.0 * n) / (M_PI * std::exp(lngamma(2.0 * n + 1)));
     const int Ns = 101;
     g.sv.assign(Ns, 0.0);
     g.Sv.assign(Ns, 0.0);
@@ -651,6 +671,26 @@ DustMix parseMix(const Ctx& c, const XmlElement* e, const WavelengthGrid& wl) {
     }
     finishMix(mix, muv, sabs, ssca, gv, Nlambda);
     return mix;
+}
+
+// DustMix::kappaext(lambda) (DustMix.cpp:482-522): log-log interpolation on a panchromatic grid, the
+// matching wavelength (to 1e-5) of an oligochromatic one
+double mixKappaext(const DustMix& mix, const WavelengthGrid& wl, double lambda) {
+    if (wl.pan) {
+        const int ell = nr::locateFail(wl.lambda, lambda);
+        if (ell < 0) throw std::runtime_error("Optical properties are not defined for this wavelength");
+        const double p = (std::log10(lambda) - std::log10(wl.lambda[ell])) /
+                         (std::log10(wl.lambda[ell + 1]) - std::log10(wl.lambda[ell]));
+        const double kL = mix.kext[ell], kR = mix.kext[ell + 1];
+        if (kL > 0 && kR > 0) {
+            const double lL = std::log10(kL), lR = std::log10(kR);
+            return std::pow(10, lL + p * (lR - lL));
+        }
+        return kL + p * (kR - kL);
+    }
+    for (int ell = 0; ell < wl.n(); ell++)
+        if (std::fabs(lambda / wl.lambda[ell] - 1.0) < 1e-5) return mix.kext[ell];
+    throw std::runtime_error("Optical properties are not defined for this wavelength");
 }
 
 // ------------------------------------------------------------ stellar components
@@ -1334,9 +1374,20 @@ Model loadSki(const std::string& path, UniformSource& rng, const std::string& da
             comp.geom = parseGeometry(c, need(dc, "geometry"));
             comp.mix = parseMix(c, need(dc, "mix"), m.wl);
             const XmlElement* nrm = need(dc, "normalization");
-            if (nrm->name != "DustMassDustCompNormalization")
+            if (nrm->name == "DustMassDustCompNormalization") {
+                comp.nf = attr(c, nrm, "dustMass", "mass", 0);
+            } else if (nrm->name == "FaceOnDustCompNormalization" || nrm->name == "EdgeOnDustCompNormalization" ||
+                       nrm->name == "RadialDustCompNormalization") {
+                // {FaceOn,EdgeOn,Radial}DustCompNormalization::normalizationFactor:
+                // tau / (Sigma * kappaext(lambda)), Sigma = SigmaZ / SigmaR / Sigmar
+                const double tau = attr(c, nrm, "opticalDepth", "", 0);
+                const double lambda = attr(c, nrm, "wavelength", "wavelength", 0);
+                const double Sigma = nrm->name[0] == 'F' ? comp.geom.SigmaZ()
+                                     : nrm->name[0] == 'E' ? comp.geom.SigmaR() : comp.geom.Sigmar();
+                comp.nf = tau / (Sigma * mixKappaext(comp.mix, m.wl, lambda));
+            } else {
                 throw std::runtime_error("unsupported dust normalization " + nrm->name);
-            comp.nf = attr(c, nrm, "dustMass", "mass", 0);
+            }
             m.dust.push_back(comp);
         }
         if (m.dust.empty()) throw std::runtime_error("dust distribution has no components");

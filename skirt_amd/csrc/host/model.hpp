@@ -33,11 +33,16 @@ struct Geometry {
     double c = 0;     // Plummer scale length
     double rho0 = 0;  // Plummer: 0.75/c^3/pi (PlummerGeometry.cpp setupSelfBefore); ExpDisk, Sersic: theirs
     double hR = 0, hz = 0, Rmax = 0, zmax = 0, Rmin = 0;  // ExpDisk scales and truncations (0: none)
-    double n = 0, reff = 0;                    // Sersic index and effective radius
+    double n = 0, reff = 0, b = 0;             // Sersic index, effective radius and b(n)
     std::vector<double> sv, Sv, Mv;            // SersicFunction tables
 
     double density(double x, double y, double z) const;
     double sersicInverseMass(double M) const;  // SersicFunction::inversemass
+    // surface densities of the normalizations (AxGeometry::SigmaR / SigmaZ, SpheGeometry::Sigmar):
+    // ExpDiskGeometry.cpp SigmaR/SigmaZ, PlummerGeometry.cpp:73-77, SersicGeometry.cpp Sigmar
+    double SigmaR() const;
+    double SigmaZ() const;
+    double Sigmar() const;
 };
 
 // SpecialFunctions::LambertW1 (SKIRTcore/SpecialFunctions.cpp:579-626): the W_{-1} branch

@@ -140,3 +140,19 @@ def grid_paths(ski, rays, maxseg=4096):
     if rc:
         raise RuntimeError("oracle failed: " + L.oracle_last_error().decode())
     return [(out[i, :nseg[i], :6], out[i, :nseg[i], 6]) for i in range(n)], nc.value
+
+
+def dust_component(ski, comp=0):
+    """(normalization factor, kappa_ext per wavelength, wavelengths) of dust component `comp`."""
+    L = lib()
+    L.oracle_dust_component.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int,
+                                        ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
+                                        ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int)]
+    nf, nl = ctypes.c_double(), ctypes.c_int()
+    kext, lam = np.zeros(4096), np.zeros(4096)
+    rc = L.oracle_dust_component(ski.encode(), DATA_DIR.encode(), comp, ctypes.byref(nf),
+                                 kext.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
+                                 lam.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), ctypes.byref(nl))
+    if rc:
+        raise RuntimeError("oracle failed: " + L.oracle_last_error().decode())
+    return nf.value, kext[:nl.value].copy(), lam[:nl.value].copy()
