@@ -46,7 +46,7 @@ enum {
 
 enum { SKIRT_GRID_CARTESIAN = 0, SKIRT_GRID_OCTREE = 1, SKIRT_GRID_VORONOI = 2 };
 enum { SKIRT_TREE_TOPDOWN = 0, SKIRT_TREE_NEIGHBOR = 1, SKIRT_TREE_BOOKKEEPING = 2 /* octrees only */ };
-enum { SKIRT_GEOM_PLUMMER = 0, SKIRT_GEOM_EXPDISK = 1, SKIRT_GEOM_SERSIC = 2 };
+enum { SKIRT_GEOM_PLUMMER = 0, SKIRT_GEOM_EXPDISK = 1, SKIRT_GEOM_SERSIC = 2, SKIRT_GEOM_POINT = 3 };
 enum { SKIRT_INSTR_FULL = 0, SKIRT_INSTR_SIMPLE = 1, SKIRT_INSTR_SED = 2, SKIRT_INSTR_FRAME = 3 };
 enum { SKIRT_PHASE_STELLAR = 0, SKIRT_PHASE_DUST_EMISSION = 1, SKIRT_PHASE_DUST_SELFABS = 2 };
 

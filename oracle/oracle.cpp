@@ -746,7 +746,9 @@ public:
         }
         const Geometry& geo = M.starGeom[h];
         Vec3 pos;
-        if (geo.kind == GeometryKind::ExpDisk) {
+        if (geo.kind == GeometryKind::Point) {
+            pos = Vec3{0, 0, 0};  // PointGeometry::generatePosition: no draws
+        } else if (geo.kind == GeometryKind::ExpDisk) {
             // ExpDiskGeometry::randomR / randomz, SepAxGeometry::generatePosition
             expDiskPosition(geo, rng, pos.x, pos.y, pos.z);
         } else if (geo.kind == GeometryKind::Sersic) {
@@ -1077,7 +1079,9 @@ int oracle_star_positions(const char* ski, const char* datadir, int comp, int n,
         MTRng rng(&mtr);
         for (int i = 0; i < n; i++) {
             double* o = out + 3 * (size_t)i;
-            if (geo.kind == GeometryKind::ExpDisk) {
+            if (geo.kind == GeometryKind::Point) {
+                o[0] = o[1] = o[2] = 0.0;
+            } else if (geo.kind == GeometryKind::ExpDisk) {
                 expDiskPosition(geo, rng, o[0], o[1], o[2]);
             } else if (geo.kind == GeometryKind::Sersic) {
                 sersicPosition(geo, rng, o[0], o[1], o[2]);

@@ -1884,7 +1884,9 @@ struct Events {
             L = L0 * (1.0 / (1.0 - xi + xi * Lmean / Lh));
         }
         const double* gp = a.geomParam + 8 * h;
-        if ((int)gp[7] == SKIRT_GEOM_EXPDISK) {
+        if ((int)gp[7] == SKIRT_GEOM_POINT) {
+            p.rx = 0.0; p.ry = 0.0; p.rz = 0.0;  // PointGeometry::generatePosition: no draws
+        } else if ((int)gp[7] == SKIRT_GEOM_EXPDISK) {
             expDiskPosition(p.rng, gp, p.rx, p.ry, p.rz);
         } else if ((int)gp[7] == SKIRT_GEOM_SERSIC) {
             // SersicGeometry::randomradius (SersicFunction::inversemass: locate_clip + log-log
@@ -2719,7 +2721,7 @@ int skirt_mcrt_upload_sources(SkirtMcrt* c, const SkirtSourceDesc* s) {
     bool tables = false;
     for (int h = 0; h < s->ncomp; h++) {
         if (s->geom_kind[h] != SKIRT_GEOM_PLUMMER && s->geom_kind[h] != SKIRT_GEOM_EXPDISK &&
-            s->geom_kind[h] != SKIRT_GEOM_SERSIC)
+            s->geom_kind[h] != SKIRT_GEOM_SERSIC && s->geom_kind[h] != SKIRT_GEOM_POINT)
             return fail(c, SKIRT_ERR_UNSUPPORTED, "unsupported source geometry");
         if (s->geom_kind[h] == SKIRT_GEOM_SERSIC) {
             if (!s->geom_table) return fail(c, SKIRT_ERR_ARG, "SersicGeometry without its tables");

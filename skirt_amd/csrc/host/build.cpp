@@ -15,6 +15,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cfloat>
+#include <limits>
 #include <cstring>
 #include <dlfcn.h>
 #include <fstream>
@@ -188,6 +189,8 @@ double Geometry::density(double x, double y, double z) const {
         double s = r / c;
         return rho0 * std::pow(1.0 + s * s, -2.5);
     }
+    case GeometryKind::Point:  // PointGeometry::density
+        return (x * x + y * y + z * z) == 0 ? std::numeric_limits<double>::infinity() : 0.0;
     case GeometryKind::Sersic: {
         // SpheGeometry::density(Position) -> SersicGeometry::density(r) = rho0 S(r/reff)
         const double r = std::sqrt(x * x + y * y + z * z);
@@ -488,6 +491,8 @@ Geometry parseGeometry(const Ctx& c, const XmlElement* g) {
         geo.c = attr(c, g, "scale", "length", 0);
         if (geo.c <= 0) throw std::runtime_error("the scale length c should be positive");
         geo.rho0 = 0.75 / std::pow(geo.c, 3) / M_PI;
+    } else if (g->name == "PointGeometry") {
+        geo.kind = GeometryKind::Point;
     } else if (g->name == "SersicGeometry") {
         // SersicGeometry::setupSelfBefore
         geo.kind = GeometryKind::Sersic;
@@ -1372,6 +1377,8 @@ Model loadSki(const std::string& path, UniformSource& rng, const std::string& da
         for (const XmlElement* dc : dd->items("components")) {
             DustComp comp;
             comp.geom = parseGeometry(c, need(dc, "geometry"));
+            if (comp.geom.kind == GeometryKind::Point)  // a delta density cannot be sampled on a dust grid
+                throw std::runtime_error("PointGeometry is not supported for dust components");
             comp.mix = parseMix(c, need(dc, "mix"), m.wl);
             const XmlElement* nrm = need(dc, "normalization");
             if (nrm->name == "DustMassDustCompNormalization") {

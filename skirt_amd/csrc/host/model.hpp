@@ -26,7 +26,8 @@ namespace skirt {
 // SersicGeometry.cpp (setupSelfBefore, density, randomradius) with SersicFunction.cpp (its 101-point
 // tables of the deprojected profile S(s) and the cumulative mass M(s), log-log interpolated) and
 // SpheGeometry::generatePosition (radius, then Random::direction).
-enum class GeometryKind : int { Plummer = 0, ExpDisk = 1, Sersic = 2 };
+// PointGeometry.cpp: every position at the origin (no random draws), an infinite density there.
+enum class GeometryKind : int { Plummer = 0, ExpDisk = 1, Sersic = 2, Point = 3 };
 
 struct Geometry {
     GeometryKind kind = GeometryKind::Plummer;

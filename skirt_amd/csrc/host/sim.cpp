@@ -165,7 +165,9 @@ int skirt_sim_attach(SkirtSim* s, int device) {
     std::vector<double> gp(8 * ns, 0.0), lum(ns * Nl), cdf(Nl * (ns + 1)), gt;
     for (int h = 0; h < ns; h++) {
         const Geometry& g = m.starGeom[h];
-        if (g.kind == GeometryKind::Sersic) {
+        if (g.kind == GeometryKind::Point) {
+            gk[h] = SKIRT_GEOM_POINT;
+        } else if (g.kind == GeometryKind::Sersic) {
             gk[h] = SKIRT_GEOM_SERSIC;
             gp[8 * h] = g.reff; gp[8 * h + 1] = g.n; gp[8 * h + 2] = g.rho0;
             gt.resize(202 * (size_t)ns, 0.0);

@@ -75,7 +75,7 @@ def test_exp_disk_positions_follow_the_density(tmp_path, comp_geom):
     assert np.all(np.abs(chi) < 6) and np.mean(chi ** 2) < 2.0, chi
 
 
-@pytest.mark.parametrize("name", ["disk_cart", "disk_oct", "bulge_oct", "sersic_cart"])
+@pytest.mark.parametrize("name", ["disk_cart", "disk_oct", "bulge_oct", "sersic_cart", "point_oct", "point_cart"])
 def test_geometry_models_run_deterministically(tmp_path, name):
     """The oracle's MT mode (the reference's -t 1 draw order) runs the disk models; two runs agree bit
     for bit and the tallies are positive and finite."""
@@ -111,3 +111,22 @@ def test_sersic_positions_have_the_effective_radius(tmp_path, geom, n, reff_pc):
     assert abs(np.mean(pos[:, 2] / r)) < 0.01
     order = np.argsort(r)
     assert np.all(np.diff(dens[order][:: N // 50]) <= 0)
+
+
+def test_point_geometry_positions_are_the_origin(tmp_path):
+    """PointGeometry (SKIRTcore/PointGeometry.cpp): generatePosition returns the origin without random
+    draws, the density is infinite there and zero elsewhere."""
+    path = T.write_geometry("point_oct", str(tmp_path))
+    pos, dens = O.star_positions(path, 0, 1000, seed=5)
+    assert np.all(pos == 0.0)
+    assert np.all(np.isinf(dens))
+
+
+def test_point_geometry_is_refused_for_dust(tmp_path):
+    T.GEOMETRIES["_pdust"] = ("pan_oct", T.STAR_DISK, T.POINT)
+    try:
+        path = T.write_geometry("_pdust", str(tmp_path))
+    finally:
+        del T.GEOMETRIES["_pdust"]
+    with pytest.raises(RuntimeError, match="PointGeometry"):
+        O.run(path, rng=O.RNG_MT, threads=1, packages=10)

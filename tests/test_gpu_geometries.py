@@ -12,7 +12,7 @@ from test_gpu_parity import close_fraction
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("name", ["disk_cart", "disk_oct", "bulge_oct", "sersic_cart"])
+@pytest.mark.parametrize("name", ["disk_cart", "disk_oct", "bulge_oct", "sersic_cart", "point_oct", "point_cart"])
 def test_geometry_engine_matches_oracle_same_streams(tmp_path, name):
     path = T.write_geometry(name, str(tmp_path))
     packages = 3000

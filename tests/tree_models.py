@@ -62,12 +62,16 @@ DUST_DISK = ('<ExpDiskGeometry radialScale="150 pc" axialScale="40 pc" radialTru
              'innerRadius="20 pc"/>')
 SERSIC4 = '<SersicGeometry index="4" radius="60 pc"/>'
 SERSIC1 = '<SersicGeometry index="1.5" radius="120 pc"/>'
+POINT = '<PointGeometry/>'
 GEOMETRIES = {
     "disk_cart": ("pan_cart16", STAR_DISK, DUST_DISK),
     "disk_oct": ("pan_oct", STAR_DISK, DUST_DISK),
     # a Sersic bulge in a dust disk, and Sersic dust (density sampling of the host setup)
     "bulge_oct": ("pan_oct", SERSIC4, DUST_DISK),
     "sersic_cart": ("pan_cart16", SERSIC1, SERSIC4),
+    # a point source (PointGeometry) at the origin, a cell corner of both grids
+    "point_oct": ("pan_oct", POINT, DUST_DISK),
+    "point_cart": ("pan_cart16", POINT, DUST_DISK),
 }
 
 
