@@ -139,7 +139,7 @@ struct alignas(16) VoronoiNbr {
 };
 constexpr int kVorLast = (int)0x80000000u;
 #ifndef SKIRT_VOR_UNROLL
-#define SKIRT_VOR_UNROLL 4
+#define SKIRT_VOR_UNROLL 8
 #endif
 constexpr int kVorUnroll = SKIRT_VOR_UNROLL;  // list entries loaded per round trip (the array is padded)
 
