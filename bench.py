@@ -33,7 +33,9 @@ CONFIGS = {
 }
 DUST_CONFIGS = ("c5",)
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip-level parameters (spec)
-ATOMIC_PEAK_ADDS = 2.36e10  # scattered 8-byte atomic adds per second, measured (profiles/r01_atomic_bench.txt)
+# f64 atomic requests per second (one scattered add per 64-byte request), measured chip-wide
+# (tools/atomic_bench.hip, profiles/r01_atomic_bench.txt); requests carrying 2-8 adds of one line cost the same
+ATOMIC_PEAK_REQUESTS = 2.36e10
 
 
 def pmc_traffic(config):
@@ -98,7 +100,7 @@ def main():
     torch.cuda.set_device(local)
 
     import skirt_amd
-    from skirt_amd.sharding import allreduce_tallies, shard_range
+    from skirt_amd.sharding import TallyReducer, shard_slice
 
     ski_rel, ppl_default, geom_bytes, desc = CONFIGS[args.config]
     ski = os.path.join(REPO, ski_rel)
@@ -107,9 +109,9 @@ def main():
     sim = skirt_amd.Simulation(ski, packages=float(ppl * world))
     setup_s = time.perf_counter() - t_setup  # host model setup: grid, densities (outside the timed region)
     info = sim.info
-    # weak scaling: the phase has ppl packets per wavelength per rank; rank r shoots its contiguous
-    # slice of the global packet index space
-    first, share = shard_range(ppl * info.nlambda * world, rank, world)
+    # weak scaling: the phase has ppl packets per wavelength per rank; rank r shoots its slice of every
+    # wavelength (the reference's IdenticalAssigner, skirt_mcrt_run_phase_shard)
+    share = shard_slice(ppl * world, rank, world)[1] * info.nlambda
     sim.attach(local)
     if args.threshold or args.slots or args.trace_grid:
         sim.configure(slots=args.slots, grid=args.trace_grid, threshold=args.threshold)
@@ -120,24 +122,24 @@ def main():
     instr = torch.zeros(max(1, n_instr), dtype=torch.float64, device="cuda")
     sim.bind_tallies(labs.data_ptr(), instr.data_ptr())
     dust_phases = args.config in DUST_CONFIGS
+    bound = [labs, instr]
     if dust_phases:
         dust = torch.zeros(max(1, n_labs), dtype=torch.float64, device="cuda")
         sim.bind_dust_labs(dust.data_ptr())
-    sim.zero_tallies()
+        bound.append(dust)
+    # the reference's reductions (PanDustSystem::sumResults, Instrument::sumResults) as RCCL all-reduces,
+    # called by the engine at the phase ends (skirt_mcrt_set_reducer)
+    sim.set_reducer(TallyReducer(*bound))
 
     def step():
-        if not dust_phases:
-            sim.run_stellar(first, share)
-            # phase end: PanDustSystem::sumResults (Labs) and Instrument::sumResults, over RCCL/xGMI
-            allreduce_tallies(labs, instr)
-            return
-        # the whole simulation (PanMonteCarloSimulation::runSelf): stellar emission, the Labs summed over
-        # ranks, the self-absorption cycles (dust Labs summed after each), dust emission, instruments
+        # one simulation's photon phases from zeroed tallies, as the reference runs each phase once
         sim.zero_tallies()
-        sim.run_stellar(first, share)
-        allreduce_tallies(labs)
-        sim.run_dust(rank, world, lambda: allreduce_tallies(dust))
-        allreduce_tallies(instr)
+        sim.run_stellar_shard(rank, world)  # + the Labs summed over the ranks at the phase end
+        if dust_phases:
+            # PanMonteCarloSimulation::runSelf: self-absorption cycles (dust Labs summed after each) and
+            # dust emission, every phase sharded over the ranks' slices of every wavelength
+            sim.run_dust(rank, world)
+        sim.reduce_instruments()  # Instrument::sumResults
 
     for _ in range(args.warmup):
         step()
@@ -147,7 +149,7 @@ def main():
     torch.cuda.synchronize()
     s0 = sim.stats()
     kernel_ms = []
-    per_step = []  # dust configs zero the tallies (and counters) every step: collect each step's counters
+    per_step = []  # every step zeroes the tallies and counters: collect each step's counters
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
@@ -165,13 +167,12 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    delta = {k: s1[k] - s0[k] for k in s1 if k not in ("kernel_ms", "iterations", "device_cells")}
-    if dust_phases:
-        for k in ("packets", "segments_fill", "segments_walk", "segments_peel", "detects", "absorb_adds", "lane_slots",
-                  "labs_requests"):
-            delta[k] = sum(st[k] for st in per_step)
+    delta = {k: sum(st[k] for st in per_step) for k in ("packets", "segments_fill", "segments_walk", "segments_peel",
+                                                        "detects", "absorb_adds", "lane_slots", "labs_requests")}
+    delta["trace_ms"] = s1["trace_ms"] - s0["trace_ms"]
+    delta["trace_launches"] = s1["trace_launches"] - s0["trace_launches"]
     trace_ms, trace_launches = delta["trace_ms"], delta["trace_launches"]
-    packets_all = share * world * args.steps
+    packets_all = ppl * world * info.nlambda * args.steps
     if dust_phases:
         # every phase's launched packets (stellar, self-absorption cycles, dust emission), all ranks
         n = torch.tensor([float(delta["packets"])], dtype=torch.float64, device="cuda")
@@ -179,8 +180,7 @@ def main():
             dist.all_reduce(n)
         packets_all = float(n.item())
     value = packets_all / elapsed
-    launched = torch.tensor([float(sum(st["packets"] for st in per_step) if dust_phases else delta["packets"])],
-                            dtype=torch.float64, device="cuda")
+    launched = torch.tensor([float(delta["packets"])], dtype=torch.float64, device="cuda")
     if world > 1:
         dist.all_reduce(launched)
     launched_rate = float(launched.item()) / elapsed
@@ -193,6 +193,9 @@ def main():
     bytes_per_launch = trace_bytes / max(1, trace_launches)
     achieved = bytes_per_launch / launch_s / 1e9
     traffic = pmc_traffic(args.config)
+    hbm_frac = achieved / HBM_PEAK_GBS
+    requests_per_s = delta["labs_requests"] / max(1e-9, trace_ms / 1e3)
+    atomic_frac = requests_per_s / ATOMIC_PEAK_REQUESTS
 
     result = {
         "metric": "photon packets/sec (whole node), 128^3 octree, 1/2/4/8 MI355X + HBM%",
@@ -228,23 +231,28 @@ def main():
                            ("segments_fill", "segments_walk", "segments_peel", "absorb_adds", "detects")},
         },
         "roofline": {
-            "bound": "hbm",
+            # the limiter is whichever resource the trace kernel uses the largest fraction of: HBM bytes
+            # (SURVEY 8(d) algorithmic bytes) or the chip's f64 atomic request rate (the Labs adds)
+            "bound": "hbm" if hbm_frac >= atomic_frac else "atomic",
             "achieved": achieved,
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS,
+            "frac": hbm_frac,
+            "atomic_frac": atomic_frac,
             "traffic": traffic["bytes_per_launch"] if traffic else None,
             "kernel": {0: "traceKernel<cartesian>", 1: "traceKernel<octree leaf map>", 2: "traceKernel<voronoi>"}[info.grid_kind],
             "launch_ms_avg": launch_s * 1e3,
             "launches_per_step": trace_launches / args.steps,
             "algorithmic_bytes_per_launch": bytes_per_launch,
             "traffic_source": traffic["source"] if traffic else None,
-            # what actually bounds the kernel: Labs adds are scattered f64 atomics, executed memory-side
-            # at a fixed chip-wide rate (tools/atomic_bench.hip, profiles/r01_atomic_bench.txt)
+            "traffic_gbs": traffic["bytes_per_launch"] / launch_s / 1e9 if traffic else None,
+            # Labs adds are scattered f64 atomics, executed memory-side in 64-byte requests at a fixed
+            # chip-wide request rate (tools/atomic_bench.hip, profiles/r01_atomic_bench.txt); adds of one
+            # wave instruction that fall in one line share a request
             "labs_atomic_adds_per_s": delta["absorb_adds"] / max(1e-9, trace_ms / 1e3),
-            # adds that shared a 64-byte request (same line, same wave instruction)
+            "labs_requests_per_s": requests_per_s,
             "labs_adds_per_request": delta["absorb_adds"] / max(1, delta["labs_requests"]),
-            "labs_atomic_peak_measured": ATOMIC_PEAK_ADDS,
+            "atomic_request_peak_measured": ATOMIC_PEAK_REQUESTS,
         },
         "phase_ms_avg": avg_kernel_s * 1e3,
     }

@@ -6,9 +6,10 @@
  * construction, cell density sampling, optical tables, instrument geometry) runs on the host exactly as
  * in the reference; the photon loop runs on the GPU through include/skirt_mcrt.h.
  *
- * Multi-GPU: one process per GPU. Each process loads the same ski, attaches its device and runs a slice
- * of the global packet index space (skirt_sim_run_stellar(first, count)); the caller sums the device
- * tallies across processes (RCCL all-reduce) before calling skirt_sim_write on one rank.
+ * Multi-GPU: one process per GPU. Each process loads the same ski, attaches its device, sets the
+ * engine's reducer (e.g. an RCCL all-reduce) and runs its shard of every phase
+ * (skirt_sim_run_stellar_shard, skirt_sim_run_dust_shard); skirt_sim_fetch then returns the whole
+ * simulation's tallies on every rank, and one rank calls skirt_sim_write.
  */
 #ifndef SKIRT_HOST_H
 #define SKIRT_HOST_H
@@ -50,15 +51,13 @@ int skirt_sim_run_stellar(SkirtSim* sim, uint64_t first, uint64_t count);
  * whose detections add to the instrument tallies. Single process; fetches the stellar Labs first.
  * Returns after launching the dust emission phase (asynchronous, like run_stellar). */
 int skirt_sim_run_dust(SkirtSim* sim);
-/* The same, one rank of `world` processes (one per GPU): every phase shoots this rank's contiguous slice
- * of its packets, and after each self-absorption cycle `reduce(user, SKIRT_REDUCE_DUST_LABS)` must sum
- * the engine's dust Labs device buffer over all ranks in place (e.g. an RCCL all-reduce of the tensor
- * bound with skirt_mcrt_bind_dust_labs, on the engine's stream), as PanDustSystem::Labsdusttot and
- * the next cycle's spectra need the whole simulation's absorption. The stellar Labs on the device must
- * already be summed over ranks. Returns nonzero if `reduce` does. */
-enum { SKIRT_REDUCE_DUST_LABS = 0 };
-typedef int (*SkirtReduceFn)(void* user, int what);
-int skirt_sim_run_dust_sharded(SkirtSim* sim, int rank, int world, SkirtReduceFn reduce, void* user);
+/* Multi-GPU: the same phases on rank `rank` of `world` processes (one per GPU). Every phase shoots this
+ * rank's slice of EVERY wavelength (skirt_mcrt_run_phase_shard, the reference's IdenticalAssigner), and
+ * the engine's reducer (skirt_mcrt_set_reducer, required for world > 1) sums the stellar Labs after the
+ * stellar phase, the dust Labs after every self-absorption cycle and the instruments before they are
+ * read, so every rank follows the same self-absorption schedule as one process would. */
+int skirt_sim_run_stellar_shard(SkirtSim* sim, int rank, int world);
+int skirt_sim_run_dust_shard(SkirtSim* sim, int rank, int world);
 /* dust Labs of the last self-absorption cycle (row-major cell x wavelength), or NULL */
 const double* skirt_sim_labs_dust(SkirtSim* sim);
 /* Labsdusttot after every self-absorption cycle; returns the number of cycles */

@@ -9,8 +9,9 @@
  * This ABI replaces those call sites (MonteCarloSimulation.cpp:256-257 stellar emission,
  * PanMonteCarloSimulation.cpp:144-145 self-absorption, :260-261 dust emission) with one device launch
  * per phase. The host describes the grid, media, sources and instruments once as flat arrays; each
- * run call shoots a contiguous range of global packet indices, so the packet space can be sharded
- * over GPUs (one process per GPU) with results independent of the shard count.
+ * run call shoots a range of global packet indices (run_phase) or one rank's slice of every wavelength
+ * (run_phase_shard), so a phase can be sharded over GPUs (one process per GPU) with results independent
+ * of the shard count.
  *
  * Conventions: plain C, host owns every host buffer, all functions return 0 on success and a nonzero
  * SKIRT_ERR_* code on failure (message via skirt_mcrt_last_error), no exceptions cross the boundary.
@@ -33,7 +34,7 @@
 extern "C" {
 #endif
 
-#define SKIRT_MCRT_ABI_VERSION 5
+#define SKIRT_MCRT_ABI_VERSION 6
 
 enum {
     SKIRT_OK = 0,
@@ -214,6 +215,31 @@ int skirt_mcrt_run_stellar(SkirtMcrt* ctx, uint64_t npp, uint64_t first, uint64_
  *                             cycles of the simulation (0, 1, ...) */
 int skirt_mcrt_run_phase(SkirtMcrt* ctx, int phase, uint32_t cycle, uint64_t npp, uint64_t first, uint64_t count,
                          uint64_t seed, const SkirtPhaseParams* params);
+/* Multi-GPU (one process per GPU): rank `rank` of `world` shoots packets [lo, lo + count) of EVERY
+ * wavelength, lo and count from skirt_mcrt_shard_slice. This is the reference's IdenticalAssigner
+ * (IdenticalAssigner.cpp:37-58), which gives each process a block of chunks at every wavelength through a
+ * SequentialAssigner (SequentialAssigner.cpp:37-59), with chunks of one packet. Philox streams are keyed
+ * on the global packet index (wavelength * npp + packet), so the union of the ranks' packets equals one
+ * unsharded run. world > 1 requires a reducer (below), which run_phase_shard calls at the phase end. */
+int skirt_mcrt_run_phase_shard(SkirtMcrt* ctx, int phase, uint32_t cycle, uint64_t npp, int rank, int world,
+                               uint64_t seed, const SkirtPhaseParams* params);
+void skirt_mcrt_shard_slice(uint64_t npp, int rank, int world, uint64_t* lo, uint64_t* count);
+/* The cross-process sum of the tallies (PanDustSystem::sumResults, PanDustSystem.cpp:394-403;
+ * Instrument::sumResults, Instrument.cpp:57-66). The engine calls fn(user, tally, d_buf, n, hip_stream)
+ * with a device buffer of n doubles that the callback must sum over all processes IN PLACE, ordered
+ * after the work already enqueued on hip_stream (e.g. ncclAllReduce(d_buf, d_buf, n, ncclDouble, ncclSum,
+ * comm, stream), an MPI_Allreduce after a stream synchronize, or torch.distributed over RCCL):
+ *   SKIRT_TALLY_LABS         at the end of every stellar run that stores absorption
+ *   SKIRT_TALLY_DUST_LABS    at the end of every self-absorption run (before Labsdusttot is read)
+ *   SKIRT_TALLY_INSTRUMENTS  once before the instrument tallies are read (skirt_mcrt_download, or
+ *                            skirt_mcrt_reduce_instruments); again only after a further run or zeroing
+ * A nonzero return fails the calling function. fn NULL disables the reduction (single process). Every
+ * run of a phase must start from tallies that are zero on all ranks but one, or zero everywhere (as in
+ * the reference, where each phase runs once per simulation). */
+enum { SKIRT_TALLY_LABS = 0, SKIRT_TALLY_DUST_LABS = 1, SKIRT_TALLY_INSTRUMENTS = 2 };
+typedef int (*SkirtReduceTallyFn)(void* user, int tally, double* d_buf, size_t n, void* hip_stream);
+int skirt_mcrt_set_reducer(SkirtMcrt* ctx, SkirtReduceTallyFn fn, void* user);
+int skirt_mcrt_reduce_instruments(SkirtMcrt* ctx);
 int skirt_mcrt_upload_cell_sources(SkirtMcrt* ctx, const SkirtCellSourceDesc* src);
 /* The same cell sources computed on the device from the current Labs tally (plus the dust Labs when
  * include_dust): grey-body spectra at the cells' equilibrium temperatures, cell luminosities and their
@@ -228,7 +254,8 @@ int skirt_mcrt_bind_dust_labs(SkirtMcrt* ctx, double* d_labs_dust);
 int skirt_mcrt_zero_dust_labs(SkirtMcrt* ctx);
 int skirt_mcrt_download_dust_labs(SkirtMcrt* ctx, double* labs_dust);
 int skirt_mcrt_synchronize(SkirtMcrt* ctx);
-/* Copies tallies to host (Labs converted to row-major cell x wavelength); either pointer may be NULL. */
+/* Copies tallies to host (Labs converted to row-major cell x wavelength); either pointer may be NULL.
+ * With a reducer set, the instrument tallies are summed over the processes first. */
 int skirt_mcrt_download(SkirtMcrt* ctx, double* labs, double* instr);
 int skirt_mcrt_stats(SkirtMcrt* ctx, SkirtStats* out);
 /* engine knobs (0 = default): packet slots in flight, trace-kernel workgroups, and the number of idle

@@ -841,7 +841,21 @@ void oracle_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t
 
 OracleRun* oracle_run(const char* ski, const char* datadir, int rngKind, int nthreads, double packages,
                       uint64_t seed, uint64_t packet_begin, uint64_t packet_end, int phases, const char* outprefix) {
+    return oracle_run_shard(ski, datadir, rngKind, nthreads, packages, seed, packet_begin, packet_end, phases,
+                            outprefix, 0, 1, nullptr, nullptr);
+}
+
+OracleRun* oracle_run_shard(const char* ski, const char* datadir, int rngKind, int nthreads, double packages,
+                            uint64_t seed, uint64_t packet_begin, uint64_t packet_end, int phases,
+                            const char* outprefix, int rank, int world, OracleReduceFn reduce, void* user) {
     try {
+        if (world < 1 || rank < 0 || rank >= world) throw std::runtime_error("bad shard (rank, world)");
+        if (world > 1 && (rngKind != ORACLE_RNG_PHILOX || packet_end))
+            throw std::runtime_error("a shard needs Philox streams and no packet range");
+        auto sum = [&](int tally, std::vector<double>& v) {
+            if (world > 1 && reduce && !v.empty() && reduce(user, tally, v.data(), v.size()))
+                throw std::runtime_error("the reduction failed");
+        };
         auto run = std::make_unique<OracleRun>();
         // the MT stream must be seeded before setup, so the seed is read from the XML first
         unsigned long theSeed = seed ? (unsigned long)seed : readSkiSeed(ski);
@@ -887,8 +901,23 @@ OracleRun* oracle_run(const char* ski, const char* datadir, int rngKind, int nth
         };
         // runs a phase over packets [pb, pe): MT mode in the reference's -t 1 order (chunk = wavelength,
         // packets in order), Philox mode over threads with one stream per packet
+        // (pb, pe) index the phase's packets of this process: all of them, wavelength-slowest, or with a
+        // shard (world > 1) the slice [lo, lo + cnt) of every wavelength (IdenticalAssigner.cpp:37-58)
+        uint64_t sliceLo = 0, sliceCnt = 0;  // sliceCnt 0: no shard
+        auto global = [&](const PhaseSpec& ph, uint64_t j) -> uint64_t {
+            if (!sliceCnt) return j;
+            const uint64_t ell = j / sliceCnt;
+            return ell * ph.Npp + sliceLo + (j - ell * sliceCnt);
+        };
         auto runPhase = [&](const PhaseSpec& ph, uint64_t pb, uint64_t pe) {
             Tallies& tl = run->tal;
+            if (world > 1) {
+                sliceLo = ph.Npp * (uint64_t)rank / (uint64_t)world;
+                sliceCnt = ph.Npp * (uint64_t)(rank + 1) / (uint64_t)world - sliceLo;
+                pb = 0;
+                pe = sliceCnt * (uint64_t)Nl;
+                if (!sliceCnt) return;
+            }
             if (rngKind == ORACLE_RNG_MT) {
                 Path p, tmp;
                 p.v.reserve(1024);
@@ -914,7 +943,8 @@ OracleRun* oracle_run(const char* ski, const char* datadir, int rngKind, int nth
                             uint64_t b = next.fetch_add(grain);
                             if (b >= pe) break;
                             uint64_t e = std::min(pe, b + grain);
-                            for (uint64_t pk = b; pk < e; pk++) {
+                            for (uint64_t j = b; j < e; j++) {
+                                const uint64_t pk = global(ph, j);
                                 rng.start(pk);
                                 shoot(ph, tl, rng, pk, p, tmp, cnt[w]);
                             }
@@ -940,9 +970,11 @@ OracleRun* oracle_run(const char* ski, const char* datadir, int rngKind, int nth
             uint64_t total = ph.Npp * (uint64_t)Nl;
             uint64_t pb = packet_begin, pe = packet_end ? std::min<uint64_t>(packet_end, total) : total;
             runPhase(ph, pb, pe);
+            if (ph.store) sum(ORACLE_TALLY_LABS, run->tal.labs);  // PanDustSystem::sumResults(true)
         }
         // ---- rundustselfabsorption + rundustemission (PanMonteCarloSimulation::runSelf, .cpp:96-105)
         if ((phases & ORACLE_PHASES_DUST) && M.hasDust && M.dustEmission) {
+            if (world > 1 && !reduce) throw std::runtime_error("sharded dust phases need a reducer");
             std::vector<PlanckTable> tables = planckTables(M);
             std::vector<double> lum;
             CellSources src;
@@ -964,6 +996,7 @@ OracleRun* oracle_run(const char* ski, const char* datadir, int rngKind, int nth
                     ph.labs = &run->tal.labsDust;
                     ph.store = true;
                     runPhase(ph, 0, ph.Npp * (uint64_t)Nl);
+                    sum(ORACLE_TALLY_DUST_LABS, run->tal.labsDust);  // Labsdusttot sums over processes
                     run->labsDustTotals.push_back(tableTotal(run->tal.labsDust));
                     sched.finishCycle(run->labsDustTotals.back());
                 }

@@ -23,6 +23,7 @@
 #ifndef SKIRT_ORACLE_H
 #define SKIRT_ORACLE_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -51,6 +52,17 @@ typedef struct OracleRun OracleRun;
 OracleRun* oracle_run(const char* ski, const char* datadir, int rng, int nthreads, double packages,
                       uint64_t seed, uint64_t packet_begin, uint64_t packet_end, int phases,
                       const char* outprefix);
+/* The same on rank `rank` of `world` processes (Philox mode only): every phase shoots the rank's slice
+ * [npp*rank/world, npp*(rank+1)/world) of every wavelength, the reference's IdenticalAssigner
+ * (IdenticalAssigner.cpp:37-58), like skirt_mcrt_run_phase_shard. reduce(user, tally, data, n) must sum a
+ * host array over the processes in place: the stellar Labs after the stellar phase, the dust Labs after
+ * every self-absorption cycle (ORACLE_TALLY_*); it may be NULL when only the stellar phase runs. The caller
+ * sums the instrument tallies at the end. */
+enum { ORACLE_TALLY_LABS = 0, ORACLE_TALLY_DUST_LABS = 1 };
+typedef int (*OracleReduceFn)(void* user, int tally, double* data, size_t n);
+OracleRun* oracle_run_shard(const char* ski, const char* datadir, int rng, int nthreads, double packages,
+                            uint64_t seed, uint64_t packet_begin, uint64_t packet_end, int phases,
+                            const char* outprefix, int rank, int world, OracleReduceFn reduce, void* user);
 const char* oracle_last_error(void);
 
 /* stellar Labs(m, ell) row-major, Ncells x Nlambda (PanDustSystem::_Labsstelvv) */

@@ -62,12 +62,17 @@ ABI_SYMBOLS = [
     "skirt_mcrt_upload_emissivity", "skirt_mcrt_compute_cell_sources", "skirt_mcrt_dust_labs_total",
     "skirt_sim_load", "skirt_sim_info", "skirt_sim_attach", "skirt_sim_engine", "skirt_sim_run_stellar",
     "skirt_sim_fetch", "skirt_sim_labs", "skirt_sim_instrument", "skirt_sim_set_tallies", "skirt_sim_write",
-    "skirt_sim_error", "skirt_sim_free", "skirt_sim_run_dust", "skirt_sim_run_dust_sharded", "skirt_sim_labs_dust", "skirt_sim_selfabs_totals",
+    "skirt_sim_error", "skirt_sim_free", "skirt_sim_run_dust", "skirt_sim_labs_dust", "skirt_sim_selfabs_totals",
+    "skirt_mcrt_run_phase_shard", "skirt_mcrt_shard_slice", "skirt_mcrt_set_reducer", "skirt_mcrt_reduce_instruments",
+    "skirt_sim_run_stellar_shard", "skirt_sim_run_dust_shard",
 ]
 
 _lib = None
-# int (*)(void* user, int what): the reduction callback of skirt_sim_run_dust_sharded
-REDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int)
+# SKIRT_TALLY_*: what the engine's reducer is asked to sum
+TALLY_LABS, TALLY_DUST_LABS, TALLY_INSTRUMENTS = 0, 1, 2
+# int (*)(void* user, int tally, double* d_buf, size_t n, void* hip_stream): skirt_mcrt_set_reducer's callback
+REDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t,
+                             ctypes.c_void_p)
 
 
 def lib():
@@ -88,7 +93,12 @@ def lib():
         L.skirt_sim_run_stellar.argtypes = [vp, c_u64, c_u64]
         L.skirt_sim_fetch.argtypes = [vp]
         L.skirt_sim_run_dust.argtypes = [vp]
-        L.skirt_sim_run_dust_sharded.argtypes = [vp, c_int, c_int, REDUCE_FN, vp]
+        L.skirt_sim_run_stellar_shard.argtypes = [vp, c_int, c_int]
+        L.skirt_sim_run_dust_shard.argtypes = [vp, c_int, c_int]
+        L.skirt_mcrt_set_reducer.argtypes = [vp, REDUCE_FN, vp]
+        L.skirt_mcrt_reduce_instruments.argtypes = [vp]
+        L.skirt_mcrt_shard_slice.restype = None
+        L.skirt_mcrt_shard_slice.argtypes = [c_u64, c_int, c_int, ctypes.POINTER(c_u64), ctypes.POINTER(c_u64)]
         L.skirt_mcrt_bind_dust_labs.argtypes = [vp, vp]
         L.skirt_sim_labs_dust.restype = ctypes.POINTER(c_dbl)
         L.skirt_sim_labs_dust.argtypes = [vp]
@@ -166,23 +176,40 @@ class Simulation:
     def run_stellar(self, first=0, count=0):
         self._check(lib().skirt_sim_run_stellar(self._h, first, count))
 
-    def run_dust(self, rank=0, world=1, reduce_dust_labs=None):
+    def run_stellar_shard(self, rank, world):
+        """This rank's slice of every wavelength of the stellar phase (IdenticalAssigner); with world > 1
+        the reducer (set_reducer) sums the stellar Labs at the phase end."""
+        self._check(lib().skirt_sim_run_stellar_shard(self._h, rank, world))
+
+    def run_dust(self, rank=0, world=1):
         """Self-absorption cycles (if enabled) and the dust emission phase (PanMonteCarloSimulation::runSelf).
-        With world > 1 this rank shoots its slice of every phase and reduce_dust_labs() must sum the
-        bound dust Labs tensor over the ranks (it is called after every self-absorption cycle)."""
-        if world == 1:
-            self._check(lib().skirt_sim_run_dust(self._h))
+        With world > 1 this rank shoots its slice of every wavelength of every phase, and the reducer
+        (set_reducer) sums the dust Labs after every self-absorption cycle."""
+        self._check(lib().skirt_sim_run_dust_shard(self._h, rank, world))
+
+    def set_reducer(self, fn):
+        """fn(tally, device_ptr, n, hip_stream) sums the engine's device buffer over all processes in place
+        (skirt_mcrt_set_reducer); e.g. skirt_amd.sharding.TallyReducer over the bound tally tensors.
+        None removes it."""
+        if fn is None:
+            self._reducer = None
+            self._check_engine(lib().skirt_mcrt_set_reducer(self.engine, ctypes.cast(None, REDUCE_FN), None))
             return
 
-        def cb(_user, _what):
+        def cb(_user, tally, ptr, n, stream):
             try:
-                reduce_dust_labs()
+                fn(tally, ptr, n, stream)
                 return 0
-            except Exception:  # noqa: BLE001 -- reported to the C side as a failed reduction
+            except Exception as e:  # noqa: BLE001 -- reported to the C side as a failed reduction
+                self.reducer_error = e
                 return 1
 
-        fn = REDUCE_FN(cb)
-        self._check(lib().skirt_sim_run_dust_sharded(self._h, rank, world, fn, None))
+        self._reducer = REDUCE_FN(cb)  # kept alive as long as the engine may call it
+        self._check_engine(lib().skirt_mcrt_set_reducer(self.engine, self._reducer, None))
+
+    def reduce_instruments(self):
+        """Instrument::sumResults: sums the instrument tallies over the processes (once per simulation)."""
+        self._check_engine(lib().skirt_mcrt_reduce_instruments(self.engine))
 
     def bind_dust_labs(self, ptr):
         """Make the engine accumulate the dust Labs in caller device memory (tally_sizes()[0] doubles)."""

@@ -204,6 +204,9 @@ struct Args {
     int nsed;
     // phase
     unsigned long long npp, first, end, seed;
+    // the per-wavelength slice [sliceLo, sliceLo + sliceCnt) of a sharded phase (sliceCnt == npp: the
+    // whole phase); first/end index the slice's packets, wavelength-slowest (see globalPacket)
+    unsigned long long sliceLo, sliceCnt;
     unsigned int tag;
     double minWeightReduction;
     int minScatt;
@@ -2019,6 +2022,16 @@ __device__ __forceinline__ void blockReserve3(unsigned* ctr0, unsigned c0, unsig
     __syncthreads();  // the scratch words are reused by the next call
 }
 
+// Global packet index of the j-th packet of this call. A sharded call (IdenticalAssigner,
+// IdenticalAssigner.cpp:37-58: every process runs its block of chunks at every wavelength) shoots
+// packets [sliceLo, sliceLo + sliceCnt) of each wavelength; the Philox stream is keyed on the global
+// index, so the packets are the same whatever the number of ranks.
+__device__ __forceinline__ unsigned long long globalPacket(const Args& a, unsigned long long j) {
+    if (a.sliceCnt == a.npp) return j;
+    const unsigned long long ell = j / a.sliceCnt;
+    return ell * a.npp + a.sliceLo + (j - ell * a.sliceCnt);
+}
+
 template <int GRID, bool ONECOMP>
 __global__ void __launch_bounds__(kBlock) SKIRT_EVENT_ATTR eventKernel(const Args a) {
     __shared__ unsigned long long resv[3 * (kBlock / 64) + 3];
@@ -2090,7 +2103,7 @@ __global__ void __launch_bounds__(kBlock) SKIRT_EVENT_ATTR eventKernel(const Arg
             blockReserve<unsigned long long, unsigned int>(a.claim, need ? 1ull : 0ull, idx, nullptr, 0u, unused, resv);
             if (need) {
                 if (idx >= total) need = false;  // exhausted: the slot retires
-                else if (E.launch(p, a.first + idx)) {
+                else if (E.launch(p, globalPacket(a, a.first + idx))) {
                     if (!(p.L > 0)) {
                         // a zero-weight dust packet (a cell without emission drawn uniformly): every
                         // tally it would touch receives 0, so it ends here
@@ -2263,6 +2276,10 @@ struct SkirtMcrt {
     uint64_t traceLaunchesTotal = 0;
     int numCUs = 0;
     int lastIterations = 0;
+    // multi-process reduction of the tallies (skirt_mcrt_set_reducer)
+    SkirtReduceTallyFn reduce = nullptr;
+    void* reduceUser = nullptr;
+    bool instrReduced = false;
 };
 
 namespace {
@@ -2840,6 +2857,7 @@ int skirt_mcrt_zero_tallies(SkirtMcrt* c) {
     if (c->dTally && c->nInstrTally) HIPCHECK(c, hipMemsetAsync(c->dTally, 0, c->nInstrTally * sizeof(double), c->stream));
     HIPCHECK(c, hipMemsetAsync(c->dStats, 0, 8 * kStatCopies * sizeof(unsigned long long), c->stream));
     HIPCHECK(c, hipMemsetAsync(c->dError, 0, sizeof(unsigned int), c->stream));
+    c->instrReduced = false;
     return SKIRT_OK;
 }
 
@@ -2996,9 +3014,79 @@ int skirt_mcrt_download_dust_labs(SkirtMcrt* c, double* labs) {
     return SKIRT_OK;
 }
 
+static const char* const kSummedTwice =
+    "the instrument tallies were already summed over the processes: zero the tallies before another phase";
+static int runPhase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, uint64_t first, uint64_t count,
+                    uint64_t sliceLo, uint64_t sliceCnt, uint64_t seed, const SkirtPhaseParams* p);
+static int phaseEndReduce(SkirtMcrt* c, int phase, const SkirtPhaseParams* p);
+
 int skirt_mcrt_run_phase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, uint64_t first, uint64_t count,
                          uint64_t seed, const SkirtPhaseParams* p) {
     if (!c || !p) return SKIRT_ERR_ARG;
+    if (npp == 0) return fail(c, SKIRT_ERR_ARG, "npp must be positive");
+    if (first + count > npp * (uint64_t)c->nlambda) return fail(c, SKIRT_ERR_ARG, "packet range exceeds npp*nlambda");
+    if (c->instrReduced) return fail(c, SKIRT_ERR_STATE, kSummedTwice);
+    int rc = runPhase(c, phase, cycle, npp, first, count, 0, npp, seed, p);
+    return rc ? rc : phaseEndReduce(c, phase, p);
+}
+
+int skirt_mcrt_run_phase_shard(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, int rank, int world,
+                               uint64_t seed, const SkirtPhaseParams* p) {
+    if (!c || !p) return SKIRT_ERR_ARG;
+    if (npp == 0) return fail(c, SKIRT_ERR_ARG, "npp must be positive");
+    if (world < 1 || rank < 0 || rank >= world) return fail(c, SKIRT_ERR_ARG, "bad shard (rank, world)");
+    if (world > 1 && !c->reduce) return fail(c, SKIRT_ERR_STATE, "a sharded phase needs a reducer (skirt_mcrt_set_reducer)");
+    if (c->instrReduced) return fail(c, SKIRT_ERR_STATE, kSummedTwice);
+    // SequentialAssigner over the packets of one wavelength (SequentialAssigner.cpp:37-59), the same
+    // block at every wavelength (IdenticalAssigner.cpp:37-58)
+    uint64_t lo = 0, cnt = 0;
+    skirt_mcrt_shard_slice(npp, rank, world, &lo, &cnt);
+    int rc = runPhase(c, phase, cycle, npp, 0, cnt * (uint64_t)c->nlambda, lo, cnt, seed, p);
+    return rc ? rc : phaseEndReduce(c, phase, p);
+}
+
+void skirt_mcrt_shard_slice(uint64_t npp, int rank, int world, uint64_t* lo, uint64_t* count) {
+    const unsigned __int128 n = npp;
+    const uint64_t a = (uint64_t)(n * (unsigned)rank / (unsigned)world);
+    const uint64_t b = (uint64_t)(n * (unsigned)(rank + 1) / (unsigned)world);
+    if (lo) *lo = a;
+    if (count) *count = b - a;
+}
+
+int skirt_mcrt_set_reducer(SkirtMcrt* c, SkirtReduceTallyFn fn, void* user) {
+    if (!c) return SKIRT_ERR_ARG;
+    c->reduce = fn;
+    c->reduceUser = user;
+    return SKIRT_OK;
+}
+
+int skirt_mcrt_reduce_instruments(SkirtMcrt* c) {
+    if (!c) return SKIRT_ERR_ARG;
+    if (!c->reduce || c->instrReduced || !c->dTally || !c->nInstrTally) return SKIRT_OK;
+    HIPCHECK(c, hipSetDevice(c->device));
+    c->instrReduced = true;
+    if (c->reduce(c->reduceUser, SKIRT_TALLY_INSTRUMENTS, c->dTally, c->nInstrTally, (void*)c->stream))
+        return fail(c, SKIRT_ERR_STATE, "the instrument reduction failed");
+    return SKIRT_OK;
+}
+
+// PanDustSystem::sumResults at the end of a phase (PanDustSystem.cpp:394-403): the stellar Labs after the
+// stellar phase, the dust Labs after a self-absorption cycle, summed over the processes by the caller's
+// reducer, enqueued behind the phase on the engine stream. Instrument::sumResults (Instrument.cpp:57)
+// comes once, before the tallies are read (skirt_mcrt_reduce_instruments / download).
+static int phaseEndReduce(SkirtMcrt* c, int phase, const SkirtPhaseParams* p) {
+    if (!c->reduce) return SKIRT_OK;
+    const size_t n = (size_t)c->labsStride * c->nlambda;
+    int r = 0;
+    if (phase == SKIRT_PHASE_STELLAR && p->store_absorption && c->dLabs && n)
+        r = c->reduce(c->reduceUser, SKIRT_TALLY_LABS, c->dLabs, n, (void*)c->stream);
+    else if (phase == SKIRT_PHASE_DUST_SELFABS && c->dLabsDust && n)
+        r = c->reduce(c->reduceUser, SKIRT_TALLY_DUST_LABS, c->dLabsDust, n, (void*)c->stream);
+    return r ? fail(c, SKIRT_ERR_STATE, "the absorption reduction failed") : SKIRT_OK;
+}
+
+static int runPhase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, uint64_t first, uint64_t count,
+                    uint64_t sliceLo, uint64_t sliceCnt, uint64_t seed, const SkirtPhaseParams* p) {
     if (phase < SKIRT_PHASE_STELLAR || phase > SKIRT_PHASE_DUST_SELFABS) return fail(c, SKIRT_ERR_ARG, "unknown phase");
     if (cycle >= (1u << 30)) return fail(c, SKIRT_ERR_ARG, "cycle number too large");
     const bool cellPhase = phase != SKIRT_PHASE_STELLAR;
@@ -3066,6 +3154,7 @@ int skirt_mcrt_run_phase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, 
     a.lumtot = c->dLumtot; a.cdf = c->dCdf; a.emissionBias = c->emissionBias;
     a.ninstr = (int)c->instr.size(); a.instr = c->dInstr; a.nsed = c->nsed;
     a.npp = npp; a.first = first; a.end = first + count; a.seed = seed;
+    a.sliceLo = sliceLo; a.sliceCnt = sliceCnt;
     a.tag = (unsigned)phase | (cycle << 2);  // Philox counter word 1: streams differ per phase and cycle
     a.phase = phase;
     a.peel = phase != SKIRT_PHASE_DUST_SELFABS;
@@ -3257,7 +3346,9 @@ int skirt_mcrt_synchronize(SkirtMcrt* c) {
 
 int skirt_mcrt_download(SkirtMcrt* c, double* labs, double* instr) {
     if (!c) return SKIRT_ERR_ARG;
-    int rc = skirt_mcrt_synchronize(c);
+    int rc = instr ? skirt_mcrt_reduce_instruments(c) : SKIRT_OK;
+    if (rc) return rc;
+    rc = skirt_mcrt_synchronize(c);
     if (rc) return rc;
     const size_t nl = (size_t)c->labsStride * c->nlambda;
     if (labs && nl) {

@@ -221,19 +221,21 @@ int skirt_sim_run_stellar(SkirtSim* s, uint64_t first, uint64_t count) {
     return check(s, skirt_mcrt_run_stellar(s->eng, s->npp, first, count, s->m.seed, &p));
 }
 
-int skirt_sim_run_dust(SkirtSim* s) { return skirt_sim_run_dust_sharded(s, 0, 1, nullptr, nullptr); }
-
-int skirt_sim_run_dust_sharded(SkirtSim* s, int rank, int world, SkirtReduceFn reduce, void* user) {
+int skirt_sim_run_stellar_shard(SkirtSim* s, int rank, int world) {
     if (!s || !s->eng) { g_err = "no engine attached"; return SKIRT_ERR_STATE; }
-    if (world < 1 || rank < 0 || rank >= world || (world > 1 && !reduce)) {
-        g_err = "bad shard (rank, world) or missing reduction";
+    SkirtPhaseParams p{s->m.minWeightReduction, s->m.minScattEvents, s->m.scattBias,
+                       s->m.hasDust && s->m.storeAbsorption ? 1 : 0, s->m.hasDust ? 1 : 0};
+    return check(s, skirt_mcrt_run_phase_shard(s->eng, SKIRT_PHASE_STELLAR, 0, s->npp, rank, world, s->m.seed, &p));
+}
+
+int skirt_sim_run_dust(SkirtSim* s) { return skirt_sim_run_dust_shard(s, 0, 1); }
+
+int skirt_sim_run_dust_shard(SkirtSim* s, int rank, int world) {
+    if (!s || !s->eng) { g_err = "no engine attached"; return SKIRT_ERR_STATE; }
+    if (world < 1 || rank < 0 || rank >= world) {
+        g_err = "bad shard (rank, world)";
         return SKIRT_ERR_ARG;
     }
-    // this rank's contiguous slice of a phase's npp * Nlambda packets (skirt_amd.sharding.shard_range)
-    auto shard = [&](uint64_t total, uint64_t& first, uint64_t& count) {
-        first = total * (uint64_t)rank / (uint64_t)world;
-        count = total * (uint64_t)(rank + 1) / (uint64_t)world - first;
-    };
     const Model& m = s->m;
     if (!(m.hasDust && m.pan && m.dustEmission)) return SKIRT_OK;  // no dust emission: nothing to do
     try {
@@ -248,7 +250,8 @@ int skirt_sim_run_dust_sharded(SkirtSim* s, int rank, int world, SkirtReduceFn r
         std::vector<double> lum;
         CellSources src;
         if (hostSources) {
-            if ((rc = skirt_sim_fetch(s))) return rc;  // the stellar phase's Labs on the host
+            // the stellar phase's Labs on the host (already summed over the processes at its phase end)
+            if (!s->labs.empty() && (rc = check(s, skirt_mcrt_download(s->eng, s->labs.data(), nullptr)))) return rc;
         } else {
             std::vector<double> sigma, kabs, mu, planck;
             for (int h = 0; h < m.ncomp(); h++) {
@@ -274,8 +277,11 @@ int skirt_sim_run_dust_sharded(SkirtSim* s, int rank, int world, SkirtReduceFn r
         };
         s->dustTotals.clear();
         if (m.selfAbsorption) {
-            // PanMonteCarloSimulation::rundustselfabsorption (PanMonteCarloSimulation.cpp:109-181)
+            // PanMonteCarloSimulation::rundustselfabsorption (PanMonteCarloSimulation.cpp:109-181). The
+            // first cycle's spectra come from the stellar Labs alone: the dust Labs start at zero (also
+            // on the device, where an earlier run may have left its last cycle's tally)
             s->labsDust.assign((size_t)m.ncells() * Nl, 0.0);
+            if ((rc = check(s, skirt_mcrt_zero_dust_labs(s->eng)))) return rc;
             SelfAbsorptionSchedule sched;
             sched.fixedCycles = m.cycles;
             uint32_t cycle = 0;
@@ -283,16 +289,11 @@ int skirt_sim_run_dust_sharded(SkirtSim* s, int rank, int world, SkirtReduceFn r
                 if ((rc = prepare(true))) return rc;  // calculatedustemission, Labsbolv = Labs(m)
                 if ((rc = check(s, skirt_mcrt_zero_dust_labs(s->eng)))) return rc;  // rebootLabsdust
                 uint64_t npp = (uint64_t)std::ceil(m.packages * SelfAbsorptionSchedule::factor(sched.stage));
-                uint64_t first, count;
-                shard(npp * (uint64_t)Nl, first, count);
-                if ((rc = check(s, skirt_mcrt_run_phase(s->eng, SKIRT_PHASE_DUST_SELFABS, cycle++, npp, first,
-                                                        count, m.seed, &p))))
+                // this rank's slice of every wavelength; the engine's reducer sums the dust Labs over the
+                // processes at the phase end (PanDustSystem::Labsdusttot sums over processes)
+                if ((rc = check(s, skirt_mcrt_run_phase_shard(s->eng, SKIRT_PHASE_DUST_SELFABS, cycle++, npp, rank,
+                                                              world, m.seed, &p))))
                     return rc;
-                // PanDustSystem::Labsdusttot sums over processes: the caller all-reduces the dust Labs
-                if (world > 1 && (rc = reduce(user, SKIRT_REDUCE_DUST_LABS))) {
-                    g_err = "the dust Labs reduction failed";
-                    return rc;
-                }
                 double total = 0;
                 if (hostSources) {
                     if ((rc = check(s, skirt_mcrt_download_dust_labs(s->eng, s->labsDust.data())))) return rc;
@@ -308,9 +309,7 @@ int skirt_sim_run_dust_sharded(SkirtSim* s, int rank, int world, SkirtReduceFn r
         // PanMonteCarloSimulation::rundustemission (PanMonteCarloSimulation.cpp:245-264)
         if ((rc = prepare(m.selfAbsorption))) return rc;
         uint64_t npp = (uint64_t)std::ceil(m.packages * m.emissionBoost);
-        uint64_t first, count;
-        shard(npp * (uint64_t)Nl, first, count);
-        return check(s, skirt_mcrt_run_phase(s->eng, SKIRT_PHASE_DUST_EMISSION, 0, npp, first, count, m.seed, &p));
+        return check(s, skirt_mcrt_run_phase_shard(s->eng, SKIRT_PHASE_DUST_EMISSION, 0, npp, rank, world, m.seed, &p));
     } catch (std::exception& e) {
         g_err = e.what();
         return SKIRT_ERR_ARG;

@@ -15,6 +15,11 @@ RNG_MT = 0
 RNG_PHILOX = 1
 PHASES_STELLAR, PHASES_DUST, PHASES_ALL = 1, 2, 3  # oracle_run's phase mask (oracle.h)
 
+TALLY_LABS, TALLY_DUST_LABS = 0, 1  # ORACLE_TALLY_* (oracle.h)
+# int (*)(void* user, int tally, double* data, size_t n): oracle_run_shard's host-array reduction
+REDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_double),
+                             ctypes.c_size_t)
+
 _lib = None
 
 
@@ -27,6 +32,8 @@ def lib():
         L.oracle_run.restype = ctypes.c_void_p
         L.oracle_run.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_double,
                                  ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int, ctypes.c_char_p]
+        L.oracle_run_shard.restype = ctypes.c_void_p
+        L.oracle_run_shard.argtypes = L.oracle_run.argtypes + [ctypes.c_int, ctypes.c_int, REDUCE_FN, ctypes.c_void_p]
         L.oracle_last_error.restype = ctypes.c_char_p
         L.oracle_labs.restype = ctypes.POINTER(ctypes.c_double)
         L.oracle_labs.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]
@@ -81,12 +88,28 @@ class OracleResult:
 
 
 def run(ski, rng=RNG_MT, threads=1, packages=0.0, seed=0, packet_begin=0, packet_end=0, outprefix=None,
-        phases=PHASES_STELLAR):
+        phases=PHASES_STELLAR, rank=0, world=1, reduce=None):
     """Runs the oracle; by default only the stellar emission phase (phases=PHASES_ALL adds the dust
-    self-absorption and dust emission phases of a Pan simulation with dust emission)."""
+    self-absorption and dust emission phases of a Pan simulation with dust emission).
+
+    With world > 1 (Philox mode) this is rank `rank`'s shard: its slice of every wavelength of every
+    phase; reduce(tally, array) must sum the numpy array over the ranks in place (called for the stellar
+    Labs and after every self-absorption cycle for the dust Labs)."""
     L = lib()
-    h = L.oracle_run(ski.encode(), DATA_DIR.encode(), rng, threads, float(packages), seed, packet_begin,
-                     packet_end, phases, outprefix.encode() if outprefix else None)
+    args = [ski.encode(), DATA_DIR.encode(), rng, threads, float(packages), seed, packet_begin, packet_end, phases,
+            outprefix.encode() if outprefix else None]
+    if world == 1:
+        h = L.oracle_run(*args)
+    else:
+        def cb(_user, tally, data, n):
+            try:
+                reduce(tally, np.ctypeslib.as_array(data, shape=(n,)))
+                return 0
+            except Exception:  # noqa: BLE001 -- reported to the C side as a failed reduction
+                return 1
+
+        fn = REDUCE_FN(cb) if reduce else ctypes.cast(None, REDUCE_FN)
+        h = L.oracle_run_shard(*args, rank, world, fn, None)
     if not h:
         raise RuntimeError("oracle failed: " + L.oracle_last_error().decode())
     try:

@@ -1,8 +1,11 @@
-"""The multi-GPU path's sharding and reduction, exercised with torch.distributed over gloo on the CPU
-(world size 2): each rank shoots its shard_range slice of the packet index space (with the oracle in
-Philox mode standing in for the engine, since the packet streams are identical), the tallies are
-all-reduced with allreduce_tallies exactly as bench.py does on the GPUs, and the result equals one
-unsharded run."""
+"""The multi-GPU path's sharding and reductions, exercised with torch.distributed over gloo on the CPU.
+
+Each rank shoots its slice of every wavelength of every phase (the reference's IdenticalAssigner,
+IdenticalAssigner.cpp:37-58; skirt_mcrt_run_phase_shard on the GPUs), with the oracle in Philox mode
+standing in for the engine, since the packet streams are identical. The oracle calls its reducer where
+the engine calls its own (the stellar Labs after the stellar phase, the dust Labs after every
+self-absorption cycle); the reducer sums with torch.distributed exactly as TallyReducer does on the GPUs.
+"""
 import os
 import socket
 
@@ -13,10 +16,12 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 import oracle_lib as O
-from skirt_amd.sharding import allreduce_tallies, shard_range
+from skirt_amd.sharding import allreduce_tallies, shard_packets, shard_slice
 
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
-SKI = os.path.join(GOLD, "ski", "pan_cart16.ski")
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SKI_SA = os.path.join(GOLD, "ski", "pan_cart16_sa.ski")
+SKI_C3 = os.path.join(REPO, "benchmarks", "c3_oct128.ski")
 PACKAGES = 300
 
 
@@ -32,44 +37,100 @@ def _tallies(res):
     return np.concatenate(parts)
 
 
-def _worker(rank, world, port, outdir):
+def _init(rank, world, port):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
+
+
+def _sum(_tally, arr):
+    t = torch.from_numpy(arr)  # shares the oracle's host array: summed in place
+    dist.all_reduce(t)
+
+
+def _worker_all_phases(rank, world, port, outdir):
+    _init(rank, world, port)
     try:
-        total = O.run(SKI, rng=O.RNG_PHILOX, packages=PACKAGES, packet_begin=0, packet_end=1).nlambda * PACKAGES
-        first, count = shard_range(total, rank, world)
-        res = O.run(SKI, rng=O.RNG_PHILOX, threads=2, packages=PACKAGES, packet_begin=first,
-                    packet_end=first + count)
-        t = torch.from_numpy(_tallies(res))
+        res = O.run(SKI_SA, rng=O.RNG_PHILOX, threads=2, packages=PACKAGES, phases=O.PHASES_ALL, rank=rank,
+                    world=world, reduce=_sum)
+        t = torch.from_numpy(np.concatenate([f.ravel() for f in res.frames] + [s.ravel() for s in res.seds]))
         n = torch.tensor([float(res.packets)], dtype=torch.float64)
-        allreduce_tallies(t, n)
+        allreduce_tallies(t, n)  # Instrument::sumResults, once at the end
         if rank == 0:
-            np.save(os.path.join(outdir, "reduced.npy"), t.numpy())
+            np.save(os.path.join(outdir, "instr.npy"), t.numpy())
             np.save(os.path.join(outdir, "packets.npy"), n.numpy())
+            np.save(os.path.join(outdir, "labs.npy"), res.labs)
+            np.save(os.path.join(outdir, "dust.npy"), res.labs_dust)
+            np.save(os.path.join(outdir, "totals.npy"), np.array(res.labs_dust_totals))
     finally:
         dist.destroy_process_group()
 
 
-def test_shard_range_partitions_exactly():
-    for total in (0, 1, 7, 1000, 10 ** 9 + 7):
+def _worker_balance(rank, world, port, outdir, packages):
+    _init(rank, world, port)
+    try:
+        res = O.run(SKI_C3, rng=O.RNG_PHILOX, threads=1, packages=packages, rank=rank, world=world)
+        seg = torch.tensor([float(res.segments), float(res.packets)], dtype=torch.float64)
+        out = [torch.zeros(2, dtype=torch.float64) for _ in range(world)]
+        dist.all_gather(out, seg)
+        if rank == 0:
+            np.save(os.path.join(outdir, "work.npy"), torch.stack(out).numpy())
+    finally:
+        dist.destroy_process_group()
+
+
+def test_shard_slices_cover_every_wavelength_exactly():
+    for npp in (1, 7, 1000, 10 ** 9 + 7):
         for world in (1, 2, 3, 8):
-            spans = [shard_range(total, r, world) for r in range(world)]
+            spans = [shard_slice(npp, r, world) for r in range(world)]
             assert spans[0][0] == 0
-            assert sum(c for _, c in spans) == total
+            assert sum(c for _, c in spans) == npp
             for (f0, c0), (f1, _) in zip(spans, spans[1:]):
                 assert f0 + c0 == f1
             assert max(c for _, c in spans) - min(c for _, c in spans) <= 1
+    # the union of the ranks' global packets is the phase, each once, and every rank has every wavelength
+    npp, nl, world = 11, 5, 3
+    got = sorted(p for r in range(world) for p in shard_packets(npp, nl, r, world))
+    assert got == list(range(npp * nl))
+    for r in range(world):
+        assert sorted({p // npp for p in shard_packets(npp, nl, r, world)}) == list(range(nl))
     with pytest.raises(ValueError):
-        shard_range(10, 2, 2)
+        shard_slice(10, 2, 2)
 
 
-def test_two_rank_gloo_sharding_equals_single_run(tmp_path):
-    mp.spawn(_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
-    reduced = np.load(os.path.join(tmp_path, "reduced.npy"))
-    packets = np.load(os.path.join(tmp_path, "packets.npy"))[0]
-    full = O.run(SKI, rng=O.RNG_PHILOX, threads=2, packages=PACKAGES)
-    assert packets == full.packets
-    ref = _tallies(full)
-    np.testing.assert_allclose(reduced, ref, rtol=1e-12, atol=1e-300)
-    assert ref.sum() > 0
+def test_shard_slice_matches_the_engine_abi():
+    import skirt_amd as S
+    import ctypes
+
+    lo, n = ctypes.c_uint64(), ctypes.c_uint64()
+    for npp, r, w in ((1000, 0, 8), (1000, 7, 8), (10 ** 12 + 3, 5, 7), (3, 2, 8)):
+        S.lib().skirt_mcrt_shard_slice(npp, r, w, ctypes.byref(lo), ctypes.byref(n))
+        assert (lo.value, n.value) == shard_slice(npp, r, w)
+
+
+def test_two_rank_gloo_shards_with_self_absorption_equal_single_run(tmp_path):
+    """Stellar phase, self-absorption cycles (convergence-driven schedule, the dust Labs summed after each)
+    and dust emission, over 2 ranks: the summed tallies and the per-cycle totals equal one run."""
+    mp.spawn(_worker_all_phases, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    load = lambda n: np.load(os.path.join(tmp_path, n + ".npy"))  # noqa: E731
+    full = O.run(SKI_SA, rng=O.RNG_PHILOX, threads=2, packages=PACKAGES, phases=O.PHASES_ALL)
+    assert load("packets")[0] == full.packets
+    np.testing.assert_allclose(load("totals"), full.labs_dust_totals, rtol=1e-12)
+    np.testing.assert_allclose(load("labs"), full.labs, rtol=1e-12, atol=1e-300)
+    np.testing.assert_allclose(load("dust"), full.labs_dust, rtol=1e-12, atol=1e-300)
+    ref = np.concatenate([f.ravel() for f in full.frames] + [s.ravel() for s in full.seds])
+    np.testing.assert_allclose(load("instr"), ref, rtol=1e-12, atol=1e-300)
+    assert len(full.labs_dust_totals) > 1 and ref.sum() > 0
+
+
+def test_eight_rank_gloo_shards_balance_the_c3_work(tmp_path):
+    """C3 (the 128^3 octree, 25 wavelengths, 5 of them without stellar luminosity) over 8 ranks: every
+    rank shoots every wavelength, so the ranks' grid segments (the trace kernel's work) agree to within
+    5 % of the mean. The contiguous split of the wavelength-slowest packet space used before gave a
+    max/mean of 2.16, one rank holding only wavelengths without luminosity."""
+    packages = 1600
+    mp.spawn(_worker_balance, args=(8, _free_port(), str(tmp_path), packages), nprocs=8, join=True)
+    work = np.load(os.path.join(tmp_path, "work.npy"))
+    segs, pkts = work[:, 0], work[:, 1]
+    assert np.all(pkts == pkts[0]) and pkts[0] > 0
+    assert segs.max() / segs.mean() <= 1.05, segs

@@ -17,6 +17,7 @@ import pytest
 import oracle_lib as O
 import skirt_files as F
 import skirt_amd as S
+from skirt_amd.sharding import shard_slice
 
 pytestmark = pytest.mark.gpu
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
@@ -150,6 +151,32 @@ def test_sharded_packet_ranges_sum_to_the_whole():
     ff, sf = full.instrument(0)
     np.testing.assert_allclose(sa + sb, sf, rtol=1e-12)
     np.testing.assert_allclose(fa + fb, ff, rtol=1e-12, atol=1e-300)
+
+
+def test_wavelength_shards_sum_to_the_whole():
+    """Three ranks' slices of every wavelength (skirt_mcrt_run_phase_shard, the reference's
+    IdenticalAssigner) add up to the full run exactly, and each rank shoots every wavelength."""
+    name = "pan_cart16"
+    full = run_gpu(name, packages=2000)
+    parts = []
+    for r in range(3):
+        sim = S.Simulation(ski(name), packages=2000)
+        sim.attach(0)
+        calls = []
+        sim.set_reducer(lambda tally, ptr, n, stream: calls.append(tally))  # single process: no sum
+        sim.run_stellar_shard(r, 3)
+        sim.fetch()
+        assert calls == [S.TALLY_LABS, S.TALLY_INSTRUMENTS]
+        lo, n = shard_slice(2000, r, 3)
+        assert sim.stats()["packets"] == n * np.count_nonzero(full.labs().sum(axis=0) > 0)
+        assert np.all(sim.labs().sum(axis=0)[full.labs().sum(axis=0) > 0] > 0)
+        parts.append(sim)
+    np.testing.assert_allclose(sum(p.labs() for p in parts), full.labs(), rtol=1e-12, atol=1e-300)
+    ff, sf = full.instrument(0)
+    np.testing.assert_allclose(sum(p.instrument(0)[1] for p in parts), sf, rtol=1e-12)
+    np.testing.assert_allclose(sum(p.instrument(0)[0] for p in parts), ff, rtol=1e-12, atol=1e-300)
+    with pytest.raises(S.SkirtError, match="summed"):
+        parts[0].run_stellar_shard(0, 3)  # the instruments were summed: a further phase is refused
 
 
 def _isrf_sums(path):

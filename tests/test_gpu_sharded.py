@@ -1,7 +1,8 @@
-"""Multi-rank photon phases on the GPU: two processes share the box's GPU, each shooting its
-shard_range slice of every phase (stellar emission, self-absorption cycles, dust emission), with the
-tallies summed between phases exactly where the multi-GPU run sums them (bench.py uses RCCL; here gloo
-on host copies, since both ranks sit on one device). The result must equal one unsharded run."""
+"""Multi-rank photon phases on the GPU: two processes share the box's GPU, each shooting its slice of
+every wavelength of every phase (stellar emission, self-absorption cycles, dust emission;
+skirt_mcrt_run_phase_shard), with the engine's reducer summing the tallies where the reference sums them
+(bench.py reduces over RCCL; here gloo on host copies, since both ranks sit on one device). The result
+must equal one unsharded run."""
 import os
 import socket
 
@@ -12,7 +13,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 import skirt_amd as S
-from skirt_amd.sharding import shard_range
+from skirt_amd.sharding import TallyReducer
 
 pytestmark = pytest.mark.gpu
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
@@ -24,12 +25,6 @@ def _free_port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         return s.getsockname()[1]
-
-
-def _host_allreduce(t):
-    c = t.cpu()
-    dist.all_reduce(c)
-    t.copy_(c)
 
 
 def _worker(rank, world, port, outdir):
@@ -48,15 +43,15 @@ def _worker(rank, world, port, outdir):
         dust = torch.zeros(n_labs, dtype=torch.float64, device="cuda")
         sim.bind_tallies(labs.data_ptr(), instr.data_ptr())
         sim.bind_dust_labs(dust.data_ptr())
+        red = TallyReducer(labs, instr, dust, via_host=True)
+        sim.set_reducer(red)
         sim.zero_tallies()
-        first, count = shard_range(sim.info.total_packets, rank, world)
-        sim.run_stellar(first, count)
-        sim.synchronize()
-        _host_allreduce(labs)  # PanDustSystem::sumResults before the dust phases
-        sim.run_dust(rank, world, lambda: (torch.cuda.synchronize(), _host_allreduce(dust)))
-        sim.synchronize()
-        _host_allreduce(instr)
-        sim.fetch()
+        sim.run_stellar_shard(rank, world)  # + Labs summed at the phase end
+        sim.run_dust(rank, world)           # + dust Labs summed after every cycle
+        sim.fetch()                         # + instruments summed once
+        tallies = [c[0] for c in red.calls]
+        assert tallies[0] == S.TALLY_LABS and tallies[-1] == S.TALLY_INSTRUMENTS, tallies
+        assert tallies.count(S.TALLY_DUST_LABS) == len(sim.selfabs_totals()) > 0, tallies
         if rank == 0:
             np.save(os.path.join(outdir, "labs.npy"), sim.labs())
             np.save(os.path.join(outdir, "dust.npy"), sim.labs_dust())
