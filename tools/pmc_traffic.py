@@ -5,9 +5,11 @@
   profiles/pmc_<cfg>.json                           HBM bytes per traceKernel launch (read by bench.py)
 
 HBM bytes follow MI355X_MICROARCH.md (HBM section): FETCH_SIZE and WRITE_SIZE come from separate passes
-(they cannot share one on gfx950), in KiB; FETCH_SIZE reads half the bytes of 16-byte-per-lane
-global loads on gfx950 (the trace kernel's leaf-map and ray-record loads are all of that width), so it
-is doubled; WRITE_SIZE is exact for 16-byte stores and for the f64 atomics.
+(they cannot share one on gfx950), in KiB; WRITE_SIZE is exact for 16-byte stores and for the f64
+atomics. The guide's halving of FETCH_SIZE holds for coalesced 16-byte-per-lane streams only; a
+scattered gather (one lane per 64-byte line, the trace kernel's leaf-map, Labs and neighbour loads)
+reports its whole 64-byte line (tools/gather_bench.hip, profiles/r02_gather_calibration.txt), so
+FETCH_SIZE is taken as it is: traffic = FETCH_SIZE + WRITE_SIZE.
 usage: python tools/pmc_traffic.py <cfg> <round>
 """
 import collections
@@ -77,8 +79,8 @@ def main():
     w = avg.get(("traceKernel", "WRITE_SIZE"))
     if f is not None and w is not None:
         d = {"kernel": "traceKernel", "fetch_size_kib": f, "write_size_kib": w,
-             "traffic_bytes_per_launch": 2 * f * 1024 + w * 1024,
-             "source": "profiles/%s_rocprof_%s.txt: 2 x FETCH_SIZE + WRITE_SIZE per traceKernel dispatch" % (rnd, cfg)}
+             "traffic_bytes_per_launch": f * 1024 + w * 1024,
+             "source": "profiles/%s_rocprof_%s.txt: FETCH_SIZE + WRITE_SIZE per traceKernel dispatch" % (rnd, cfg)}
         json.dump(d, open(os.path.join(prof, "pmc_%s.json" % cfg), "w"), indent=1)
         print(json.dumps(d))
     print("\n".join(lines))
