@@ -40,6 +40,10 @@ typedef struct {
  * failure (skirt_sim_error). */
 SkirtSim* skirt_sim_load(const char* ski, const char* datadir, double packages, uint64_t seed);
 int skirt_sim_info(SkirtSim* sim, SkirtSimInfo* info);
+/* The seed of the photon phases' Philox streams (default: the setup seed). The grid, densities and every
+ * other setup draw stay those of the setup seed, so runs that differ only in this seed are independent
+ * Monte Carlo realisations on one and the same grid (per-cell statistics against a reference run). */
+int skirt_sim_set_photon_seed(SkirtSim* sim, uint64_t seed);
 /* creates the engine on HIP device `device` and uploads grid, media, sources and instruments */
 int skirt_sim_attach(SkirtSim* sim, int device);
 SkirtMcrt* skirt_sim_engine(SkirtSim* sim);
@@ -73,6 +77,17 @@ int skirt_sim_set_tallies(SkirtSim* sim, const double* labs, const double* instr
 int skirt_sim_write(SkirtSim* sim, const char* prefix);
 const char* skirt_sim_error(void);
 void skirt_sim_free(SkirtSim* sim);
+
+/* Voronoi dust grids for a binding inside SKIRT. The reference's VoronoiMesh
+ * keeps its cells' neighbour lists in an implementation type private to VoronoiMesh.cpp, so a binding
+ * hands over the generating sites (VoronoiMesh::particlePosition, in cell order) and the domain, and this
+ * host library tessellates them again (the same tessellation, neighbour order and block lists as the .ski
+ * driver, pinned to the reference's Voronoi fixtures). skirt_host_voronoi_describe fills the Voronoi fields
+ * of a SkirtGridDesc, valid while the SkirtVoronoi lives. */
+typedef struct SkirtVoronoi SkirtVoronoi;
+SkirtVoronoi* skirt_host_voronoi_build(const double* sites, int nsites, const double extent[6]);
+int skirt_host_voronoi_describe(const SkirtVoronoi* v, SkirtGridDesc* grid);
+void skirt_host_voronoi_free(SkirtVoronoi* v);
 
 #ifdef __cplusplus
 }

@@ -64,7 +64,8 @@ ABI_SYMBOLS = [
     "skirt_sim_fetch", "skirt_sim_labs", "skirt_sim_instrument", "skirt_sim_set_tallies", "skirt_sim_write",
     "skirt_sim_error", "skirt_sim_free", "skirt_sim_run_dust", "skirt_sim_labs_dust", "skirt_sim_selfabs_totals",
     "skirt_mcrt_run_phase_shard", "skirt_mcrt_shard_slice", "skirt_mcrt_set_reducer", "skirt_mcrt_reduce_instruments",
-    "skirt_sim_run_stellar_shard", "skirt_sim_run_dust_shard",
+    "skirt_sim_run_stellar_shard", "skirt_sim_run_dust_shard", "skirt_sim_set_photon_seed",
+    "skirt_host_voronoi_build", "skirt_host_voronoi_describe", "skirt_host_voronoi_free",
 ]
 
 _lib = None
@@ -93,6 +94,7 @@ def lib():
         L.skirt_sim_run_stellar.argtypes = [vp, c_u64, c_u64]
         L.skirt_sim_fetch.argtypes = [vp]
         L.skirt_sim_run_dust.argtypes = [vp]
+        L.skirt_sim_set_photon_seed.argtypes = [vp, c_u64]
         L.skirt_sim_run_stellar_shard.argtypes = [vp, c_int, c_int]
         L.skirt_sim_run_dust_shard.argtypes = [vp, c_int, c_int]
         L.skirt_mcrt_set_reducer.argtypes = [vp, REDUCE_FN, vp]
@@ -136,6 +138,11 @@ class Simulation:
         L.skirt_sim_info(self._h, ctypes.byref(info))
         self.info = info
         self.attached = False
+
+    def set_photon_seed(self, seed):
+        """Seed of the photon phases' random streams; the grid and other setup draws keep the setup seed."""
+        self._check(lib().skirt_sim_set_photon_seed(self._h, int(seed)))
+        self.info.seed = int(seed)
 
     def _check(self, rc):
         if rc != 0:

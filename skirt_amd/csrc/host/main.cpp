@@ -35,7 +35,7 @@ int main(int argc, char** argv) {
     skirt_sim_info(sim, &info);
     std::printf("Setup: %d cells, %d wavelengths, %llu packets per wavelength (%.2f s)\n", info.ncells, info.nlambda,
                 (unsigned long long)info.npp, info.setup_seconds);
-    if (skirt_sim_attach(sim, device) || skirt_sim_run_stellar(sim, 0, 0) || skirt_sim_fetch(sim)) {
+    if (skirt_sim_attach(sim, device) || skirt_sim_run_stellar(sim, 0, 0)) {
         std::fprintf(stderr, "*** Error: %s\n", skirt_sim_error());
         skirt_sim_free(sim);
         return 1;
@@ -44,6 +44,18 @@ int main(int argc, char** argv) {
     skirt_mcrt_stats(skirt_sim_engine(sim), &st);
     std::printf("Stellar emission phase: %llu packets in %.3f ms (%.3g packets/s)\n", (unsigned long long)st.packets,
                 st.kernel_ms, st.packets / (st.kernel_ms * 1e-3));
+    // PanMonteCarloSimulation::runSelf (PanMonteCarloSimulation.cpp:96-104): the self-absorption cycles and
+    // the dust emission phase follow the stellar phase (a no-op for Oligo models and Pan models without
+    // dust emission), so the written outputs hold every phase the model asks for
+    const double* dustTot = nullptr;
+    if (skirt_sim_run_dust(sim) || skirt_sim_fetch(sim)) {
+        std::fprintf(stderr, "*** Error: %s\n", skirt_sim_error());
+        skirt_sim_free(sim);
+        return 1;
+    }
+    int ncycles = skirt_sim_selfabs_totals(sim, &dustTot);
+    for (int c = 0; c < ncycles; c++)
+        std::printf("Self-absorption cycle %d: total absorbed dust luminosity %.9g\n", c + 1, dustTot[c]);
     if (skirt_sim_write(sim, out.c_str())) { std::fprintf(stderr, "*** Error: %s\n", skirt_sim_error()); return 1; }
     skirt_sim_free(sim);
     return 0;

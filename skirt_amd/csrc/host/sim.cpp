@@ -107,6 +107,12 @@ int skirt_sim_info(SkirtSim* s, SkirtSimInfo* o) {
     return SKIRT_OK;
 }
 
+int skirt_sim_set_photon_seed(SkirtSim* s, uint64_t seed) {
+    if (!s || !seed) return SKIRT_ERR_ARG;
+    s->m.seed = seed;
+    return SKIRT_OK;
+}
+
 int skirt_sim_attach(SkirtSim* s, int device) {
     if (!s) return SKIRT_ERR_ARG;
     if (s->eng) { skirt_mcrt_destroy(s->eng); s->eng = nullptr; }
@@ -372,5 +378,45 @@ int skirt_sim_write(SkirtSim* s, const char* prefix) {
 }
 
 void skirt_sim_free(SkirtSim* s) { delete s; }
+
+struct SkirtVoronoi {
+    VoronoiGrid g;
+};
+
+SkirtVoronoi* skirt_host_voronoi_build(const double* sites, int nsites, const double extent[6]) {
+    if (!sites || nsites < 1 || !extent) {
+        g_err = "skirt_host_voronoi_build: no sites or no extent";
+        return nullptr;
+    }
+    try {
+        auto v = std::make_unique<SkirtVoronoi>();
+        std::vector<double> sv(sites, sites + 3 * (size_t)nsites);
+        buildVoronoi(v->g, sv, extent[0], extent[3], extent[1], extent[4], extent[2], extent[5]);
+        return v.release();
+    } catch (std::exception& e) {
+        g_err = e.what();
+        return nullptr;
+    }
+}
+
+int skirt_host_voronoi_describe(const SkirtVoronoi* v, SkirtGridDesc* g) {
+    if (!v || !g) return SKIRT_ERR_ARG;
+    const VoronoiGrid& vg = v->g;
+    g->kind = SKIRT_GRID_VORONOI;
+    g->ncells = vg.ncells();
+    g->site = vg.site.data();
+    g->cell_nbr_offset = vg.nbrOffset.data();
+    g->cell_nbr_list = vg.nbrList.data();
+    g->cell_bbox = vg.bbox.data();
+    g->extent[0] = vg.xmin; g->extent[1] = vg.ymin; g->extent[2] = vg.zmin;
+    g->extent[3] = vg.xmax; g->extent[4] = vg.ymax; g->extent[5] = vg.zmax;
+    g->eps = vg.eps;
+    g->nblocks = vg.nb;
+    g->block_offset = vg.blockOffset.data();
+    g->block_list = vg.blockList.data();
+    return SKIRT_OK;
+}
+
+void skirt_host_voronoi_free(SkirtVoronoi* v) { delete v; }
 
 }  // extern "C"

@@ -133,4 +133,5 @@ def test_eight_rank_gloo_shards_balance_the_c3_work(tmp_path):
     work = np.load(os.path.join(tmp_path, "work.npy"))
     segs, pkts = work[:, 0], work[:, 1]
     assert np.all(pkts == pkts[0]) and pkts[0] > 0
+    print("C3 segments per rank:", segs.astype(int).tolist(), "max/mean %.4f" % (segs.max() / segs.mean()))
     assert segs.max() / segs.mean() <= 1.05, segs

@@ -7,7 +7,7 @@ import pytest
 import oracle_lib as O
 import skirt_amd as S
 import tree_models as T
-from test_gpu_parity import close_fraction
+from parity import DUST_OUTLIERS, STELLAR_OUTLIERS, assert_parity
 
 pytestmark = pytest.mark.gpu
 
@@ -26,11 +26,11 @@ def test_geometry_engine_matches_oracle_same_streams(tmp_path, name):
     labs = sim.labs()
     np.testing.assert_allclose(labs.sum(), orc.labs.sum(), rtol=1e-9)
     np.testing.assert_allclose(labs.sum(axis=0), orc.labs.sum(axis=0), rtol=1e-9)
-    assert close_fraction(labs, orc.labs, 1e-9) > 0.999
+    assert_parity(labs, orc.labs, 1e-9, STELLAR_OUTLIERS, "labs")
     frames, seds = sim.instrument(0)
     np.testing.assert_allclose(seds, orc.seds[0], rtol=1e-9, atol=1e-300)
     np.testing.assert_allclose(frames.sum(axis=2), orc.frames[0].sum(axis=2), rtol=1e-9, atol=1e-300)
-    assert close_fraction(frames, orc.frames[0], 1e-9) > 0.999
+    assert_parity(frames, orc.frames[0], 1e-9, STELLAR_OUTLIERS, "frames")
 
 
 def test_dust_free_blackbody_engine_matches_oracle(tmp_path):
@@ -58,7 +58,7 @@ def test_dust_free_blackbody_engine_matches_oracle(tmp_path):
         np.testing.assert_allclose(seds, orc.seds[i], rtol=1e-12, atol=1e-300)
         if orc.frames[i] is not None and orc.frames[i].size:
             np.testing.assert_allclose(frames.sum(axis=2), orc.frames[i].sum(axis=2), rtol=1e-9, atol=1e-300)
-            assert close_fraction(frames, orc.frames[i], 1e-9) > 0.999
+            assert_parity(frames, orc.frames[i], 1e-9, STELLAR_OUTLIERS, "frames")
 
 
 @pytest.mark.parametrize("name", ["zubko_cart", "draineli_cart"])
@@ -73,6 +73,6 @@ def test_dust_mix_engine_matches_oracle_same_streams(tmp_path, name):
     assert sim.stats()["packets"] == orc.packets
     labs = sim.labs()
     np.testing.assert_allclose(labs.sum(axis=0), orc.labs.sum(axis=0), rtol=1e-9)
-    assert close_fraction(labs, orc.labs, 1e-9) > 0.999
+    assert_parity(labs, orc.labs, 1e-9, STELLAR_OUTLIERS, "labs")
     frames, seds = sim.instrument(0)
     np.testing.assert_allclose(seds, orc.seds[0], rtol=1e-9, atol=1e-300)

@@ -7,7 +7,7 @@ import pytest
 import oracle_lib as O
 import skirt_amd as S
 import tree_models as T
-from test_gpu_parity import close_fraction
+from parity import DUST_OUTLIERS, STELLAR_OUTLIERS, assert_parity
 
 pytestmark = pytest.mark.gpu
 
@@ -38,11 +38,11 @@ def test_tree_engine_matches_oracle_same_streams(tmp_path, name, walk):
         labs = sim.labs()
         np.testing.assert_allclose(labs.sum(), orc.labs.sum(), rtol=1e-9)
         np.testing.assert_allclose(labs.sum(axis=0), orc.labs.sum(axis=0), rtol=1e-9)
-        assert close_fraction(labs, orc.labs, 1e-9) > 0.999
+        assert_parity(labs, orc.labs, 1e-9, STELLAR_OUTLIERS, "labs")
     frames, seds = sim.instrument(0)
     np.testing.assert_allclose(seds, orc.seds[0], rtol=1e-9, atol=1e-300)
     np.testing.assert_allclose(frames.sum(axis=2), orc.frames[0].sum(axis=2), rtol=1e-9, atol=1e-300)
-    assert close_fraction(frames, orc.frames[0], 1e-9) > 0.999
+    assert_parity(frames, orc.frames[0], 1e-9, STELLAR_OUTLIERS, "frames")
 
 
 @pytest.mark.parametrize("name", ["bin_pan", "bin_full"])
