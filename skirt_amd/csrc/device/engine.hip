@@ -60,7 +60,7 @@ constexpr int kStepsPerPull = SKIRT_STEPS_PER_PULL;  // grid steps between two r
 #endif
 constexpr int kHalves = SKIRT_HALVES;
 constexpr int kSersicTable = 202;  // SersicFunction: 101 radii, then 101 cumulative masses
-constexpr int kDetectCopies = 8;   // LDS copies of the SED sums in the detect kernel (one per 8 lanes)
+constexpr int kDetectCopies = 8;   // most LDS copies of the SED sums in the detect kernel (one per 8 lanes)
 constexpr int kPollEvery = 1;      // iterations between two counter copies of a half
 constexpr int kPollRing = 3;       // copies in flight per half (the host reads each kPollRing copies late)
 // occupancy attribute of the trace kernel (a build knob for tuning variants, tools/build_variant.sh):
@@ -231,6 +231,7 @@ struct Args {
                                  // [5,6] detection record counts
     int parity, init, threshold;
     int ldsMeshOff, ldsOptOff, ldsInstrOff, ldsSedOff;  // in doubles
+    int detCopies;  // detect kernel: LDS copies of the SED sums (8, 4, 2, 1), 0 = SEDs straight to the tally
 };
 
 // One finest-level cell of the octree leaf map: the leaf node that covers it, that leaf's dust cell
@@ -1231,8 +1232,6 @@ __device__ __forceinline__ void detectPeel(const Args& a, const DevInstr& ins, u
 // NR::cdf of PanMonteCarloSimulation.cpp:193-205, 273-294), computed from the device tallies so the
 // self-absorption cycles never leave the GPU. Reference cell order, like the host restatement
 // (host/dustemission.cpp), which the tests compare against.
-constexpr int kMaxEmisLambda = 64;
-
 struct EmisArgs {
     int ncells, nlambda, ncomp, ntemp;
     const int* devCell;          // reference cell -> device cell (null: identity)
@@ -1272,23 +1271,27 @@ __global__ void __launch_bounds__(kBlock) cellSpectraKernel(const EmisArgs e) {
     for (int ell = 0; ell < Nl; ell++) Labsbol += e.labs[ell * S + dm];
     if (e.labsDust)
         for (int ell = 0; ell < Nl; ell++) Labsbol += e.labsDust[ell * S + dm];
-    double Jv[kMaxEmisLambda], Lv[kMaxEmisLambda];
+    // J_lambda is needed only for the absorbed power of each component, and the emission spectrum Lv is
+    // accumulated in the cell's own column of the output (the arithmetic of the host restatement, one
+    // operation at a time), so any number of wavelengths fits
     const double fac = 4.0 * M_PI * e.volume[m];
-    for (int ell = 0; ell < Nl; ell++) {  // DustSystem::meanintensityv
+    auto meanIntensity = [&](int ell) {  // DustSystem::meanintensityv
         double L = 0;
         L += e.labs[ell * S + dm];
         if (e.labsDust) L += e.labsDust[ell * S + dm];
         double kr = 0.0;
         for (int h = 0; h < e.ncomp; h++) kr += e.kabs[h * Nl + ell] * e.rho[(size_t)dm * e.ncomp + h];
         const double J = L / (kr * fac) / e.dlambda[ell];
-        Jv[ell] = isfinite(J) ? J : 0.0;
-        Lv[ell] = 0.0;
-    }
+        return isfinite(J) ? J : 0.0;
+    };
+    double* Lv = e.lv + m;  // Lv[ell] at Lv[ell * ncells]
+    const size_t N = e.ncells;
+    for (int ell = 0; ell < Nl; ell++) Lv[ell * N] = 0.0;
     for (int h = 0; h < e.ncomp; h++) {
         // DustMix::equilibrium -> invplanckabs (NR::locate_clip + linear interpolation)
         const double* sa = e.sigmaabs + h * Nl;
         double pa = 0.0;
-        for (int ell = 0; ell < Nl; ell++) pa += sa[ell] * Jv[ell] * e.dlambda[ell];
+        for (int ell = 0; ell < Nl; ell++) pa += sa[ell] * meanIntensity(ell) * e.dlambda[ell];
         const double* tab = e.planckabs + (size_t)h * e.ntemp;
         int p;
         if (pa < tab[0]) p = 0;
@@ -1303,18 +1306,19 @@ __global__ void __launch_bounds__(kBlock) cellSpectraKernel(const EmisArgs e) {
             double ev = 0.0;
             ev += sa[ell] * planckB(T, e.lambda[ell]);
             ev /= e.mu[h];
-            if (e.ncomp > 1) Lv[ell] += ev * w;
-            else Lv[ell] = ev;
+            if (e.ncomp > 1) Lv[ell * N] += ev * w;
+            else Lv[ell * N] = ev;
         }
     }
     double total = 0.0;
     for (int ell = 0; ell < Nl; ell++) {
-        Lv[ell] *= e.dlambda[ell];
-        total += Lv[ell];
+        const double v = Lv[ell * N] * e.dlambda[ell];
+        Lv[ell * N] = v;
+        total += v;
     }
     for (int ell = 0; ell < Nl; ell++) {
-        const double lum = total > 0 ? Lv[ell] / total : Lv[ell];
-        e.lv[(size_t)ell * e.ncells + m] = Labsbol > 0.0 ? Labsbol * lum : 0.0;
+        const double lum = total > 0 ? Lv[ell * N] / total : Lv[ell * N];
+        Lv[ell * N] = Labsbol > 0.0 ? Labsbol * lum : 0.0;
     }
 }
 
@@ -1500,15 +1504,17 @@ __global__ void __launch_bounds__(kBlock) detectKernel(const Args a) {
     const unsigned int nrays = a.ctr[5 + a.parity];  // this iteration's detection records
     if (nrays == 0) return;
     Shared sh = stageTables(a, lds, STAGE_INSTR);
-    for (int q = threadIdx.x; q < kDetectCopies * a.nsed; q += blockDim.x) sh.sed[q] = 0.0;
+    const int copies = a.detCopies;
+    for (int q = threadIdx.x; q < copies * a.nsed; q += blockDim.x) sh.sed[q] = 0.0;
     __syncthreads();
     unsigned int detects = 0;
     // eight lanes per ray, one per instrument slot (mod 8): the frame adds of one detection fall in one
     // 64-byte line (frameAt) and leave in one wave instruction, so they share one atomic request. Each
-    // group of 8 lanes sums SEDs into its own LDS copy: the 8 rays of an instruction mostly hit the same
-    // few (slot, wavelength) sums, which one copy would serialize.
+    // group of 8 lanes sums SEDs into its own LDS copy (up to 8 copies, as many as the LDS holds): the 8
+    // rays of an instruction mostly hit the same few (slot, wavelength) sums, which one copy would
+    // serialize. Without room for one copy (very many wavelengths x slots) the SED adds go to the tally.
     const int lane = threadIdx.x & 63, sub = lane & 7;
-    double* sed = sh.sed + (lane >> 3) * a.nsed;
+    double* sed = copies ? sh.sed + ((lane >> 3) & (copies - 1)) * a.nsed : nullptr;
     const unsigned int waves = gridDim.x * (blockDim.x / 64);
     const unsigned int wave = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
     for (unsigned int base = wave * 8; base < nrays; base += waves * 8) {
@@ -1522,16 +1528,19 @@ __global__ void __launch_bounds__(kBlock) detectKernel(const Args a) {
         for (int slot = sub; slot < ins.nslots; slot += 8) {
             double v;
             if (!detectSlot(ins, flags, slot, Lp, Lextf, v)) continue;
-            if (ins.kind != SKIRT_INSTR_FRAME) atomicAdd(&sed[ins.sedOff + slot * a.nlambda + ell], v);
+            if (ins.kind != SKIRT_INSTR_FRAME) {
+                if (sed) atomicAdd(&sed[ins.sedOff + slot * a.nlambda + ell], v);
+                else atomicAddF64(a.tally + ins.sedBase + slot * a.nlambda + ell, v);
+            }
             if (l >= 0 && ins.kind != SKIRT_INSTR_SED) atomicAddF64(frameAt(a, ins, ell, l, slot), v);
         }
         if (sub == 0) detects++;
     }
     // flush the per-workgroup SED sums
     __syncthreads();
-    for (int q = threadIdx.x; q < a.nsed; q += blockDim.x) {
+    for (int q = threadIdx.x; copies && q < a.nsed; q += blockDim.x) {
         double v = 0.0;
-        for (int g = 0; g < kDetectCopies; g++) v += sh.sed[g * a.nsed + q];
+        for (int g = 0; g < copies; g++) v += sh.sed[g * a.nsed + q];
         if (v != 0.0) {
             int ii = 0;
             while (ii + 1 < a.ninstr && sh.instr[ii + 1].sedOff <= q) ii++;
@@ -2269,12 +2278,14 @@ struct SkirtMcrt {
     size_t poolBytes = 0;
     // config
     int traceGrid = 0, threshold = 8, slotsWanted = 0;
+    int lastDetCopies = 0;  // SED copies of the last run's detect kernel
     double lastMs = 0;
     std::vector<hipEvent_t> traceEv;  // pairs around the trace launches not yet timed
     int traceLaunches = 0;
     double traceMs = 0;               // all timed trace launches since the context was created
     uint64_t traceLaunchesTotal = 0;
     int numCUs = 0;
+    size_t ldsMax = 64 * 1024;  // LDS one workgroup may allocate (hipDeviceProp_t::sharedMemPerBlock; 160 KiB on gfx950)
     int lastIterations = 0;
     // multi-process reduction of the tallies (skirt_mcrt_set_reducer)
     SkirtReduceTallyFn reduce = nullptr;
@@ -2453,7 +2464,10 @@ int skirt_mcrt_create(int device, SkirtMcrt** out) {
     }
     c->stream = c->own;
     hipDeviceProp_t prop;
-    if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->numCUs = prop.multiProcessorCount;
+    if (hipGetDeviceProperties(&prop, device) == hipSuccess) {
+        c->numCUs = prop.multiProcessorCount;
+        if (prop.sharedMemPerBlock > 0) c->ldsMax = prop.sharedMemPerBlock;
+    }
     (void)hipMemset(c->dStats, 0, 8 * kStatCopies * sizeof(unsigned long long));
     (void)hipMemset(c->dError, 0, sizeof(unsigned int));
     *out = c;
@@ -2899,7 +2913,6 @@ int skirt_mcrt_upload_emissivity(SkirtMcrt* c, const SkirtEmissivityDesc* d) {
     if (c->gridKind < 0 || !c->dRho) return fail(c, SKIRT_ERR_STATE, "upload the grid and media before the emissivity");
     if (d->ncells != c->ncells || d->nlambda != c->nlambda || d->ncomp != c->ncomp || d->ntemp < 2)
         return fail(c, SKIRT_ERR_ARG, "emissivity tables do not match the grid, wavelengths and media");
-    if (d->nlambda > kMaxEmisLambda) return fail(c, SKIRT_ERR_UNSUPPORTED, "device dust emission supports at most 64 wavelengths");
     HIPCHECK(c, hipSetDevice(c->device));
     const size_t nl = (size_t)d->nlambda, nh = (size_t)d->ncomp;
     int rc;
@@ -3185,14 +3198,27 @@ static int runPhase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, uint6
     off += a.ninstr * (int)(sizeof(DevInstr) / sizeof(double));
     a.ldsSedOff = off;
     off += c->nsed;
-    const size_t lds = (size_t)off * sizeof(double);                       // detect kernel: everything
     const size_t ldsTrace = (size_t)a.ldsInstrOff * sizeof(double)          // grid tables + optics
                             + (size_t)kLabsBuf * kBlock * (sizeof(double) + sizeof(unsigned));  // + Labs buffers
     const size_t ldsEvent = (size_t)a.ldsSedOff * sizeof(double);           // + instruments
-    if (lds > 64 * 1024) return fail(c, SKIRT_ERR_UNSUPPORTED, "tables do not fit in LDS (" + std::to_string(lds) + " bytes)");
-    // detect kernel: kDetectCopies copies of the SED sums (one per group of 8 lanes, see detectKernel)
-    const size_t ldsDetect = lds + (size_t)(kDetectCopies - 1) * c->nsed * sizeof(double);
-    if (ldsDetect > 64 * 1024) return fail(c, SKIRT_ERR_UNSUPPORTED, "instrument SEDs do not fit in LDS");
+    // budget: what one workgroup may allocate (160 KiB on gfx950). The trace and event kernels need their
+    // tables; the detect kernel keeps as many SED copies as fit (8, 4, 2, 1), or none (SEDs to the tally)
+    const size_t budget = c->ldsMax;
+    if (ldsTrace > budget || ldsEvent > budget)
+        return fail(c, SKIRT_ERR_UNSUPPORTED, "grid and optical tables do not fit in LDS (" +
+                                                  std::to_string(std::max(ldsTrace, ldsEvent)) + " of " +
+                                                  std::to_string(budget) + " bytes)");
+    // SKIRT_AMD_DET_COPIES caps the copies (tests of the fallbacks)
+    const int capCopies = getenv("SKIRT_AMD_DET_COPIES") ? atoi(getenv("SKIRT_AMD_DET_COPIES")) : kDetectCopies;
+    a.detCopies = kDetectCopies;
+    while (a.detCopies > 0 && a.detCopies > capCopies) a.detCopies >>= 1;
+    while (a.detCopies > 0 && ldsEvent + (size_t)a.detCopies * c->nsed * sizeof(double) > budget) a.detCopies >>= 1;
+    const size_t ldsDetect = ldsEvent + (size_t)a.detCopies * c->nsed * sizeof(double);
+    c->lastDetCopies = a.detCopies;
+    // launches above 64 KiB of dynamic LDS declare it first
+    if (ldsDetect > 64 * 1024)
+        HIPCHECK(c, hipFuncSetAttribute((const void*)detectKernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                        (int)ldsDetect));
     const int kind = c->gridKind == SKIRT_GRID_CARTESIAN ? SKIRT_GRID_CARTESIAN
                      : c->gridKind == SKIRT_GRID_VORONOI ? SKIRT_GRID_VORONOI
                      : bookkeeping ? kOctreeBookkeeping
@@ -3212,6 +3238,8 @@ static int runPhase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, uint6
     else if (kind == kOctreeBookkeeping) pick(traceKernel<kOctreeBookkeeping, true>, traceKernel<kOctreeBookkeeping, false>);
     else if (kind == SKIRT_GRID_VORONOI) pick(traceKernel<SKIRT_GRID_VORONOI, true>, traceKernel<SKIRT_GRID_VORONOI, false>);
     else pick(traceKernel<kOctreeNodes, true>, traceKernel<kOctreeNodes, false>);
+    if (ldsTrace > 64 * 1024)
+        HIPCHECK(c, hipFuncSetAttribute(traceFn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ldsTrace));
     int tgrid = c->traceGrid;
     if (tgrid <= 0) {
         int per = 0;

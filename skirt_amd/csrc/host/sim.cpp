@@ -250,9 +250,9 @@ int skirt_sim_run_dust_shard(SkirtSim* s, int rank, int world) {
         const std::vector<PlanckTable> tables = planckTables(m);
         SkirtPhaseParams p{m.minWeightReduction, m.minScattEvents, m.scattBias, 0, 1};
         // The cell sources between phases: on the device from the device tallies (default), or on the
-        // host by the restatement the oracle shares (SKIRT_AMD_HOST_SOURCES=1, or more than 64 wavelengths)
+        // host by the restatement the oracle shares (SKIRT_AMD_HOST_SOURCES=1)
         const char* env = getenv("SKIRT_AMD_HOST_SOURCES");
-        const bool hostSources = (env && env[0] == '1') || Nl > 64;
+        const bool hostSources = env && env[0] == '1';
         std::vector<double> lum;
         CellSources src;
         if (hostSources) {

@@ -328,3 +328,28 @@ def test_transparent_flux_is_deterministic():
         sim.write(os.path.join(d, "t"))
         sed = F.read_text_tokens(os.path.join(d, "t_i30_sed.dat"))
     assert sed[0][6] == "2.41996378e-12"
+
+
+@pytest.mark.parametrize("copies", [None, "1", "0"])
+def test_many_wavelengths_match_oracle_same_streams(copies, monkeypatch):
+    """200 wavelengths and a FullInstrument with 2 scattering levels: 7 slots x 200 SED sums, 8 LDS copies
+    of 11.2 KB each (beyond the 64 KB the round-1 engine refused), and the dust phases' device cell
+    sources over 200 wavelengths. Also with the detect kernel's SED copies capped at 1, and at 0 (SED adds
+    straight to the tally, the fallback when not even one copy fits). Same streams as the oracle."""
+    if copies is not None:
+        monkeypatch.setenv("SKIRT_AMD_DET_COPIES", copies)
+    name = "pan_cart16_l200"
+    sim = S.Simulation(ski(name))
+    sim.attach(0)
+    sim.run_stellar()
+    sim.run_dust()
+    sim.fetch()
+    orc = O.run(ski(name), rng=O.RNG_PHILOX, threads=16, phases=O.PHASES_ALL)
+    assert sim.info.nlambda == 200
+    np.testing.assert_allclose(sim.labs().sum(axis=0), orc.labs.sum(axis=0), rtol=1e-9)
+    assert_parity(sim.labs(), orc.labs, 1e-9, STELLAR_OUTLIERS, "labs")
+    frames, seds = sim.instrument(0)
+    assert seds.shape == (7, 200) and seds[3:5].sum() > 0 and seds[5:7].sum() > 0
+    np.testing.assert_allclose(seds, orc.seds[0], rtol=1e-8, atol=1e-300)
+    np.testing.assert_allclose(frames.sum(axis=2), orc.frames[0].sum(axis=2), rtol=1e-8, atol=1e-300)
+    assert_parity(frames, orc.frames[0], 1e-8, DUST_OUTLIERS, "frames")
