@@ -21,6 +21,12 @@ import time
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
+# Bytes one grid segment of the trace kernel actually reads in this engine's layouts,
+# beside SURVEY 8(d)'s figure: octree leaf map 16 (one entry {node, cell|level, rho0}); Cartesian 8 (rho,
+# the mesh is in LDS); Voronoi 48 + 16 k (the cell's header {exact site, rho0, id, count} and one 16-byte
+# entry per neighbour, k = 15.5 on the C4 mesh)
+ENGINE_SEGMENT_BYTES = {0: 8.0, 1: 16.0, 2: 48.0 + 16.0 * 15.5}
+
 CONFIGS = {
     # name: (ski, packets per wavelength per rank, segment geometry bytes, description)
     # C3 is 4e7 packets per wavelength (1e9 in all) over 8 GPUs: 5e6 per wavelength per rank
@@ -194,6 +200,8 @@ def main():
     achieved = bytes_per_launch / launch_s / 1e9
     traffic = pmc_traffic(args.config)
     hbm_frac = achieved / HBM_PEAK_GBS
+    # the same launch priced at the bytes this engine's layouts read (ENGINE_SEGMENT_BYTES)
+    engine_bytes = (segs * ENGINE_SEGMENT_BYTES[info.grid_kind] + delta["absorb_adds"] * 16) / max(1, trace_launches)
     requests_per_s = delta["labs_requests"] / max(1e-9, trace_ms / 1e3)
     atomic_frac = requests_per_s / ATOMIC_PEAK_REQUESTS
 
@@ -244,6 +252,9 @@ def main():
             "launch_ms_avg": launch_s * 1e3,
             "launches_per_step": trace_launches / args.steps,
             "algorithmic_bytes_per_launch": bytes_per_launch,
+            "engine_bytes_per_launch": engine_bytes,
+            "engine_gbs": engine_bytes / launch_s / 1e9,
+            "engine_frac": engine_bytes / launch_s / 1e9 / HBM_PEAK_GBS,
             "traffic_source": traffic["source"] if traffic else None,
             "traffic_gbs": traffic["bytes_per_launch"] / launch_s / 1e9 if traffic else None,
             # Labs adds are scattered f64 atomics, executed memory-side in 64-byte requests at a fixed

@@ -65,10 +65,10 @@ constexpr int kPollEvery = 1;      // iterations between two counter copies of a
 constexpr int kPollRing = 3;       // copies in flight per half (the host reads each kPollRing copies late)
 // occupancy attribute of the trace kernel (a build knob for tuning variants, tools/build_variant.sh):
 // 3 waves per SIMD, i.e. at most 168 VGPRs (the grid entry on the pull path would otherwise take the
-// octree kernel to 175 and 2 waves; C3 1.91e8 -> 2.15e8 pkt/s at 3). The Voronoi step needs 190 and
-// runs faster at 2 waves than spilling at 3.
+// octree kernel to 175 and 2 waves; C3 1.91e8 -> 2.15e8 pkt/s at 3). The Voronoi step, at 4 entries per
+// load round, spills 60 B/lane at 3 waves and still runs fastest there (C4, profiles/r02_sweep_vor.txt).
 #ifndef SKIRT_TRACE_ATTR
-#define SKIRT_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(GRID == SKIRT_GRID_VORONOI ? 2 : 3)))
+#define SKIRT_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(3)))
 #endif
 #ifndef SKIRT_EVENT_ATTR
 #define SKIRT_EVENT_ATTR
@@ -109,6 +109,9 @@ struct __attribute__((aligned(16))) RayRec {
 static_assert(sizeof(RayRec) == 112, "ray record layout");
 template <int GRID>
 constexpr bool kEnterInEvent = GRID == SKIRT_GRID_VORONOI;
+// most segments one Grid<GRID>::step adds (the Voronoi step may add a pending and a new segment)
+template <int GRID>
+constexpr int kSegsPerStep = GRID == SKIRT_GRID_VORONOI ? 2 : 1;
 
 // the detection of one peel-off ray, in a compact array of its own (the detect kernel reads only these,
 // contiguously, instead of scanning every ray record): written by the event kernel, tau by the trace
@@ -128,20 +131,25 @@ __device__ __forceinline__ int rayEll(unsigned f) { return (int)(f >> 18); }
 
 struct LeafEntry;
 
-// one entry of a Voronoi cell's neighbour list: the neighbour's device cell number (walls -1 .. -6)
-// with its site inline, so that a step reads the cell's list as one contiguous run instead of
-// gathering the neighbours' sites, and where the neighbour's own list starts, so that the next step
-// needs no offset lookup. The last entry of every list has bit 31 of `next` set.
-struct alignas(16) VoronoiNbr {
-    double x, y, z;
-    int id;
-    int next;  // start of the neighbour's list | kVorLast on a list's last entry
+// Voronoi cells on the device: per cell a block of 16-byte slots, contiguous, in device cell order: a
+// 48-byte header {exact site x, y | z, rho of component 0 | device cell number, neighbour count, 0, 0}
+// followed by one slot per neighbour, in the reference's list order: the neighbour's site relative to the
+// cell's site, scaled by Args::vorScale and rounded to float (an approximate bisector plane), and where the
+// neighbour's block starts
+// (walls: -1 xmin .. -6 zmax). A step bounds every plane distance from the float offsets, and evaluates
+// the reference's exact expression only for the winner (from the winner's header, which is the next
+// step's first load) or, when the bounds cannot single one out, for every possible winner.
+struct alignas(16) VorEntry {
+    float ox, oy, oz;
+    int next;
 };
-constexpr int kVorLast = (int)0x80000000u;
+constexpr int kVorHead = 3;  // header slots
 #ifndef SKIRT_VOR_UNROLL
-#define SKIRT_VOR_UNROLL 8
+#define SKIRT_VOR_UNROLL 4
 #endif
-constexpr int kVorUnroll = SKIRT_VOR_UNROLL;  // list entries loaded per round trip (the array is padded)
+constexpr int kVorUnroll = SKIRT_VOR_UNROLL;  // entries loaded per round trip (the slot array is padded)
+// bound factor of the approximate (single-precision) plane distances: 16 x 2^-24
+constexpr float kVorEpsF = 1.0f / (1 << 20);
 
 // grid kinds of the kernels: SKIRT_GRID_CARTESIAN, SKIRT_GRID_OCTREE (leaf-map walk), the k-d tree
 // through its leaf map, and any tree walked through the node arrays (trees deeper than the leaf maps
@@ -167,8 +175,9 @@ struct Args {
     double eps;
     int search;
     const double* site;          // Voronoi, device cell order: 3 per cell
-    const int* cellNbrOffset;    // Voronoi neighbour lists
-    const VoronoiNbr* cellNbr;
+    const int* vorStart;         // Voronoi: where each device cell's block of slots starts
+    const VorEntry* vorSlots;    // Voronoi: headers and neighbour entries
+    float vorScale;              // Voronoi: 1 / (largest half-width of the domain), the entries' offset unit
     const double* cellBbox;      // Voronoi: enclosing box per cell
     const int* devCell;          // reference cell -> device cell (Voronoi launches)
     int vnb;                     // Voronoi block grid: blocks per axis
@@ -951,84 +960,181 @@ struct Grid<SKIRT_GRID_VORONOI> {
             if (d[q] > 0) seg(-1, 0.0, d[q]);
         r.x = rx; r.y = ry; r.z = rz;
         r.ci = m;
-        r.cj = a.cellNbrOffset[m];
+        r.cj = a.vorStart[m];
+        r.ck = 0;
         return true;
     }
 
-    // r.ci: the current (device) cell, r.cj: where its neighbour list starts
+    __device__ static __forceinline__ double wallDist(const Args& a, const Ray& r, int w) {
+        switch (w) {
+        case -1: return (a.gx0 - r.x) / r.dx;
+        case -2: return (a.gx1 - r.x) / r.dx;
+        case -3: return (a.gy0 - r.y) / r.dy;
+        case -4: return (a.gy1 - r.y) / r.dy;
+        case -5: return (a.gz0 - r.z) / r.dz;
+        default: return (a.gz1 - r.z) / r.dz;
+        }
+    }
+
+    // the reference's distance along the ray to the bisector plane of sites pr (the current cell) and pi
+    // (a neighbour), 0 when the ray moves away from it -- VoronoiMesh.cpp:790-806, same operation order
+    __device__ static __forceinline__ double planeDist(const Ray& r, double prx, double pry, double prz, double pix,
+                                                       double piy, double piz) {
+        const double nx = pix - prx, ny = piy - pry, nz = piz - prz;
+        const double ndotk = nx * r.dx + ny * r.dy + nz * r.dz;
+        if (!(ndotk > 0)) return 0;
+        const double px = 0.5 * (pix + prx), py = 0.5 * (piy + pry), pz = 0.5 * (piz + prz);
+        return (nx * (px - r.x) + ny * (py - r.y) + nz * (pz - r.z)) / ndotk;
+    }
+
+    __device__ static __forceinline__ void siteAt(const Args& a, int start, double& x, double& y, double& z) {
+        const double2 h0 = *reinterpret_cast<const double2*>(a.vorSlots + start);
+        const double2 h1 = *reinterpret_cast<const double2*>(a.vorSlots + start + 1);
+        x = h0.x; y = h0.y; z = h1.x;
+    }
+
+    // One step (VoronoiMesh::path, VoronoiMesh.cpp:749-844). r.cj: the block of the cell the ray is in.
+    // r.ck = 1: the previous cell's segment (cell r.ci, density r.rho0, site r.bx0..bz0) is still to be
+    // added; it ends on the bisector plane with this cell, whose exact site arrives with this step's load.
+    // A step therefore issues one round of loads (this cell's header and first entries) in the common case.
+    // It adds at most two segments (the pending one, and one more when the bounds leave several possible
+    // winners), see kSegsPerStep.
     template <class SegFn>
     __device__ static __forceinline__ bool step(const Args& a, const Shared&, Ray& r, SegFn seg) {
-        const int mr = r.ci;
-        const double* S = a.site;
-        const double prx = S[3 * mr], pry = S[3 * mr + 1], prz = S[3 * mr + 2];
-        const double rho0 = a.rho[(size_t)mr * a.ncomp];
-        const double kx = r.dx, ky = r.dy, kz = r.dz;
-        double sq = kDblMax;
-        constexpr int NO_INDEX = -99;
-        int mq = NO_INDEX, mqList = 0;
-        for (int q = r.cj;; q += kVorUnroll) {
-            VoronoiNbr e[kVorUnroll];
+        const VorEntry* B = a.vorSlots + r.cj;
+        const double2 h0 = *reinterpret_cast<const double2*>(B);
+        const double2 h1 = *reinterpret_cast<const double2*>(B + 1);
+        const int4 h2 = *reinterpret_cast<const int4*>(B + 2);
+        VorEntry e[kVorUnroll];
 #pragma unroll
-            for (int u = 0; u < kVorUnroll; u++) e[u] = a.cellNbr[q + u];
-            bool last = false;
+        for (int u = 0; u < kVorUnroll; u++) e[u] = B[kVorHead + u];
+        const double pwx = h0.x, pwy = h0.y, pwz = h1.x, rhow = h1.y;
+        const int idw = h2.x, cnt = h2.y;
+        if (r.ck) {
+            const double sq = planeDist(r, r.bx0, r.by0, r.bz0, pwx, pwy, pwz);
+            if (!seg(r.ci, r.rho0, sq)) return false;
+            r.x += (sq + a.eps) * r.dx; r.y += (sq + a.eps) * r.dy; r.z += (sq + a.eps) * r.dz;
+            r.ck = 0;
+        }
+        const double kx = r.dx, ky = r.dy, kz = r.dz;
+        // the bounds in single precision, on coordinates scaled by a.vorScale (the entries' offsets are
+        // stored scaled): each float operation adds a few 2^-24 of the sum of absolute terms, which
+        // kVorEpsF covers with margin; an approximate reciprocal (1 ulp) is covered by the |s| term
+        const float sc = a.vorScale;
+        const float Dx = (float)((pwx - r.x) * sc), Dy = (float)((pwy - r.y) * sc), Dz = (float)((pwz - r.z) * sc);
+        const float fkx = (float)kx, fky = (float)ky, fkz = (float)kz;
+        // bounds [lo, hi] of every neighbour's plane distance; U: the least upper bound of the certain
+        // exits; L1 < L2: the two least lower bounds of the possible exits, w1: the first one's `next`
+        float U = FLT_MAX, L1 = FLT_MAX, L2 = FLT_MAX;
+        int w1 = 0;
+        for (int q0 = 0; q0 < cnt; q0 += kVorUnroll) {
+            if (q0) {
+#pragma unroll
+                for (int u = 0; u < kVorUnroll; u++) e[u] = B[kVorHead + q0 + u];
+            }
 #pragma unroll
             for (int u = 0; u < kVorUnroll; u++) {
-                if (last) break;
-                const int mi = e[u].id;
-                double si = 0;
-                if (mi >= 0) {
-                    const double pix = e[u].x, piy = e[u].y, piz = e[u].z;
-                    const double nx = pix - prx, ny = piy - pry, nz = piz - prz;
-                    const double ndotk = nx * kx + ny * ky + nz * kz;
-                    if (ndotk > 0) {
-                        const double px = 0.5 * (pix + prx), py = 0.5 * (piy + pry), pz = 0.5 * (piz + prz);
-                        si = (nx * (px - r.x) + ny * (py - r.y) + nz * (pz - r.z)) / ndotk;
+                const int nxt = e[u].next;
+                float lo = FLT_MAX, hi = 0.f;
+                if (q0 + u >= cnt) {
+                    // past the list: no exit
+                } else if (nxt < 0) {
+                    const double si = wallDist(a, r, nxt);
+                    if (si > 0) {
+                        const float v = (float)(si * sc);
+                        lo = v * (1.0f - kVorEpsF);
+                        hi = v * (1.0f + kVorEpsF);
                     }
                 } else {
-                    switch (mi) {
-                    case -1: si = (a.gx0 - r.x) / kx; break;
-                    case -2: si = (a.gx1 - r.x) / kx; break;
-                    case -3: si = (a.gy0 - r.y) / ky; break;
-                    case -4: si = (a.gy1 - r.y) / ky; break;
-                    case -5: si = (a.gz0 - r.z) / kz; break;
-                    default: si = (a.gz1 - r.z) / kz; break;
+                    const float nx = e[u].ox, ny = e[u].oy, nz = e[u].oz;
+                    const float px = nx * fkx, py = ny * fky, pz = nz * fkz;
+                    const float den = px + py + pz;
+                    const float eA = kVorEpsF * (fabsf(px) + fabsf(py) + fabsf(pz));
+                    if (den > -eA) {  // else moving away from this plane for certain: no exit
+                        const float tx = Dx + 0.5f * nx, ty = Dy + 0.5f * ny, tz = Dz + 0.5f * nz;
+                        const float qx = nx * tx, qy = ny * ty, qz = nz * tz;
+                        const float num = qx + qy + qz;
+                        const float eB = kVorEpsF * (fabsf(qx) + fabsf(qy) + fabsf(qz) + 0.5f * (nx * nx + ny * ny + nz * nz));
+                        if (den > 2.0f * eA) {
+                            const float inv = __builtin_amdgcn_rcpf(den);
+                            const float sa = num * inv;
+                            const float err = 2.0f * (eB + fabsf(sa) * eA) * inv + fabsf(sa) * kVorEpsF;
+                            if (sa + err > 0.f) { lo = sa - err; hi = sa + err; }
+                        } else {
+                            lo = -FLT_MAX; hi = FLT_MAX;  // the sign of n.k is uncertain
+                        }
                     }
                 }
-                if (si > 0 && si < sq) { sq = si; mq = mi; mqList = e[u].next & ~kVorLast; }
-                last = e[u].next < 0;
+                if (lo != FLT_MAX) {
+                    if (lo > 0.f && hi < U) U = hi;
+                    if (lo < L1) { L2 = L1; L1 = lo; w1 = nxt; }
+                    else if (lo < L2) L2 = lo;
+                }
             }
-            if (last) break;
+        }
+        if (L1 != FLT_MAX && L2 > U) {
+            if (w1 >= 0) {  // the exit: its exact distance when the next cell's header arrives
+                r.ck = 1;
+                r.ci = idw; r.rho0 = rhow;
+                r.bx0 = pwx; r.by0 = pwy; r.bz0 = pwz;
+                r.cj = w1;
+                return true;
+            }
+            seg(idw, rhow, wallDist(a, r, w1));  // leaves the grid through a wall
+            return false;
+        }
+        // no exit, or several possible exits: the reference's rule, exactly, over the whole list
+        constexpr int NO_INDEX = (int)0x80000000u;
+        double sq = kDblMax;
+        int mq = NO_INDEX;
+        if (L1 != FLT_MAX) {
+            for (int q = 0; q < cnt; q++) {
+                const int nxt = B[kVorHead + q].next;
+                double si;
+                if (nxt < 0) si = wallDist(a, r, nxt);
+                else {
+                    double pix, piy, piz;
+                    siteAt(a, nxt, pix, piy, piz);
+                    si = planeDist(r, pwx, pwy, pwz, pix, piy, piz);
+                }
+                if (si > 0 && si < sq) { sq = si; mq = nxt; }
+            }
         }
         if (mq == NO_INDEX) {
             // no exit found: advance by eps and locate again (VoronoiMesh.cpp:831-835)
             r.x += kx * a.eps; r.y += ky * a.eps; r.z += kz * a.eps;
-            r.ci = cellIndex(a, r.x, r.y, r.z);
-            if (r.ci < 0) return false;
-            r.cj = a.cellNbrOffset[r.ci];
+            const int m = cellIndex(a, r.x, r.y, r.z);
+            if (m < 0) return false;
+            r.ci = m;
+            r.cj = a.vorStart[m];
             return true;
         }
-        if (!seg(mr, rho0, sq)) return false;
+        if (!seg(idw, rhow, sq)) return false;
         r.x += (sq + a.eps) * kx; r.y += (sq + a.eps) * ky; r.z += (sq + a.eps) * kz;
-        r.ci = mq;
-        r.cj = mqList;
+        r.cj = mq;
         return mq >= 0;
     }
-
 
     __device__ static __forceinline__ int whichcell(const Args& a, const Shared&, double x, double y, double z) {
         return cellIndex(a, x, y, z);
     }
 
-    // VoronoiMesh::isPointClosestTo
+    // VoronoiMesh::isPointClosestTo, over the exact sites of the cell's neighbours (their headers)
     __device__ static __forceinline__ bool closestTo(const Args& a, double x, double y, double z, int m) {
         auto d2 = [&](double sx, double sy, double sz) {
             const double dx = x - sx, dy = y - sy, dz = z - sz;
             return dx * dx + dy * dy + dz * dz;
         };
-        const double target = d2(a.site[3 * m], a.site[3 * m + 1], a.site[3 * m + 2]);
-        for (int q = a.cellNbrOffset[m]; q < a.cellNbrOffset[m + 1]; q++) {
-            const VoronoiNbr nb = a.cellNbr[q];
-            if (nb.id >= 0 && d2(nb.x, nb.y, nb.z) < target) return false;
+        const int start = a.vorStart[m];
+        double sx, sy, sz;
+        siteAt(a, start, sx, sy, sz);
+        const double target = d2(sx, sy, sz);
+        const int cnt = reinterpret_cast<const int4*>(a.vorSlots + start + 2)->y;
+        for (int q = 0; q < cnt; q++) {
+            const int nxt = a.vorSlots[start + kVorHead + q].next;
+            if (nxt < 0) continue;
+            siteAt(a, nxt, sx, sy, sz);
+            if (d2(sx, sy, sz) < target) return false;
         }
         return true;
     }
@@ -1152,6 +1258,7 @@ struct Tracer {
         if (kEnterInEvent<GRID>) {  // entered by the event kernel: the cell and its neighbour list
             r.ci = c6.z;
             r.cj = c6.w;
+            r.ck = 0;
         } else if (r.mode != RAY_NONE &&
             !Grid<GRID>::begin(a, sh, r, [&](int m, double rho0, double ds) { return segment(r, m, rho0, ds); })) {
             finish(r);  // FILL: tau = 0, no scattered luminosity; WALK: s = 0; PEEL: tau = 0
@@ -1490,7 +1597,8 @@ __global__ void __launch_bounds__(kBlock) SKIRT_TRACE_ATTR traceKernel(const Arg
                     r.mode = RAY_NONE;
                 }
             }
-            if (__ballot(T.npend == kLabsBuf)) T.drain();  // a full buffer: issue the wave's adds
+            // a buffer without room for another step's adds: issue the wave's adds
+            if (__ballot(T.npend > kLabsBuf - kSegsPerStep<GRID>)) T.drain();
         }
     }
     T.drain();
@@ -2225,8 +2333,11 @@ struct SkirtMcrt {
     bool binTree = false;
     // Voronoi grid
     double *dSite = nullptr, *dCellBbox = nullptr;
-    VoronoiNbr* dCellNbr = nullptr;
-    int *dCellNbrOffset = nullptr, *dBlockOffset = nullptr, *dBlockList = nullptr;
+    VorEntry* dVorSlots = nullptr;
+    int *dVorStart = nullptr, *dBlockOffset = nullptr, *dBlockList = nullptr;
+    std::vector<VorEntry> vorSlotsHost;  // host copy: upload_media writes the densities into the headers
+    std::vector<int> vorStartHost;
+    double vorScale = 1.0;
     int vnb = 0;
     // octree leaf map (mapL < 0: walk the node arrays)
     int mapL = -1, mapN = 0;
@@ -2670,40 +2781,52 @@ int skirt_mcrt_upload_grid(SkirtMcrt* c, const SkirtGridDesc* g) {
         std::vector<int> refOf(N);
         for (int m = 0; m < N; m++) refOf[c->devCell[m]] = m;
         std::vector<double> site(3 * (size_t)N), bbox(6 * (size_t)N);
-        std::vector<int> offset(N + 1, 0);
+        // each device cell's block: kVorHead header slots + one slot per neighbour (see VorEntry); the
+        // array is padded by kVorUnroll slots, since a step loads whole groups of entries
+        std::vector<int> start(N + 1, 0);
         for (int d = 0; d < N; d++) {
             const int m = refOf[d];
             const int cnt = g->cell_nbr_offset[m + 1] - g->cell_nbr_offset[m];
             if (cnt < 1) return fail(c, SKIRT_ERR_ARG, "Voronoi cell without neighbours");
-            offset[d + 1] = offset[d] + cnt;
+            start[d + 1] = start[d] + kVorHead + cnt;
         }
-        // kVorUnroll - 1 entries of padding: a step loads whole groups of entries
-        std::vector<VoronoiNbr> nbr((size_t)nnbr + kVorUnroll, VoronoiNbr{0., 0., 0., -1, kVorLast});
+        if ((size_t)start[N] + kVorUnroll >= (size_t)INT32_MAX) return fail(c, SKIRT_ERR_UNSUPPORTED, "Voronoi mesh too large");
+        std::vector<VorEntry> slots((size_t)start[N] + kVorUnroll, VorEntry{0.f, 0.f, 0.f, -1});
+        // offsets in units of the domain's largest half-width: single-precision squares stay in range
+        c->vorScale = 2.0 / std::max({c->gx1 - c->gx0, c->gy1 - c->gy0, c->gz1 - c->gz0});
         for (int d = 0; d < N; d++) {
             const int m = refOf[d];
-            for (int q = 0; q < 3; q++) site[3 * (size_t)d + q] = g->site[3 * (size_t)m + q];
+            const double* sm = g->site + 3 * (size_t)m;
+            for (int q = 0; q < 3; q++) site[3 * (size_t)d + q] = sm[q];
             for (int q = 0; q < 6; q++) bbox[6 * (size_t)d + q] = g->cell_bbox[6 * (size_t)m + q];
-            int o = offset[d];
+            VorEntry* blk = slots.data() + start[d];
+            const double head[4] = {sm[0], sm[1], sm[2], 0.0};  // rho of component 0: set by upload_media
+            std::memcpy(blk, head, sizeof head);
+            const int cnt = g->cell_nbr_offset[m + 1] - g->cell_nbr_offset[m];
+            const int ids[4] = {d, cnt, 0, 0};
+            std::memcpy(blk + 2, ids, sizeof ids);
+            int o = kVorHead;
             for (int q = g->cell_nbr_offset[m]; q < g->cell_nbr_offset[m + 1]; q++, o++) {
                 const int id = g->cell_nbr_list[q];
-                VoronoiNbr& e = nbr[o];
-                e = VoronoiNbr{0., 0., 0., id, 0};
-                if (id >= 0) {
-                    const int did = c->devCell[id];
-                    e.id = did;
-                    e.next = offset[did];
-                    e.x = g->site[3 * (size_t)id]; e.y = g->site[3 * (size_t)id + 1]; e.z = g->site[3 * (size_t)id + 2];
+                VorEntry& e = blk[o];
+                if (id < 0) {
+                    e = VorEntry{0.f, 0.f, 0.f, id};
+                } else {
+                    const double* si = g->site + 3 * (size_t)id;
+                    e = VorEntry{(float)((si[0] - sm[0]) * c->vorScale), (float)((si[1] - sm[1]) * c->vorScale),
+                                 (float)((si[2] - sm[2]) * c->vorScale), start[c->devCell[id]]};
                 }
-                if (q + 1 == g->cell_nbr_offset[m + 1]) e.next |= kVorLast;
             }
         }
+        c->vorSlotsHost = std::move(slots);
         std::vector<int> blocks(std::max(nbl, 1), 0);
         for (int q = 0; q < nbl; q++) blocks[q] = c->devCell[g->block_list[q]];
         int rc;
         if ((rc = upload(c, c->dSite, site.data(), site.size()))) return rc;
         if ((rc = upload(c, c->dCellBbox, bbox.data(), bbox.size()))) return rc;
-        if ((rc = upload(c, c->dCellNbrOffset, offset.data(), offset.size()))) return rc;
-        if ((rc = upload(c, c->dCellNbr, nbr.data(), nbr.size()))) return rc;
+        if ((rc = upload(c, c->dVorStart, start.data(), start.size()))) return rc;
+        if ((rc = upload(c, c->dVorSlots, c->vorSlotsHost.data(), c->vorSlotsHost.size()))) return rc;
+        c->vorStartHost = std::move(start);
         if ((rc = upload(c, c->dBlockOffset, g->block_offset, nb3 + 1))) return rc;
         if ((rc = upload(c, c->dBlockList, blocks.data(), blocks.size()))) return rc;
         if ((rc = upload(c, c->dDevCell, c->devCell.data(), c->devCell.size()))) return rc;
@@ -2741,6 +2864,15 @@ int skirt_mcrt_upload_media(SkirtMcrt* c, const SkirtMediaDesc* m) {
         if ((rc = upload(c, c->dRho, rho.data(), rho.size()))) return rc;
     }
     if ((rc = upload(c, c->dOptics, opt.data(), opt.size()))) return rc;
+    if (c->gridKind == SKIRT_GRID_VORONOI && !c->vorSlotsHost.empty()) {
+        // the density of component 0 in every cell's header, next to its site
+        for (int q = 0; q < m->ncells; q++) {
+            const double v = m->rho[(size_t)q * m->ncomp];
+            std::memcpy(reinterpret_cast<char*>(c->vorSlotsHost.data() + c->vorStartHost[c->devCell[q]]) + 3 * sizeof(double),
+                        &v, sizeof v);
+        }
+        if ((rc = upload(c, c->dVorSlots, c->vorSlotsHost.data(), c->vorSlotsHost.size()))) return rc;
+    }
     return SKIRT_OK;
 }
 
@@ -3149,7 +3281,7 @@ static int runPhase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, uint6
     a.splitDir = c->binTree ? c->dSplitDir : nullptr;
     a.father = c->dFather;
     a.nbrOffset = c->dNbrOffset; a.nbrList = c->dNbrList; a.eps = c->eps; a.search = c->search;
-    a.site = c->dSite; a.cellNbrOffset = c->dCellNbrOffset; a.cellNbr = c->dCellNbr; a.cellBbox = c->dCellBbox;
+    a.site = c->dSite; a.vorStart = c->dVorStart; a.vorSlots = c->dVorSlots; a.vorScale = (float)c->vorScale; a.cellBbox = c->dCellBbox;
     a.devCell = c->dDevCell;
     a.vnb = c->vnb; a.blockOffset = c->dBlockOffset; a.blockList = c->dBlockList;
     const bool bookkeeping = c->gridKind == SKIRT_GRID_OCTREE && c->search == SKIRT_TREE_BOOKKEEPING;
@@ -3445,7 +3577,7 @@ void skirt_mcrt_destroy(SkirtMcrt* c) {
     void* bufs[] = {c->dMesh, c->dBox, c->dFirstChild, c->dSplitDir, c->dFather, c->dCellnumber, c->dNbrOffset, c->dNbrList, c->dTreeT,
                     c->dLeafMap, c->dCellLv, c->dCellCdf, c->dCellLtot, c->dCellNode, c->dEmisVolume, c->dEmisKabs,
                     c->dEmisSigma, c->dEmisMu, c->dEmisTv, c->dEmisPlanck, c->dEmisLambda, c->dEmisDlambda,
-                    c->dEmisScratch, c->dDevCell, c->dSite, c->dCellBbox, c->dCellNbrOffset, c->dCellNbr,
+                    c->dEmisScratch, c->dDevCell, c->dSite, c->dCellBbox, c->dVorStart, c->dVorSlots,
                     c->dBlockOffset, c->dBlockList, c->dRho,
                     c->dOptics, c->dGeomParam, c->dGeomTable, c->dLum, c->dLumtot, c->dCdf, c->dInstr,
                     c->dClaim, c->dStats, c->dError, c->dCtr, c->dPool};

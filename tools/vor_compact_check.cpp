@@ -1,0 +1,227 @@
+// Host check of the compact Voronoi step (float neighbour offsets + exact winner), the arithmetic that
+// Grid<SKIRT_GRID_VORONOI>::step in engine.hip runs: walks random rays through a tessellation twice,
+// once with the reference's step (VoronoiMesh::path, VoronoiMesh.cpp:749-844, double sites) and once with
+// the compact step (interval bounds from float offsets, the exact reference expression for the winner,
+// exact re-evaluation of every possible winner when the bounds cannot separate them), and requires the
+// same cells and bitwise equal segment lengths. Reports how often the exact re-evaluation was needed.
+//   g++ -O2 -std=c++17 -ffp-contract=off -I include tools/vor_compact_check.cpp -L skirt_amd -lskirt_amd \
+//       -Wl,-rpath,$PWD/skirt_amd -o /tmp/vor_compact_check && /tmp/vor_compact_check 100000 20000
+#include <cfloat>
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <random>
+#include <vector>
+
+#include "skirt_host.h"
+
+namespace {
+constexpr double kEps = 1.0 / (1 << 21);  // bound factor: 8x the float rounding of the offsets
+
+struct Mesh {
+    SkirtGridDesc g;
+    std::vector<float> off;  // per list entry: float(site_nbr - site_own), 3 per entry
+};
+
+double wallDist(const SkirtGridDesc& g, int mi, const double r[3], const double k[3]) {
+    switch (mi) {
+    case -1: return (g.extent[0] - r[0]) / k[0];
+    case -2: return (g.extent[3] - r[0]) / k[0];
+    case -3: return (g.extent[1] - r[1]) / k[1];
+    case -4: return (g.extent[4] - r[1]) / k[1];
+    case -5: return (g.extent[2] - r[2]) / k[2];
+    default: return (g.extent[5] - r[2]) / k[2];
+    }
+}
+
+// the reference's distance to the bisector plane with neighbour mi (0 when the ray moves away from it)
+double exactDist(const SkirtGridDesc& g, int m, int mi, const double r[3], const double k[3]) {
+    if (mi < 0) return wallDist(g, mi, r, k);
+    const double* pr = g.site + 3 * (size_t)m;
+    const double* pi = g.site + 3 * (size_t)mi;
+    const double nx = pi[0] - pr[0], ny = pi[1] - pr[1], nz = pi[2] - pr[2];
+    const double ndotk = nx * k[0] + ny * k[1] + nz * k[2];
+    if (!(ndotk > 0)) return 0;
+    const double px = 0.5 * (pi[0] + pr[0]), py = 0.5 * (pi[1] + pr[1]), pz = 0.5 * (pi[2] + pr[2]);
+    return (nx * (px - r[0]) + ny * (py - r[1]) + nz * (pz - r[2])) / ndotk;
+}
+
+// reference step: (exit neighbour or -99, distance)
+int refStep(const SkirtGridDesc& g, int m, const double r[3], const double k[3], double& sq) {
+    sq = DBL_MAX;
+    int mq = -99;
+    for (int q = g.cell_nbr_offset[m]; q < g.cell_nbr_offset[m + 1]; q++) {
+        const int mi = g.cell_nbr_list[q];
+        const double si = exactDist(g, m, mi, r, k);
+        if (si > 0 && si < sq) { sq = si; mq = mi; }
+    }
+    return mq;
+}
+
+// the same bounds in single precision on coordinates scaled by 1/L (the device's f32 variant): every float
+// operation adds at most a few 2^-24 of the sum of absolute terms, covered by kEpsF
+constexpr float kEpsF = 1.0f / (1 << 20);
+float gScale = 1.0f;
+
+// compact step: the same result from float offsets, exact only for the winner (or all possible winners)
+int compactStep(const Mesh& M, int m, const double r[3], const double k[3], double& sq, long& fallbacks) {
+    const SkirtGridDesc& g = M.g;
+    const double* pr = g.site + 3 * (size_t)m;
+    const double D[3] = {pr[0] - r[0], pr[1] - r[1], pr[2] - r[2]};
+    double U = DBL_MAX, L1 = DBL_MAX, L2 = DBL_MAX;
+    int w1 = -99;
+    for (int q = g.cell_nbr_offset[m]; q < g.cell_nbr_offset[m + 1]; q++) {
+        const int mi = g.cell_nbr_list[q];
+        double lo, hi;
+        if (mi < 0) {
+            const double si = wallDist(g, mi, r, k);
+            if (!(si > 0)) continue;
+            lo = hi = si;
+        } else {
+            const double nx = M.off[3 * (size_t)q], ny = M.off[3 * (size_t)q + 1], nz = M.off[3 * (size_t)q + 2];
+            const double den = nx * k[0] + ny * k[1] + nz * k[2];
+            const double eA = kEps * (fabs(nx * k[0]) + fabs(ny * k[1]) + fabs(nz * k[2]));
+            if (den <= -eA) continue;  // moving away for certain: si = 0
+            const double tx = D[0] + 0.5 * nx, ty = D[1] + 0.5 * ny, tz = D[2] + 0.5 * nz;
+            const double num = nx * tx + ny * ty + nz * tz;
+            const double eB = kEps * (fabs(nx * tx) + fabs(ny * ty) + fabs(nz * tz) + 0.5 * (nx * nx + ny * ny + nz * nz));
+            if (den > 2 * eA) {
+                const double inv = 1.0 / den;
+                const double s = num * inv;
+                const double err = 2.0 * (eB + fabs(s) * eA) * inv;
+                lo = s - err;
+                hi = s + err;
+                if (hi <= 0) continue;  // si <= 0 for certain
+            } else {
+                lo = -DBL_MAX;  // the sign of ndotk is uncertain
+                hi = DBL_MAX;
+            }
+        }
+        if (lo > 0 && hi < U) U = hi;
+        if (lo < L1) { L2 = L1; L1 = lo; w1 = mi; }
+        else if (lo < L2) L2 = lo;
+    }
+    if (L1 == DBL_MAX) { sq = DBL_MAX; return -99; }  // no exit for certain
+    if (L2 > U) {  // one possible winner: its exact distance
+        sq = exactDist(g, m, w1, r, k);
+        return w1;
+    }
+    // several possible winners: the reference's rule over them, exactly, in list order
+    fallbacks++;
+    sq = DBL_MAX;
+    int mq = -99;
+    for (int q = g.cell_nbr_offset[m]; q < g.cell_nbr_offset[m + 1]; q++) {
+        const int mi = g.cell_nbr_list[q];
+        const double si = exactDist(g, m, mi, r, k);
+        if (si > 0 && si < sq) { sq = si; mq = mi; }
+    }
+    return mq;
+}
+}  // namespace
+
+static int compactStepF(const Mesh& M, int m, const double r[3], const double k[3], double& sq, long& fallbacks) {
+    const SkirtGridDesc& g = M.g;
+    const double* pr = g.site + 3 * (size_t)m;
+    const float Dx = (float)((pr[0] - r[0]) * gScale), Dy = (float)((pr[1] - r[1]) * gScale),
+                Dz = (float)((pr[2] - r[2]) * gScale);
+    const float kx = (float)k[0], ky = (float)k[1], kz = (float)k[2];
+    float U = FLT_MAX, L1 = FLT_MAX, L2 = FLT_MAX;
+    int w1 = -99;
+    for (int q = g.cell_nbr_offset[m]; q < g.cell_nbr_offset[m + 1]; q++) {
+        const int mi = g.cell_nbr_list[q];
+        float lo, hi;
+        if (mi < 0) {
+            const double si = wallDist(g, mi, r, k);
+            if (!(si > 0)) continue;
+            const float v = (float)(si * gScale);
+            lo = v * (1.0f - kEpsF);
+            hi = v * (1.0f + kEpsF);
+        } else {
+            const float nx = M.off[3 * (size_t)q] * gScale, ny = M.off[3 * (size_t)q + 1] * gScale,
+                        nz = M.off[3 * (size_t)q + 2] * gScale;
+            const float den = nx * kx + ny * ky + nz * kz;
+            const float eA = kEpsF * (fabsf(nx * kx) + fabsf(ny * ky) + fabsf(nz * kz));
+            if (den <= -eA) continue;
+            const float tx = Dx + 0.5f * nx, ty = Dy + 0.5f * ny, tz = Dz + 0.5f * nz;
+            const float num = nx * tx + ny * ty + nz * tz;
+            const float eB = kEpsF * (fabsf(nx * tx) + fabsf(ny * ty) + fabsf(nz * tz) + 0.5f * (nx * nx + ny * ny + nz * nz));
+            if (den > 2 * eA) {
+                const float inv = 1.0f / den;
+                const float s = num * inv;
+                const float err = 2.0f * (eB + fabsf(s) * eA) * inv + fabsf(s) * kEpsF;
+                lo = s - err;
+                hi = s + err;
+                if (hi <= 0) continue;
+            } else {
+                lo = -FLT_MAX;
+                hi = FLT_MAX;
+            }
+        }
+        if (lo > 0 && hi < U) U = hi;
+        if (lo < L1) { L2 = L1; L1 = lo; w1 = mi; }
+        else if (lo < L2) L2 = lo;
+    }
+    if (L1 == FLT_MAX) { sq = DBL_MAX; return -99; }
+    if (L2 > U) {
+        sq = exactDist(g, m, w1, r, k);
+        return w1;
+    }
+    fallbacks++;
+    return refStep(g, m, r, k, sq);
+}
+
+int main(int argc, char** argv) {
+    const int N = argc > 1 ? atoi(argv[1]) : 100000;
+    const int R = argc > 2 ? atoi(argv[2]) : 20000;
+    std::mt19937_64 rng(4357);
+    std::uniform_real_distribution<double> U01(0.0, 1.0);
+    const double L = 1.5428387e19;  // 500 pc in m
+    // Plummer-distributed sites (c = 100 pc) inside the box, like VoronoiDustGrid's DustDensity sites
+    std::vector<double> sites;
+    while ((int)sites.size() < 3 * N) {
+        const double u = U01(rng);
+        const double rr = 0.2 * L / sqrt(pow(u, -2.0 / 3.0) - 1.0);
+        const double ct = 2 * U01(rng) - 1, ph = 2 * M_PI * U01(rng), st = sqrt(1 - ct * ct);
+        const double x = rr * st * cos(ph), y = rr * st * sin(ph), z = rr * ct;
+        if (fabs(x) < L && fabs(y) < L && fabs(z) < L) { sites.push_back(x); sites.push_back(y); sites.push_back(z); }
+    }
+    const double ext[6] = {-L, -L, -L, L, L, L};
+    gScale = (float)(1.0 / L);
+    const bool f32 = argc > 3 && argv[3][0] == 'f';
+    SkirtVoronoi* v = skirt_host_voronoi_build(sites.data(), N, ext);
+    if (!v) { fprintf(stderr, "voronoi: %s\n", skirt_sim_error()); return 1; }
+    Mesh M{};
+    skirt_host_voronoi_describe(v, &M.g);
+    const SkirtGridDesc& g = M.g;
+    const int nn = g.cell_nbr_offset[N];
+    M.off.assign(3 * (size_t)nn, 0.f);
+    for (int m = 0; m < N; m++)
+        for (int q = g.cell_nbr_offset[m]; q < g.cell_nbr_offset[m + 1]; q++) {
+            const int mi = g.cell_nbr_list[q];
+            if (mi < 0) continue;
+            for (int d = 0; d < 3; d++) M.off[3 * (size_t)q + d] = (float)(g.site[3 * (size_t)mi + d] - g.site[3 * (size_t)m + d]);
+        }
+    long steps = 0, fallbacks = 0, mismatches = 0;
+    for (int i = 0; i < R; i++) {
+        // a random start site's cell and an isotropic direction (positions start at the site)
+        int m = (int)(U01(rng) * N);
+        double r[3] = {g.site[3 * (size_t)m], g.site[3 * (size_t)m + 1], g.site[3 * (size_t)m + 2]};
+        const double ct = 2 * U01(rng) - 1, ph = 2 * M_PI * U01(rng), st = sqrt(1 - ct * ct);
+        const double k[3] = {st * cos(ph), st * sin(ph), ct};
+        for (int s = 0; s < 100000 && m >= 0; s++) {
+            double sa, sb;
+            const int a = refStep(g, m, r, k, sa);
+            const int b = f32 ? compactStepF(M, m, r, k, sb, fallbacks) : compactStep(M, m, r, k, sb, fallbacks);
+            steps++;
+            if (a != b || sa != sb) { mismatches++; break; }
+            if (a == -99) break;
+            for (int d = 0; d < 3; d++) r[d] += (sa + g.eps) * k[d];
+            m = a;
+        }
+    }
+    printf("%s: sites %d, rays %d, steps %ld, exact re-evaluations %ld (%.3g per step), mismatches %ld\n", f32 ? "f32 bounds" : "f64 bounds", N, R, steps,
+           fallbacks, (double)fallbacks / steps, mismatches);
+    skirt_host_voronoi_free(v);
+    return mismatches ? 1 : 0;
+}
