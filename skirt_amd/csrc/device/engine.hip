@@ -70,8 +70,10 @@ constexpr int kPollRing = 3;       // copies in flight per half (the host reads 
 #ifndef SKIRT_TRACE_ATTR
 #define SKIRT_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(3)))
 #endif
+// the event kernel at 2 waves per SIMD: the Voronoi instantiation (cellIndex on the grid entry of every
+// queued ray) would otherwise take 256 VGPRs + AGPRs and run at 1
 #ifndef SKIRT_EVENT_ATTR
-#define SKIRT_EVENT_ATTR
+#define SKIRT_EVENT_ATTR __attribute__((amdgpu_waves_per_eu(2)))
 #endif
 
 // ------------------------------------------------------------------ descriptors
@@ -1164,6 +1166,40 @@ struct Tracer {
         const int lane = threadIdx.x & 63;
         const int wbase = threadIdx.x - lane;
         const int j = lane & (kLabsBuf - 1);
+#ifdef SKIRT_EXPERIMENT_LINE_COUNT
+        // tuning experiment only (the counts replace the request and lane-slot statistics): the distinct
+        // 64-byte lines and distinct addresses among the wave's buffered adds, i.e. what a perfect
+        // per-wave merge of the buffer would issue
+        {
+            unsigned mine[kLabsBuf];
+            bool dupLine[kLabsBuf], dupAddr[kLabsBuf];
+#pragma unroll
+            for (int i = 0; i < kLabsBuf; i++) {
+                mine[i] = pendIdx[i * kBlock + threadIdx.x];
+                dupLine[i] = dupAddr[i] = false;
+            }
+            for (int l2 = 0; l2 < 64; l2++) {
+                const int n2 = __shfl(npend, l2);
+                for (int s2 = 0; s2 < n2; s2++) {
+                    const unsigned o = pendIdx[s2 * kBlock + wbase + l2];
+#pragma unroll
+                    for (int i = 0; i < kLabsBuf; i++) {
+                        const bool earlier = l2 < lane || (l2 == lane && s2 < i);
+                        if (earlier && (o >> 3) == (mine[i] >> 3)) dupLine[i] = true;
+                        if (earlier && o == mine[i]) dupAddr[i] = true;
+                    }
+                }
+            }
+            unsigned nl = 0, na = 0;
+#pragma unroll
+            for (int i = 0; i < kLabsBuf; i++) {
+                if (i < npend && !dupLine[i]) nl++;
+                if (i < npend && !dupAddr[i]) na++;
+            }
+            for (int off = 32; off > 0; off >>= 1) { nl += __shfl_xor(nl, off); na += __shfl_xor(na, off); }
+            if (lane == 0) { requests += nl; laneSlots += na; }
+        }
+#endif
 #pragma unroll
         for (int i = 0; i < kLabsBuf; i++) {
             const int src = G * i + lane / kLabsBuf;
@@ -1175,7 +1211,9 @@ struct Tracer {
             const unsigned line = (unsigned)(reinterpret_cast<size_t>(a.labs + idx) >> 6);
             const unsigned prev = __shfl(line, lane - 1);
             const unsigned long long starts = __ballot(j < n && (j == 0 || prev != line));
+#ifndef SKIRT_EXPERIMENT_LINE_COUNT
             if (lane == 0) requests += (unsigned)__popcll(starts);
+#endif
 #ifdef SKIRT_EXPERIMENT_NO_LABS_ATOMICS  // tuning experiment only: the cost of the Labs atomics
             if (j < n && pendVal[q] == -1.0) atomicAddF64(a.labs + idx, pendVal[q]);
 #else
@@ -1590,7 +1628,9 @@ __global__ void __launch_bounds__(kBlock) SKIRT_TRACE_ATTR traceKernel(const Arg
 #pragma unroll 1
         for (int it = 0; it < kStepsPerPull; it++) {
             if (__ballot(r.mode != RAY_NONE) == 0) break;
+#ifndef SKIRT_EXPERIMENT_LINE_COUNT
             T.laneSlots++;
+#endif
             if (r.mode != RAY_NONE) {
                 if (!Grid<GRID>::step(a, sh, r, [&](int m, double rho0, double ds) { return T.segment(r, m, rho0, ds); })) {
                     T.finish(r);
