@@ -353,3 +353,32 @@ def test_many_wavelengths_match_oracle_same_streams(copies, monkeypatch):
     np.testing.assert_allclose(seds, orc.seds[0], rtol=1e-8, atol=1e-300)
     np.testing.assert_allclose(frames.sum(axis=2), orc.frames[0].sum(axis=2), rtol=1e-8, atol=1e-300)
     assert_parity(frames, orc.frames[0], 1e-8, DUST_OUTLIERS, "frames")
+
+
+BENCH = os.path.join(os.path.dirname(GOLD), "..", "benchmarks")
+
+
+@pytest.mark.parametrize("config,packages", [("c2_cart64", 50), ("c3_oct128", 20), ("c4_vor1e5", 20),
+                                             ("c5_oct128_sa", 4)])
+def test_benchmark_models_match_oracle_same_streams(config, packages):
+    """The BASELINE configurations at their full grid sizes (C2 64^3 Cartesian, C3 622,490-leaf octree, C4
+    1e5-site Voronoi, C5 = C3 with self-absorption and dust emission), with few packets per wavelength:
+    engine = oracle on the same Philox streams, every phase the model has."""
+    path = os.path.join(BENCH, config + ".ski")
+    sim = S.Simulation(path, packages=packages)
+    sim.attach(0)
+    sim.run_stellar()
+    sim.run_dust()
+    sim.fetch()
+    orc = O.run(path, rng=O.RNG_PHILOX, threads=16, packages=packages, phases=O.PHASES_ALL)
+    dust = orc.labs_dust is not None or config == "c5_oct128_sa"
+    rtol = 1e-8 if dust else 1e-9
+    np.testing.assert_allclose(sim.labs().sum(axis=0), orc.labs.sum(axis=0), rtol=1e-9)
+    assert_parity(sim.labs(), orc.labs, 1e-9, STELLAR_OUTLIERS, "labs")
+    if orc.labs_dust is not None:
+        np.testing.assert_allclose(sim.selfabs_totals(), orc.labs_dust_totals, rtol=1e-8)
+        assert_parity(sim.labs_dust(), orc.labs_dust, 1e-8, DUST_OUTLIERS, "labs_dust")
+    frames, seds = sim.instrument(0)
+    np.testing.assert_allclose(seds, orc.seds[0], rtol=rtol, atol=1e-300)
+    np.testing.assert_allclose(frames.sum(axis=2), orc.frames[0].sum(axis=2), rtol=rtol, atol=1e-300)
+    assert_parity(frames, orc.frames[0], rtol, DUST_OUTLIERS if dust else STELLAR_OUTLIERS, "frames")
