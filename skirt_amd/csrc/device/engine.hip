@@ -67,6 +67,12 @@ constexpr int kPollRing = 3;       // copies in flight per half (the host reads 
 // 3 waves per SIMD, i.e. at most 168 VGPRs (the grid entry on the pull path would otherwise take the
 // octree kernel to 175 and 2 waves; C3 1.91e8 -> 2.15e8 pkt/s at 3). The Voronoi step, at 4 entries per
 // load round, spills 60 B/lane at 3 waves and still runs fastest there (C4, profiles/r02_sweep_vor.txt).
+// leaf-map step: check the estimated finest cell against the found leaf's faces instead of the finest
+// cell's own split coordinates (see LeafMapGrid::step; 0 restores the finest-cell check: C3 2.154e8 ->
+// 2.162e8, C5 1.071e8 -> 1.091e8 pkt/s with 1)
+#ifndef SKIRT_LEAF_CHECK_FACES
+#define SKIRT_LEAF_CHECK_FACES 1
+#endif
 #ifndef SKIRT_TRACE_ATTR
 #define SKIRT_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(3)))
 #endif
@@ -886,18 +892,42 @@ struct LeafMapGrid {
         double z = r.z + (ds + a.eps) * r.dz;
         // the next leaf's entry is requested first; the segment's own work (optical depth, absorption)
         // runs while the load is in flight
+#if SKIRT_LEAF_CHECK_FACES
+        // the entry of the estimated finest cell; its leaf is the right one when the leaf's own faces
+        // (read anyway) contain the point, since T is monotone: then the exact finest cell lies in it too
+        const int N = a.mapN;
+        int fx = estimate(N, a.mapX0, a.mapInvX, x);
+        int fy = estimate(N, a.mapY0, a.mapInvY, y);
+        int fz = estimate(N, a.mapZ0, a.mapInvZ, z);
+        const int4 raw = *reinterpret_cast<const int4*>(a.leafMap + leafIndex(N, fx, fy, fz));
+#else
         int fx, fy, fz;
         const int4 raw = fetch(a, sh, x, y, z, fx, fy, fz);
+#endif
         if (!seg(r.cj, r.rho0, ds)) return false;
         if (!inside(a, x, y, z)) return false;  // no neighbour and no root descent contains it
         LeafEntry e = decode(raw);
         int lx, ly, lz;
         shifts(a, e.cl, lx, ly, lz);
-        const int jx = (fx >> lx) << lx, jy = (fy >> ly) << ly, jz = (fz >> lz) << lz;
+        int jx = (fx >> lx) << lx, jy = (fy >> ly) << ly, jz = (fz >> lz) << lz;
         // the new leaf's six faces in one LDS round trip: the lower ones decide whether the exit point
         // lies on a face, the ones ahead of the ray are the next step's exit planes
-        const double lox = tx[jx], loy = ty[jy], loz = tz[jz];
-        const double hix = tx[jx + (1 << lx)], hiy = ty[jy + (1 << ly)], hiz = tz[jz + (1 << lz)];
+        double lox = tx[jx], loy = ty[jy], loz = tz[jz];
+        double hix = tx[jx + (1 << lx)], hiy = ty[jy + (1 << ly)], hiz = tz[jz + (1 << lz)];
+#if SKIRT_LEAF_CHECK_FACES
+        if (!(x >= lox && x < hix && y >= loy && y < hiy && z >= loz && z < hiz)) {
+            // the estimate fell into a neighbouring leaf (or the point is on the grid's far faces): the
+            // exact finest cell, its entry and its leaf's faces
+            fx = correct(tx, N, fx, x);
+            fy = correct(ty, N, fy, y);
+            fz = correct(tz, N, fz, z);
+            e = decode(*reinterpret_cast<const int4*>(a.leafMap + leafIndex(N, fx, fy, fz)));
+            shifts(a, e.cl, lx, ly, lz);
+            jx = (fx >> lx) << lx; jy = (fy >> ly) << ly; jz = (fz >> lz) << lz;
+            lox = tx[jx]; loy = ty[jy]; loz = tz[jz];
+            hix = tx[jx + (1 << lx)]; hiy = ty[jy + (1 << ly)]; hiz = tz[jz + (1 << lz)];
+        }
+#endif
         r.x = x; r.y = y; r.z = z;
         if (e.node == r.ci || x == lox || y == loy || z == loz) {
             // on a face, or not out of the current leaf: the reference's own search decides

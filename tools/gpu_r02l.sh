@@ -1,0 +1,9 @@
+# round 2: the BASELINE models at full grid size against the oracle on the same streams
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+export SKIRT_PARITY_LOG=$PWD/gpurun_out/parity_outliers_bench.jsonl
+rm -f $SKIRT_PARITY_LOG
+run() { local name=$1 t=$2; shift 2; echo "== $name"; timeout -k 10 $t "$@" > gpurun_out/$name.log 2>&1; local rc=$?; echo "rc=$rc"; tail -${TAILN:-1} gpurun_out/$name.log | cut -c1-200; return $rc; }
+TAILN=20 run pytest_bench_models 900 python -u -m pytest tests/test_gpu_parity.py -m gpu -k benchmark_models -v -s --timeout 600 --timeout-method thread
