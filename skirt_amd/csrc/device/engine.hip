@@ -98,23 +98,22 @@ enum State : int { S_NEW = 0, S_FILL = 2, S_WALK = 3 };
 // peel-off categories (which FullInstrument arrays a detection adds to, FullInstrument.cpp:115-171)
 enum PeelCat : unsigned { CAT_STAR_DIRECT = 0, CAT_STAR_SCATTERED = 1, CAT_DUST_DIRECT = 2, CAT_DUST_SCATTERED = 3 };
 
-// one queued ray, 112 bytes = 7 x 16-byte chunks, written by the event kernel with the reciprocal
-// direction computed. The trace kernel enters the grid when it pulls the ray (the path before the grid,
-// the first cell): that lookup then overlaps with the other lanes' steps instead of stalling the event
-// kernel, whose waves are few (2 per SIMD) and long. Voronoi rays are entered by the event kernel
-// (kEnterInEvent): s0 then holds the path length before the grid, ci/cj the first cell.
+// one queued ray, 80 bytes = 5 x 16-byte chunks, written by the event kernel. The trace kernel enters the
+// grid when it pulls the ray (the path before the grid, the first cell): that lookup then overlaps with the
+// other lanes' steps instead of stalling the event kernel, whose waves are few (2 per SIMD) and long.
+// Voronoi rays are entered by the event kernel (kEnterInEvent): s0 then holds the path length before the
+// grid, ci/cj the first cell. The reciprocal direction is recomputed by the trace kernel (three divisions
+// per ray, against 24 bytes more per record written and read).
 struct __attribute__((aligned(16))) RayRec {
     double x, y, z;        // c0-c1: start point
     double dx, dy, dz;     // c1-c2: direction
-    double ix, iy, iz;     // c3-c4: 1/direction (0 where |k| <= 1e-15: that axis is never crossed)
-    double s0;             // c4: path length before the grid (Voronoi) or 0; a finished PEEL ray: optical depth
-    double unused;         // c5
-    double param;          // c5: FILL: packet luminosity L; WALK: optical depth to reach; PEEL: peel-off L
-    int idx;               // c6: FILL/WALK: slot; PEEL: frame pixel (-1: none)
-    unsigned flags;        // c6: mode | cat << 2 | instrument << 4 | scattering level << 10 | ell << 18
-    int ci, cj;            // c6: Voronoi: first cell and where its neighbour list starts
+    double s0;             // c3: path length before the grid (Voronoi) or 0
+    double param;          // c3: FILL: packet luminosity L; WALK: optical depth to reach; PEEL: peel-off L
+    int idx;               // c4: FILL/WALK: slot; PEEL: detection record
+    unsigned flags;        // c4: mode | cat << 2 | instrument << 4 | scattering level << 10 | ell << 18
+    int ci, cj;            // c4: Voronoi: first cell and where its block starts
 };
-static_assert(sizeof(RayRec) == 112, "ray record layout");
+static_assert(sizeof(RayRec) == 80, "ray record layout");
 template <int GRID>
 constexpr bool kEnterInEvent = GRID == SKIRT_GRID_VORONOI;
 // most segments one Grid<GRID>::step adds (the Voronoi step may add a pending and a new segment)
@@ -1306,23 +1305,26 @@ struct Tracer {
     // it, m = -1) and the first cell (DustGrid::path); an empty path finishes the ray at once
     __device__ __forceinline__ void load(Ray& r, unsigned id) {
         const double2* c = reinterpret_cast<const double2*>(a.rays + id);
-        const double2 c0 = c[0], c1 = c[1], c2 = c[2], c3 = c[3], c4 = c[4], c5 = c[5];
-        const int4 c6 = reinterpret_cast<const int4*>(c)[6];
+        const double2 c0 = c[0], c1 = c[1], c2 = c[2], c3 = c[3];
+        const int4 c6 = reinterpret_cast<const int4*>(c)[4];
         r.id = id;
         r.x = c0.x; r.y = c0.y; r.z = c1.x;
         r.dx = c1.y; r.dy = c2.x; r.dz = c2.y;
-        r.ix = c3.x; r.iy = c3.y; r.iz = c4.x;
-        r.param = c5.y;
+        // 1/direction, 0 where |k| <= 1e-15 (that axis is never crossed), as the event kernel computed it
+        r.ix = (fabs(r.dx) > 1e-15) ? 1.0 / r.dx : 0.0;
+        r.iy = (fabs(r.dy) > 1e-15) ? 1.0 / r.dy : 0.0;
+        r.iz = (fabs(r.dz) > 1e-15) ? 1.0 / r.dz : 0.0;
+        r.param = c3.y;
         r.idx = c6.x;
         r.flags = (unsigned)c6.y;
         r.mode = rayMode(r.flags);
         r.ell = rayEll(r.flags);
         r.tau = 0;
-        r.s = c4.y;
+        r.s = c3.x;
         r.kext = sh.kext[r.ell];
         // FILL: f1 = exp(-tau) = 1, f2 = scattered luminosity; WALK: tau and s at the last segment end
         r.f1 = (r.mode == RAY_FILL) ? 1.0 : 0.0;
-        r.f2 = (r.mode == RAY_WALK) ? c4.y : 0.0;
+        r.f2 = (r.mode == RAY_WALK) ? c3.x : 0.0;
         if (kEnterInEvent<GRID>) {  // entered by the event kernel: the cell and its neighbour list
             r.ci = c6.z;
             r.cj = c6.w;
@@ -1775,17 +1777,15 @@ struct Events {
                 a.resA[idx] = 0.0;  // FILL: tau = 0 (and no scattered luminosity); WALK: s = 0
                 if (!ONECOMP) a.resB[idx] = 0.0;
             }
-            dst[6] = make_int4(idx, (int)RAY_NONE, 0, 0);
+            dst[4] = make_int4(idx, (int)RAY_NONE, 0, 0);
             return;
         }
         double2* d2 = reinterpret_cast<double2*>(dst);
         d2[0] = make_double2(r.x, r.y);
         d2[1] = make_double2(r.z, dx);
         d2[2] = make_double2(dy, dz);
-        d2[3] = make_double2(r.ix, r.iy);
-        d2[4] = make_double2(r.iz, r.s);
-        d2[5] = make_double2(0.0, prm);
-        dst[6] = make_int4(idx, (int)flags, r.ci, r.cj);
+        d2[3] = make_double2(r.s, prm);
+        dst[4] = make_int4(idx, (int)flags, r.ci, r.cj);
     }
 
     __device__ __forceinline__ void load(int s, Packet& p) const {
