@@ -151,6 +151,10 @@ struct alignas(16) VorEntry {
     int next;
 };
 constexpr int kVorHead = 3;  // header slots
+// FMA contraction in the Voronoi step's single-precision bounds (C4 5.33e7 -> 5.45e7 pkt/s)
+#ifndef SKIRT_VOR_CONTRACT
+#define SKIRT_VOR_CONTRACT 1
+#endif
 #ifndef SKIRT_VOR_UNROLL
 #define SKIRT_VOR_UNROLL 4
 #endif
@@ -1058,6 +1062,52 @@ struct Grid<SKIRT_GRID_VORONOI> {
         // exits; L1 < L2: the two least lower bounds of the possible exits, w1: the first one's `next`
         float U = FLT_MAX, L1 = FLT_MAX, L2 = FLT_MAX;
         int w1 = 0;
+        // the bounds of one entry's plane distance; lo = FLT_MAX: certainly no exit
+        auto bound = [&](const VorEntry& en, float& lo, float& hi) {
+            lo = FLT_MAX; hi = 0.f;
+            const int nxt = en.next;
+            if (nxt < 0) {
+                const double si = wallDist(a, r, nxt);
+                if (si > 0) {
+                    const float v = (float)(si * sc);
+                    lo = v * (1.0f - kVorEpsF);
+                    hi = v * (1.0f + kVorEpsF);
+                }
+                return;
+            }
+            {
+#if SKIRT_VOR_CONTRACT
+            // FMA contraction in the bounds only: a fused operation rounds once where the bound counts
+            // two roundings, so the intervals stay valid
+#pragma clang fp contract(fast)
+#endif
+            const float nx = en.ox, ny = en.oy, nz = en.oz;
+            const float px = nx * fkx, py = ny * fky, pz = nz * fkz;
+            const float den = px + py + pz;
+            const float eA = kVorEpsF * (fabsf(px) + fabsf(py) + fabsf(pz));
+            if (den > -eA) {  // else moving away from this plane for certain: no exit
+                const float tx = Dx + 0.5f * nx, ty = Dy + 0.5f * ny, tz = Dz + 0.5f * nz;
+                const float qx = nx * tx, qy = ny * ty, qz = nz * tz;
+                const float num = qx + qy + qz;
+                const float eB = kVorEpsF * (fabsf(qx) + fabsf(qy) + fabsf(qz) + 0.5f * (nx * nx + ny * ny + nz * nz));
+                if (den > 2.0f * eA) {
+                    const float inv = __builtin_amdgcn_rcpf(den);
+                    const float sa = num * inv;
+                    const float err = 2.0f * (eB + fabsf(sa) * eA) * inv + fabsf(sa) * kVorEpsF;
+                    if (sa + err > 0.f) { lo = sa - err; hi = sa + err; }
+                } else {
+                    lo = -FLT_MAX; hi = FLT_MAX;  // the sign of n.k is uncertain
+                }
+            }
+            }
+        };
+        auto update = [&](int nxt, float lo, float hi) {
+            if (lo != FLT_MAX) {
+                if (lo > 0.f && hi < U) U = hi;
+                if (lo < L1) { L2 = L1; L1 = lo; w1 = nxt; }
+                else if (lo < L2) L2 = lo;
+            }
+        };
         for (int q0 = 0; q0 < cnt; q0 += kVorUnroll) {
             if (q0) {
 #pragma unroll
@@ -1065,42 +1115,9 @@ struct Grid<SKIRT_GRID_VORONOI> {
             }
 #pragma unroll
             for (int u = 0; u < kVorUnroll; u++) {
-                const int nxt = e[u].next;
                 float lo = FLT_MAX, hi = 0.f;
-                if (q0 + u >= cnt) {
-                    // past the list: no exit
-                } else if (nxt < 0) {
-                    const double si = wallDist(a, r, nxt);
-                    if (si > 0) {
-                        const float v = (float)(si * sc);
-                        lo = v * (1.0f - kVorEpsF);
-                        hi = v * (1.0f + kVorEpsF);
-                    }
-                } else {
-                    const float nx = e[u].ox, ny = e[u].oy, nz = e[u].oz;
-                    const float px = nx * fkx, py = ny * fky, pz = nz * fkz;
-                    const float den = px + py + pz;
-                    const float eA = kVorEpsF * (fabsf(px) + fabsf(py) + fabsf(pz));
-                    if (den > -eA) {  // else moving away from this plane for certain: no exit
-                        const float tx = Dx + 0.5f * nx, ty = Dy + 0.5f * ny, tz = Dz + 0.5f * nz;
-                        const float qx = nx * tx, qy = ny * ty, qz = nz * tz;
-                        const float num = qx + qy + qz;
-                        const float eB = kVorEpsF * (fabsf(qx) + fabsf(qy) + fabsf(qz) + 0.5f * (nx * nx + ny * ny + nz * nz));
-                        if (den > 2.0f * eA) {
-                            const float inv = __builtin_amdgcn_rcpf(den);
-                            const float sa = num * inv;
-                            const float err = 2.0f * (eB + fabsf(sa) * eA) * inv + fabsf(sa) * kVorEpsF;
-                            if (sa + err > 0.f) { lo = sa - err; hi = sa + err; }
-                        } else {
-                            lo = -FLT_MAX; hi = FLT_MAX;  // the sign of n.k is uncertain
-                        }
-                    }
-                }
-                if (lo != FLT_MAX) {
-                    if (lo > 0.f && hi < U) U = hi;
-                    if (lo < L1) { L2 = L1; L1 = lo; w1 = nxt; }
-                    else if (lo < L2) L2 = lo;
-                }
+                if (q0 + u < cnt) bound(e[u], lo, hi);
+                update(e[u].next, lo, hi);
             }
         }
         if (L1 != FLT_MAX && L2 > U) {
