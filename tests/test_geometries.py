@@ -1,7 +1,7 @@
 """ExpDiskGeometry (SKIRTcore/ExpDiskGeometry.cpp, SepAxGeometry::generatePosition,
 SpecialFunctions::LambertW1) in the host model and the oracle.
 
-No reference fixture uses this geometry (the reference binary cannot be run here), so it is parity
+No reference fixture uses this geometry (no reference binary is available here to write one), so it is parity
 unpinned against the reference itself; these tests pin the restatement to its own defining properties:
 the density formula and its normalization (setupSelfBefore's rho0 makes the density integrate to 1),
 and the random positions (randomR by LambertW1 inversion, randomz, the truncations) distributed as

@@ -3,8 +3,9 @@
 The reference fixtures cover the OctTreeDustGrid with centre splits and the Neighbor search
 (pan_oct). Its other tree grids -- BinTreeDustGrid (the k-d tree, Alternating or Barycenter split
 directions, BinTreeDustGrid.cpp, BinTreeNode.cpp, BaryBinTreeNode.cpp), barycentric octrees
-(BaryOctTreeNode.cpp), the TopDown and Bookkeeping searches -- have no reference outputs here (the reference binary
-cannot be built or run in this repository), so these variants swap only the <dustGrid> element of a
+(BaryOctTreeNode.cpp), the TopDown and Bookkeeping searches -- have no reference outputs here (the fixtures came from the
+survey's reference build, which this repository may not rebuild: it needs the reference's own qmake/moc
+build system), so these variants swap only the <dustGrid> element of a
 pinned model and are checked against the pinned octree walk (geometric equivalence) and against the
 oracle on the same random streams.
 """
