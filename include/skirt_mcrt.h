@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define SKIRT_MCRT_ABI_VERSION 6
+#define SKIRT_MCRT_ABI_VERSION 7
 
 enum {
     SKIRT_OK = 0,
@@ -162,6 +162,9 @@ typedef struct {
     double scatt_bias;
     int store_absorption;       /* DustSystem::storeabsorptionrates() */
     int has_dust;
+    int continuous_scattering;  /* MonteCarloSimulation::continuousScattering: peel-offs from every dust
+                                   segment of each path (continuouspeeloffscattering, MonteCarloSimulation.cpp:
+                                   367-434) instead of at the interaction points */
 } SkirtPhaseParams;
 
 typedef struct {

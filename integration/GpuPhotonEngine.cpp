@@ -102,11 +102,13 @@ void GpuPhotonEngine::check(int rc) const
 
 ////////////////////////////////////////////////////////////////////
 
-void GpuPhotonEngine::setPhaseParams(double minWeightReduction, int minScattEvents, double scattBias)
+void GpuPhotonEngine::setPhaseParams(double minWeightReduction, int minScattEvents, double scattBias,
+                                     bool continuousScattering)
 {
     _params.min_weight_reduction = minWeightReduction;
     _params.min_scatt_events = minScattEvents;
     _params.scatt_bias = scattBias;
+    _params.continuous_scattering = continuousScattering ? 1 : 0;
 }
 
 ////////////////////////////////////////////////////////////////////

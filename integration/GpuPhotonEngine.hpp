@@ -43,7 +43,7 @@ public:
     GpuPhotonEngine& operator=(const GpuPhotonEngine&) = delete;
 
     // The MonteCarloSimulation properties of the photon loop (MonteCarloSimulation.cpp:31-35)
-    void setPhaseParams(double minWeightReduction, int minScattEvents, double scattBias);
+    void setPhaseParams(double minWeightReduction, int minScattEvents, double scattBias, bool continuousScattering);
 
     // dostellaremissionchunk over this process's share of every wavelength (rank of size, as the
     // reference's IdenticalAssigner hands out chunks); the absorbed stellar luminosities go into the dust

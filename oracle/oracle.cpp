@@ -559,6 +559,54 @@ public:
         }
     }
 
+    // MonteCarloSimulation::continuouspeeloffscattering (MonteCarloSimulation.cpp:367-434), unpolarized:
+    // from a uniformly drawn point of every path segment with scattering dust, a peel-off toward every
+    // instrument weighted by the luminosity scattered in the segment
+    void continuousPeelOff(Tallies& t, Rng& rng, const Packet& pp, const Path& p, Path& tmp) const {
+        const int Ncomp = M.ncomp();
+        const int ell = pp.ell;
+        double wv[16];
+        const int N = (int)p.v.size();
+        for (int n = 0; n < N; n++) {
+            const int m = p.v[n].m;
+            if (m == -1) continue;
+            double ksca = 0.0, kext = 0.0;
+            for (int h = 0; h < Ncomp; h++) {
+                const double rho = M.rho[(size_t)m * Ncomp + h];
+                wv[h] = rho * M.dust[h].mix.ksca[ell];
+                ksca += rho * M.dust[h].mix.ksca[ell];
+                kext += rho * M.dust[h].mix.kext[ell];
+            }
+            if (!(ksca > 0.0)) continue;
+            for (int h = 0; h < Ncomp; h++) wv[h] /= ksca;
+            const double albedo = ksca / kext;
+            const double tau0 = (n == 0) ? 0.0 : p.v[n - 1].tau;
+            const double dtau = p.v[n].dtau;
+            const double s0 = (n == 0) ? 0.0 : p.v[n - 1].s;
+            const double ds = p.v[n].ds;
+            const double factorm = albedo * exp(-tau0) * (-expm1(-dtau));
+            const double s = s0 + rng.uniform() * ds;
+            const Vec3 rnew{pp.r.x + s * pp.k.x, pp.r.y + s * pp.k.y, pp.r.z + s * pp.k.z};
+            for (size_t i = 0; i < M.instruments.size(); i++) {
+                const Instrument& ins = M.instruments[i];
+                double I = 0;
+                for (int h = 0; h < Ncomp; h++) {
+                    const double cosalpha = pp.k.x * ins.kobs[0] + pp.k.y * ins.kobs[1] + pp.k.z * ins.kobs[2];
+                    const double g = M.dust[h].mix.g[ell];
+                    const double tt = 1.0 + g * g - 2 * g * cosalpha;
+                    const double w = wv[h] * ((1.0 - g) * (1.0 + g) / sqrt(tt * tt * tt));
+                    I += w * 1.0;
+                }
+                Packet ppp = pp;  // PhotonPackage::launchScatteringPeelOff(pp, bfrnew, bfkobs, factorm*I)
+                ppp.L = pp.L * (factorm * I);
+                ppp.r = rnew;
+                ppp.k = {ins.kobs[0], ins.kobs[1], ins.kobs[2]};
+                ppp.nscatt = pp.nscatt + 1;
+                detect(t, (int)i, ppp, tmp);
+            }
+        }
+    }
+
     // the photon life cycle after launch: MonteCarloSimulation.cpp:283-293
     void lifeCycle(Tallies& t, Rng& rng, Packet& pp, double Lthreshold, bool peel, bool store,
                    std::vector<double>* labs, Path& p, Path& tmp) const {
@@ -580,6 +628,7 @@ public:
             double taupath = p.v.empty() ? 0 : p.v.back().tau;
             if (taupath < 0.0 || std::isnan(taupath) || std::isinf(taupath))
                 throw std::runtime_error("the optical depth along the path is not a positive number");
+            if (peel && M.continuousScattering) continuousPeelOff(t, rng, pp, p, tmp);
             // simulateescapeandabsorption
             double L = pp.L;
             if (Ncomp == 1) {
@@ -654,8 +703,9 @@ public:
                 }
                 pp.r = {pp.r.x + s * pp.k.x, pp.r.y + s * pp.k.y, pp.r.z + s * pp.k.z};
             }
-            // peeloffscattering (MonteCarloSimulation.cpp:319-363), unpolarized
-            if (peel) {
+            // peeloffscattering (MonteCarloSimulation.cpp:319-363), unpolarized; replaced by the continuous
+            // peel-off along the path when continuousScattering is on (:289-291)
+            if (peel && !M.continuousScattering) {
                 double wv[16];
                 bool ok = true;
                 if (Ncomp == 1) wv[0] = 1.0;

@@ -114,6 +114,17 @@ struct __attribute__((aligned(16))) RayRec {
     int ci, cj;            // c4: Voronoi: first cell and where its block starts
 };
 static_assert(sizeof(RayRec) == 80, "ray record layout");
+
+// continuous scattering (MonteCarloSimulation::continuouspeeloffscattering): the dust segments of a FILL
+// ray's path as DustGridPath holds them -- where the segment starts along the path (s, tau) and its
+// lengths (ds, dtau) -- recorded by the trace kernel for the peel-off kernel, at most kPathCap per path
+struct PathRec {
+    double s0, ds, tau0, dtau;
+    int m, pad;
+};
+constexpr int kPathCap = 2048;
+constexpr int kContSlots = 1 << 15;  // packet slots in flight with continuous scattering (ray queue sizing)
+enum ErrorBits : unsigned { ERR_TAU = 1u, ERR_PATH_CAP = 2u, ERR_QUEUE = 4u };
 template <int GRID>
 constexpr bool kEnterInEvent = GRID == SKIRT_GRID_VORONOI;
 // most segments one Grid<GRID>::step adds (the Voronoi step may add a pending and a new segment)
@@ -250,6 +261,10 @@ struct Args {
     unsigned int* ctr;           // [0,1] ray counts, [2,3] active counts, [4] trace pull counter,
                                  // [5,6] detection record counts
     int parity, init, threshold;
+    // continuous scattering: per slot the dust segments of its last FILL path and their number
+    int continuous, rayCap;
+    PathRec* pathBuf;            // [slot][kPathCap]
+    int* pathCnt;
     int ldsMeshOff, ldsOptOff, ldsInstrOff, ldsSedOff;  // in doubles
     int detCopies;  // detect kernel: LDS copies of the SED sums (8, 4, 2, 1), 0 = SEDs straight to the tally
 };
@@ -1189,7 +1204,7 @@ struct Grid<SKIRT_GRID_VORONOI> {
 };
 
 // ================================================================== trace kernel
-template <int GRID, bool ONECOMP>
+template <int GRID, bool ONECOMP, bool CONT>
 struct Tracer {
     const Args& a;
     const Shared& sh;
@@ -1274,13 +1289,24 @@ struct Tracer {
     // per-segment work; false stops the ray (a WALK reached its optical depth)
     __device__ __forceinline__ bool segment(Ray& r, int m, double rho0, double ds) {
         if (!(ds > 0)) return true;  // DustGridPath::addSegment skips ds <= 0
-        r.s += ds;
         double kr = 0.0;  // KappaRho functor (DustSystem.cpp:465-491)
         if (m >= 0) {
             if (ONECOMP) kr = r.kext * rho0;
             else for (int h = 0; h < a.ncomp; h++) kr += sh.kext[h * a.nlambda + r.ell] * rho(m, h);
         }
         const double dtau = kr * ds;
+        if (CONT && r.mode == RAY_FILL && m >= 0) {
+            // the segment as the path holds it, before s and tau advance; the slot's count lives in
+            // pathCnt (no register of the walk carries it)
+            const int n = a.pathCnt[r.idx];
+            if (n < kPathCap) {
+                a.pathBuf[(size_t)r.idx * kPathCap + n] = PathRec{r.s, ds, r.tau, dtau, m, 0};
+                a.pathCnt[r.idx] = n + 1;
+            } else {
+                atomicOr(a.error, ERR_PATH_CAP);
+            }
+        }
+        r.s += ds;
         r.tau += dtau;
         if (r.mode == RAY_FILL) {
             segFill++;
@@ -1337,6 +1363,7 @@ struct Tracer {
         r.mode = rayMode(r.flags);
         r.ell = rayEll(r.flags);
         r.tau = 0;
+        if (CONT && r.mode == RAY_FILL) a.pathCnt[r.idx] = 0;
         r.s = c3.x;
         r.kext = sh.kext[r.ell];
         // FILL: f1 = exp(-tau) = 1, f2 = scattered luminosity; WALK: tau and s at the last segment end
@@ -1614,7 +1641,9 @@ __global__ void __launch_bounds__(kBlock) buildLeafMapKernel(LeafEntry* map, con
     }
 }
 
-template <int GRID, bool ONECOMP>
+// CONT: continuous scattering (the FILL rays record their dust segments); its own instantiations keep
+// the recording out of the other kernels' registers
+template <int GRID, bool ONECOMP, bool CONT>
 __global__ void __launch_bounds__(kBlock) SKIRT_TRACE_ATTR traceKernel(const Args a) {
     extern __shared__ __attribute__((aligned(16))) double lds[];
     if (blockIdx.x == 0 && threadIdx.x == 0) {
@@ -1626,7 +1655,7 @@ __global__ void __launch_bounds__(kBlock) SKIRT_TRACE_ATTR traceKernel(const Arg
     if (a.ctr[a.parity] == 0) return;  // an iteration after the end of the phase
     Shared sh = stageTables(a, lds, gridParts<GRID>() | STAGE_OPTICS);
 
-    Tracer<GRID, ONECOMP> T{a, sh};
+    Tracer<GRID, ONECOMP, CONT> T{a, sh};
     T.pendVal = lds + a.ldsInstrOff;  // after the grid and optics tables
     T.pendIdx = reinterpret_cast<unsigned*>(lds + a.ldsInstrOff + kLabsBuf * kBlock);
     const int lane = threadIdx.x & 63;
@@ -1793,6 +1822,7 @@ struct Events {
             if (mode != RAY_PEEL) {  // a peel-off's detection record already holds tau = 0
                 a.resA[idx] = 0.0;  // FILL: tau = 0 (and no scattered luminosity); WALK: s = 0
                 if (!ONECOMP) a.resB[idx] = 0.0;
+                if (mode == RAY_FILL && a.continuous) a.pathCnt[idx] = 0;  // an empty path: no dust segments
             }
             dst[4] = make_int4(idx, (int)RAY_NONE, 0, 0);
             return;
@@ -2268,7 +2298,7 @@ __global__ void __launch_bounds__(kBlock) SKIRT_EVENT_ATTR eventKernel(const Arg
                 // end of fillOpticalDepth + simulateescapeandabsorption; termination; simulatepropagation
                 const double taupath = a.resA[slot];
                 if (taupath < 0.0 || isnan(taupath) || isinf(taupath)) {
-                    atomicOr(a.error, 1u);
+                    atomicOr(a.error, ERR_TAU);
                     p.state = S_NEW;
                 } else {
                     if (ONECOMP) p.L = p.L * sh.alb[p.ell] * (-expm1(-taupath));
@@ -2290,7 +2320,8 @@ __global__ void __launch_bounds__(kBlock) SKIRT_EVENT_ATTR eventKernel(const Arg
                 p.rx = p.rx + s * p.kx;
                 p.ry = p.ry + s * p.ky;
                 p.rz = p.rz + s * p.kz;
-                bool ok = a.ninstr > 0 && a.peel;
+                // peeloffscattering, unless the continuous peel-off replaces it (MonteCarloSimulation.cpp:291)
+                bool ok = a.ninstr > 0 && a.peel && !a.continuous;
                 if (ok && !ONECOMP) { double I; ok = E.peelWeight(sh.instr[0], p, p.kx, p.ky, p.kz, I); }
                 if (ok) { peel = PEEL_SCATTER; ox = p.kx; oy = p.ky; oz = p.kz; }
                 E.scatter(p);
@@ -2395,6 +2426,108 @@ __global__ void __launch_bounds__(kBlock) SKIRT_EVENT_ATTR eventKernel(const Arg
     flushStats(a, vals);
 }
 
+// MonteCarloSimulation::continuouspeeloffscattering (MonteCarloSimulation.cpp:367-434), unpolarized. Runs
+// before the event kernel of an iteration: every slot whose FILL ray just returned peels off, from a
+// uniformly drawn point of every recorded path segment with scattering dust, toward every instrument,
+// with the luminosity the segment scatters (albedo e^-tau0 (1 - e^-dtau)) times the phase function. The
+// draws are the first of the packet's stream after the FILL, as in the reference (fillOpticalDepth,
+// continuouspeeloffscattering, simulateescapeandabsorption, ...); the event kernel continues the stream.
+// Two passes over the segments with the same draws: one counts the rays (a frame instrument skips a point
+// outside its field), one writes them into the space reserved for the block.
+template <int GRID, bool ONECOMP>
+__global__ void __launch_bounds__(kBlock) contKernel(const Args a) {
+    __shared__ unsigned long long resv[3 * (kBlock / 64) + 3];
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    const unsigned int nwork = a.ctr[2 + a.parity];
+    if (nwork == 0) return;
+    Shared sh = stageTables(a, lds, gridParts<GRID>() | STAGE_OPTICS | STAGE_INSTR);
+    Events<GRID, ONECOMP> E{a, sh};
+    const int* actIn = a.act[a.parity];
+    const unsigned int stride = gridDim.x * blockDim.x;
+    const unsigned int rounds = (nwork + stride - 1) / stride;  // every lane runs every round (block reserves)
+    const int Nl = a.nlambda;
+    for (unsigned int round = 0; round < rounds; round++) {
+        const unsigned int w = round * stride + blockIdx.x * blockDim.x + threadIdx.x;
+        const int slot = w < nwork ? actIn[w] : 0;
+        Packet p;
+        p.state = S_NEW;
+        if (w < nwork) E.load(slot, p);
+        const bool fill = w < nwork && p.state == S_FILL;
+        const int nrec = fill ? a.pathCnt[slot] : 0;
+        const PathRec* rec = a.pathBuf + (size_t)slot * kPathCap;
+        // the weights of one segment (rho(m,h) kappa_sca(h) / ksca) and its albedo; false: no scattering dust
+        auto weights = [&](int m, double* wv, double& albedo) {
+            double ksca = 0.0, kext = 0.0;
+            for (int h = 0; h < a.ncomp; h++) {
+                const double rho = a.rho[(size_t)m * a.ncomp + h];
+                wv[h] = rho * sh.ksca[h * Nl + p.ell];
+                ksca += rho * sh.ksca[h * Nl + p.ell];
+                kext += rho * sh.kext[h * Nl + p.ell];
+            }
+            if (!(ksca > 0.0)) return false;
+            for (int h = 0; h < a.ncomp; h++) wv[h] /= ksca;
+            albedo = ksca / kext;
+            return true;
+        };
+        // pass 1: the rays this slot emits
+        const PacketRng rng0 = p.rng;
+        unsigned int nray = 0;
+        for (int n = 0; n < nrec; n++) {
+            double wv[8], albedo;
+            if (!weights(rec[n].m, wv, albedo)) continue;
+            const double s = rec[n].s0 + p.rng.uniform() * rec[n].ds;
+            Packet q = p;
+            q.rx = p.rx + s * p.kx; q.ry = p.ry + s * p.ky; q.rz = p.rz + s * p.kz;
+            for (int i = 0; i < a.ninstr; i++)
+                if (!(sh.instr[i].kind == SKIRT_INSTR_FRAME && E.pixel(sh.instr[i], q) < 0)) nray++;
+        }
+        unsigned int pos = 0, dpos = 0, unused = 0;
+        blockReserve3(a.ctr + a.parity, nray, pos, a.ctr + 7, 0u, unused, a.ctr + 5 + a.parity, nray, dpos, resv);
+        if (nray && (pos + nray > (unsigned)a.rayCap || dpos + nray > (unsigned)(a.rayCap - a.nslots))) {
+            atomicOr(a.error, ERR_QUEUE);  // cannot happen with the pool sized for kPathCap (ensurePool)
+            nray = 0;
+        }
+        // pass 2: the same draws again, now writing the rays and their detection records
+        if (nray) {
+            PacketRng rng = rng0;
+            for (int n = 0; n < nrec; n++) {
+                double wv[8], albedo;
+                if (!weights(rec[n].m, wv, albedo)) continue;
+                const double factorm = albedo * exp(-rec[n].tau0) * (-expm1(-rec[n].dtau));
+                const double s = rec[n].s0 + rng.uniform() * rec[n].ds;
+                Packet q = p;
+                q.rx = p.rx + s * p.kx; q.ry = p.ry + s * p.ky; q.rz = p.rz + s * p.kz;
+                for (int i = 0; i < a.ninstr; i++) {
+                    const DevInstr& ins = sh.instr[i];
+                    const int l = ins.kind == SKIRT_INSTR_SED ? -1 : E.pixel(ins, q);
+                    if (ins.kind == SKIRT_INSTR_FRAME && l < 0) continue;
+                    const double cosalpha = p.kx * ins.kobs[0] + p.ky * ins.kobs[1] + p.kz * ins.kobs[2];
+                    double I = 0;
+                    for (int h = 0; h < a.ncomp; h++) {
+                        const double g = sh.g[h * Nl + p.ell];
+                        const double t = 1.0 + g * g - 2 * g * cosalpha;
+                        const double wgt = wv[h] * ((1.0 - g) * (1.0 + g) / sqrt(t * t * t));
+                        I += wgt * 1.0;
+                    }
+                    // PhotonPackage::launchScatteringPeelOff(pp, bfrnew, bfkobs, factorm * I)
+                    const double Lp = p.L * (factorm * I);
+                    const unsigned cat = p.stellar >= 0 ? CAT_STAR_SCATTERED : CAT_DUST_SCATTERED;
+                    const unsigned level = (unsigned)min(p.nscatt + 1, 255);
+                    const unsigned flags = RAY_PEEL | (cat << 2) | ((unsigned)i << 4) | (level << 10) | ((unsigned)p.ell << 18);
+                    a.det[dpos] = DetRec{Lp, 0.0, l, flags};
+                    E.emitRay(pos++, q, ins.kobs[0], ins.kobs[1], ins.kobs[2], Lp, (int)dpos, flags);
+                    dpos++;
+                }
+            }
+        }
+        if (fill) {  // the stream continues after the continuous draws
+            a.sblock[slot] = p.rng.block; a.sw2[slot] = p.rng.w2; a.sw3[slot] = p.rng.w3; a.shave[slot] = p.rng.have;
+        }
+    }
+    const unsigned long long vals[8] = {0, E.segFill, E.segWalk, E.segPeel, 0, 0, 0, 0};
+    flushStats(a, vals);
+}
+
 }  // namespace
 
 // ====================================================================== host side: the C ABI
@@ -2472,6 +2605,7 @@ struct SkirtMcrt {
     std::vector<hipEvent_t> pollEv;      // kHalves x kPollRing events behind the counter copies
     // slot pool
     int nslots = 0, rayCap = 0;
+    bool poolPath = false;  // the pool holds the continuous-scattering path records
     void* dPool = nullptr;               // kHalves pools of nslots / kHalves slots each
     size_t poolBytes = 0;
     // config
@@ -2516,11 +2650,18 @@ int upload(SkirtMcrt* c, T*& dst, const T* src, size_t n) {
 
 // slot pool: kHalves independent pipelines, each with its ray queue, SoA packet state, per-slot
 // results and two active lists; nslots counts the slots of one half
-int ensurePool(SkirtMcrt* c, int nslots) {
-    const int rayCap = nslots * (1 + (int)c->instr.size());
+// With continuous scattering every slot may also queue one peel-off per instrument and recorded path
+// segment in one iteration, and keeps the dust segments of its last path (kPathCap each).
+int ensurePool(SkirtMcrt* c, int nslots, bool continuous) {
+    const int ninstr = (int)c->instr.size();
+    const size_t rays = (size_t)nslots * (1 + ninstr) + (continuous ? (size_t)nslots * kPathCap * ninstr : 0);
+    if (rays >= (size_t)INT32_MAX) return fail(c, SKIRT_ERR_UNSUPPORTED, "ray queue too large");
+    const int rayCap = (int)rays;
+    const size_t path = continuous ? (size_t)nslots * (kPathCap * sizeof(PathRec) + sizeof(int)) : 0;
     const size_t half = (size_t)rayCap * sizeof(RayRec) + (size_t)(rayCap - nslots) * sizeof(DetRec) +
-                        (size_t)nslots * (10 * 8 + 4 * 4 + 6 * 4 + 2 * 4) + 4096;
-    if (c->dPool && c->nslots == nslots && c->rayCap == rayCap) return SKIRT_OK;
+                        (size_t)nslots * (10 * 8 + 4 * 4 + 6 * 4 + 2 * 4) + path + 4096;
+    if (c->dPool && c->nslots == nslots && c->rayCap == rayCap && c->poolPath == (path > 0)) return SKIRT_OK;
+    c->poolPath = path > 0;
     if (c->dPool) { (void)hipFree(c->dPool); c->dPool = nullptr; }
     HIPCHECK(c, hipMalloc(&c->dPool, kHalves * half));
     c->poolBytes = half;
@@ -2544,7 +2685,16 @@ void carvePool(SkirtMcrt* c, Args& a, int h) {
     takeI(a.sell); takeI(a.snscatt); takeI(a.sstellar); takeI(a.sstate);
     takeU(a.splo); takeU(a.sphi); takeU(a.sblock); takeU(a.sw2); takeU(a.sw3); takeU(a.shave);
     takeI(a.act[0]); takeI(a.act[1]);
+    a.pathBuf = nullptr;
+    a.pathCnt = nullptr;
+    if (c->poolPath) {
+        p = reinterpret_cast<char*>(((uintptr_t)p + 15) & ~(uintptr_t)15);
+        a.pathBuf = reinterpret_cast<PathRec*>(p);
+        p += n * kPathCap * sizeof(PathRec);
+        takeI(a.pathCnt);
+    }
     a.nslots = c->nslots;
+    a.rayCap = c->rayCap;
     a.ctr = c->dCtr + 8 * h;
 }
 
@@ -3353,9 +3503,14 @@ static int runPhase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, uint6
     // launch long enough that its drain tail and the event kernel amortise (C3: 2^21 slots 1.87e8 pkt/s,
     // 2^22 1.98e8, 2^23 2.04e8, 2^24 2.05e8; tools/gpu_sweep3.sh)
     int slots = c->slotsWanted > 0 ? c->slotsWanted : (1 << 23);
+    // continuous scattering (MonteCarloSimulation::continuousScattering): peel-offs from every dust segment
+    // of every path replace the ones at the interaction points; fewer slots, each with a longer queue
+    const bool continuous = p->continuous_scattering && phase != SKIRT_PHASE_DUST_SELFABS && p->has_dust &&
+                            !c->instr.empty();
+    if (continuous) slots = std::min(slots, kContSlots);
     if ((uint64_t)slots > count) slots = (int)count;
     slots = std::max(slots, 64 * kHalves) / kHalves;  // per half
-    if ((rc = ensurePool(c, slots))) return rc;
+    if ((rc = ensurePool(c, slots, continuous))) return rc;
 
     Args a{};
     a.ncells = c->ncells;
@@ -3390,6 +3545,7 @@ static int runPhase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, uint6
     a.tag = (unsigned)phase | (cycle << 2);  // Philox counter word 1: streams differ per phase and cycle
     a.phase = phase;
     a.peel = phase != SKIRT_PHASE_DUST_SELFABS;
+    a.continuous = continuous ? 1 : 0;
     a.cellLv = c->dCellLv; a.cellCdf = c->dCellCdf; a.cellLtot = c->dCellLtot; a.cellBias = c->cellBias;
     a.cellNode = c->dCellNode;
     a.minWeightReduction = p->min_weight_reduction; a.minScatt = p->min_scatt_events; a.xi = p->scatt_bias;
@@ -3450,13 +3606,17 @@ static int runPhase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, uint6
                                                : SKIRT_WALK_TREE_NODES;
     const bool one = a.ncomp == 1;
     const void* traceFn = nullptr;
-    auto pick = [&](auto fn1, auto fnN) { traceFn = one ? (const void*)fn1 : (const void*)fnN; };
-    if (kind == SKIRT_GRID_CARTESIAN) pick(traceKernel<SKIRT_GRID_CARTESIAN, true>, traceKernel<SKIRT_GRID_CARTESIAN, false>);
-    else if (kind == SKIRT_GRID_OCTREE) pick(traceKernel<SKIRT_GRID_OCTREE, true>, traceKernel<SKIRT_GRID_OCTREE, false>);
-    else if (kind == kBinTreeMap) pick(traceKernel<kBinTreeMap, true>, traceKernel<kBinTreeMap, false>);
-    else if (kind == kOctreeBookkeeping) pick(traceKernel<kOctreeBookkeeping, true>, traceKernel<kOctreeBookkeeping, false>);
-    else if (kind == SKIRT_GRID_VORONOI) pick(traceKernel<SKIRT_GRID_VORONOI, true>, traceKernel<SKIRT_GRID_VORONOI, false>);
-    else pick(traceKernel<kOctreeNodes, true>, traceKernel<kOctreeNodes, false>);
+    auto pick = [&](auto fn1, auto fnN, auto fn1c, auto fnNc) {
+        traceFn = continuous ? (one ? (const void*)fn1c : (const void*)fnNc) : (one ? (const void*)fn1 : (const void*)fnN);
+    };
+#define SKIRT_PICK(G) pick(traceKernel<G, true, false>, traceKernel<G, false, false>, traceKernel<G, true, true>, traceKernel<G, false, true>)
+    if (kind == SKIRT_GRID_CARTESIAN) SKIRT_PICK(SKIRT_GRID_CARTESIAN);
+    else if (kind == SKIRT_GRID_OCTREE) SKIRT_PICK(SKIRT_GRID_OCTREE);
+    else if (kind == kBinTreeMap) SKIRT_PICK(kBinTreeMap);
+    else if (kind == kOctreeBookkeeping) SKIRT_PICK(kOctreeBookkeeping);
+    else if (kind == SKIRT_GRID_VORONOI) SKIRT_PICK(SKIRT_GRID_VORONOI);
+    else SKIRT_PICK(kOctreeNodes);
+#undef SKIRT_PICK
     if (ldsTrace > 64 * 1024)
         HIPCHECK(c, hipFuncSetAttribute(traceFn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ldsTrace));
     int tgrid = c->traceGrid;
@@ -3486,15 +3646,20 @@ static int runPhase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, uint6
         else { if (one) SKIRT_EVENT(kOctreeNodes, true); else SKIRT_EVENT(kOctreeNodes, false); }
 #undef SKIRT_EVENT
     };
+    auto launchCont = [&](const Args& aa, hipStream_t st) {
+#define SKIRT_CONT(G, O) hipLaunchKernelGGL((contKernel<G, O>), dim3(egrid), dim3(kBlock), ldsEvent, st, aa)
+        if (kind == SKIRT_GRID_CARTESIAN) { if (one) SKIRT_CONT(SKIRT_GRID_CARTESIAN, true); else SKIRT_CONT(SKIRT_GRID_CARTESIAN, false); }
+        else if (kind == SKIRT_GRID_OCTREE) { if (one) SKIRT_CONT(SKIRT_GRID_OCTREE, true); else SKIRT_CONT(SKIRT_GRID_OCTREE, false); }
+        else if (kind == kBinTreeMap) { if (one) SKIRT_CONT(kBinTreeMap, true); else SKIRT_CONT(kBinTreeMap, false); }
+        else if (kind == kOctreeBookkeeping) { if (one) SKIRT_CONT(kOctreeBookkeeping, true); else SKIRT_CONT(kOctreeBookkeeping, false); }
+        else if (kind == SKIRT_GRID_VORONOI) { if (one) SKIRT_CONT(SKIRT_GRID_VORONOI, true); else SKIRT_CONT(SKIRT_GRID_VORONOI, false); }
+        else { if (one) SKIRT_CONT(kOctreeNodes, true); else SKIRT_CONT(kOctreeNodes, false); }
+#undef SKIRT_CONT
+    };
     auto launchTrace = [&](const Args& aa, hipStream_t st) {
-#define SKIRT_TRACE(G, O) hipLaunchKernelGGL((traceKernel<G, O>), dim3(tgrid), dim3(kBlock), ldsTrace, st, aa)
-        if (kind == SKIRT_GRID_CARTESIAN) { if (one) SKIRT_TRACE(SKIRT_GRID_CARTESIAN, true); else SKIRT_TRACE(SKIRT_GRID_CARTESIAN, false); }
-        else if (kind == SKIRT_GRID_OCTREE) { if (one) SKIRT_TRACE(SKIRT_GRID_OCTREE, true); else SKIRT_TRACE(SKIRT_GRID_OCTREE, false); }
-        else if (kind == kBinTreeMap) { if (one) SKIRT_TRACE(kBinTreeMap, true); else SKIRT_TRACE(kBinTreeMap, false); }
-        else if (kind == kOctreeBookkeeping) { if (one) SKIRT_TRACE(kOctreeBookkeeping, true); else SKIRT_TRACE(kOctreeBookkeeping, false); }
-        else if (kind == SKIRT_GRID_VORONOI) { if (one) SKIRT_TRACE(SKIRT_GRID_VORONOI, true); else SKIRT_TRACE(SKIRT_GRID_VORONOI, false); }
-        else { if (one) SKIRT_TRACE(kOctreeNodes, true); else SKIRT_TRACE(kOctreeNodes, false); }
-#undef SKIRT_TRACE
+        // the kernel picked above (traceFn), launched through its generic entry
+        void* args[] = {const_cast<Args*>(&aa)};
+        return hipLaunchKernel(traceFn, dim3(tgrid), dim3(kBlock), args, ldsTrace, st);
     };
     if ((int)c->pollEv.size() < kHalves * kPollRing) {
         while ((int)c->pollEv.size() < kHalves * kPollRing) {
@@ -3528,6 +3693,10 @@ static int runPhase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, uint6
             hipStream_t st = streams[h];
             aa.parity = its[h] & 1;
             aa.init = (its[h] == 0) ? 1 : 0;
+            if (aa.continuous && !aa.init) {  // the continuous peel-offs of the FILL rays that just returned
+                launchCont(aa, st);
+                HIPCHECK(c, hipGetLastError());
+            }
             launchEvent(aa, st);
             HIPCHECK(c, hipGetLastError());
             if (!a.hasDust) { done[h] = true; its[h]++; continue; }  // every packet completes in the event kernel
@@ -3539,7 +3708,7 @@ static int runPhase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, uint6
                 c->traceEv.push_back(e1);
             }
             HIPCHECK(c, hipEventRecord(c->traceEv[2 * c->traceLaunches], st));
-            launchTrace(aa, st);
+            HIPCHECK(c, launchTrace(aa, st));
             HIPCHECK(c, hipGetLastError());
             HIPCHECK(c, hipEventRecord(c->traceEv[2 * c->traceLaunches + 1], st));
             c->traceLaunches++;
@@ -3587,7 +3756,11 @@ int skirt_mcrt_synchronize(SkirtMcrt* c) {
     c->traceLaunches = 0;  // timed: the event pairs can be reused
     unsigned int e = 0;
     HIPCHECK(c, hipMemcpy(&e, c->dError, sizeof e, hipMemcpyDeviceToHost));
-    if (e) return fail(c, SKIRT_ERR_NUMERIC, "the optical depth along the path is not a positive number");
+    if (e & ERR_TAU) return fail(c, SKIRT_ERR_NUMERIC, "the optical depth along the path is not a positive number");
+    if (e & ERR_PATH_CAP)
+        return fail(c, SKIRT_ERR_UNSUPPORTED, "continuous scattering: a path crosses more than " +
+                                                  std::to_string(kPathCap) + " dust cells");
+    if (e) return fail(c, SKIRT_ERR_STATE, "ray queue overflow");
     return SKIRT_OK;
 }
 

@@ -1303,7 +1303,6 @@ Model loadSki(const std::string& path, UniformSource& rng, const std::string& da
     if (m.packages < 0 || m.packages > 1e15) throw std::runtime_error("invalid number of photon packages");
     if (m.minWeightReduction < 1e3) throw std::runtime_error("the minimum weight reduction factor should be larger than 1000");
     if (m.scattBias < 0 || m.scattBias > 1) throw std::runtime_error("the scattering bias should be between 0 and 1");
-    if (m.continuousScattering) throw std::runtime_error("continuousScattering is not supported by this engine");
 
     m.wl = parseWavelengthGrid(c, need(sim, "wavelengthGrid"));
     int Nlambda = m.wl.n();

@@ -223,14 +223,14 @@ int skirt_sim_run_stellar(SkirtSim* s, uint64_t first, uint64_t count) {
     uint64_t total = s->npp * (uint64_t)s->m.wl.n();
     if (count == 0) count = total - std::min(first, total);
     SkirtPhaseParams p{s->m.minWeightReduction, s->m.minScattEvents, s->m.scattBias,
-                       s->m.hasDust && s->m.storeAbsorption ? 1 : 0, s->m.hasDust ? 1 : 0};
+                       s->m.hasDust && s->m.storeAbsorption ? 1 : 0, s->m.hasDust ? 1 : 0, s->m.continuousScattering ? 1 : 0};
     return check(s, skirt_mcrt_run_stellar(s->eng, s->npp, first, count, s->m.seed, &p));
 }
 
 int skirt_sim_run_stellar_shard(SkirtSim* s, int rank, int world) {
     if (!s || !s->eng) { g_err = "no engine attached"; return SKIRT_ERR_STATE; }
     SkirtPhaseParams p{s->m.minWeightReduction, s->m.minScattEvents, s->m.scattBias,
-                       s->m.hasDust && s->m.storeAbsorption ? 1 : 0, s->m.hasDust ? 1 : 0};
+                       s->m.hasDust && s->m.storeAbsorption ? 1 : 0, s->m.hasDust ? 1 : 0, s->m.continuousScattering ? 1 : 0};
     return check(s, skirt_mcrt_run_phase_shard(s->eng, SKIRT_PHASE_STELLAR, 0, s->npp, rank, world, s->m.seed, &p));
 }
 
@@ -248,7 +248,7 @@ int skirt_sim_run_dust_shard(SkirtSim* s, int rank, int world) {
         int rc;
         const int Nl = m.wl.n();
         const std::vector<PlanckTable> tables = planckTables(m);
-        SkirtPhaseParams p{m.minWeightReduction, m.minScattEvents, m.scattBias, 0, 1};
+        SkirtPhaseParams p{m.minWeightReduction, m.minScattEvents, m.scattBias, 0, 1, m.continuousScattering ? 1 : 0};
         // The cell sources between phases: on the device from the device tallies (default), or on the
         // host by the restatement the oracle shares (SKIRT_AMD_HOST_SOURCES=1)
         const char* env = getenv("SKIRT_AMD_HOST_SOURCES");

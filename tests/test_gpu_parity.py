@@ -87,7 +87,8 @@ def test_leaf_map_walk_equals_node_walk(path, packages, monkeypatch):
 
 
 @pytest.mark.parametrize("name,packages", [("pan_cart16", 2000), ("pan_oct", 2000), ("pan_cart16_sa", 1000),
-                                           ("pan_oct_sa", 1000), ("pan_oct_sac", 1000), ("vor_pan", 1000)])
+                                           ("pan_oct_sa", 1000), ("pan_oct_sac", 1000), ("vor_pan", 1000),
+                                           ("pan_cart16_cs", 300), ("pan_oct_cs", 300), ("vor_pan_cs", 200)])
 def test_dust_phases_match_oracle_same_streams(name, packages):
     """Stellar emission, the self-absorption cycles (if the model has them) and the dust emission phase
     (PanMonteCarloSimulation::runSelf) on the GPU against the oracle on the same Philox streams. The
@@ -267,7 +268,7 @@ def _pools(J, max_rel_sd):
     return pools
 
 
-@pytest.mark.parametrize("name", ["pan_cart16", "pan_oct"])
+@pytest.mark.parametrize("name", ["pan_cart16", "pan_oct", "vor_pan", "pan_cart16_sa"])
 def test_per_cell_mean_intensity_matches_reference(tmp_path, name):
     """north_star's per-cell criterion: every cell's J_lambda (ds_isrf, i.e. its absorbed luminosity
     divided by the cell constant of DustSystem::meanintensityv, DustSystem.cpp:935-957) within the Monte
