@@ -1,6 +1,8 @@
 """ExpDiskGeometry and SersicGeometry stars and dust on the GPU against the CPU oracle on the same Philox
 streams (the geometries' restatements are checked on their own in tests/test_geometries.py; parity
 unpinned against the reference itself, which has no fixture for them)."""
+import os
+
 import numpy as np
 import pytest
 
@@ -76,3 +78,21 @@ def test_dust_mix_engine_matches_oracle_same_streams(tmp_path, name):
     assert_parity(labs, orc.labs, 1e-9, STELLAR_OUTLIERS, "labs")
     frames, seds = sim.instrument(0)
     np.testing.assert_allclose(seds, orc.seds[0], rtol=1e-9, atol=1e-300)
+
+
+def test_cli_runs_every_phase(tmp_path):
+    """skirt-mi355x (SkirtMain's counterpart) runs the stellar phase, the self-absorption cycles and the dust
+    emission phase of a Pan model and writes SKIRT's outputs with the dust columns filled."""
+    import subprocess
+
+    import skirt_files as F
+
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "skirt_amd", "bin", "skirt-mi355x")
+    ski = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "ski", "pan_cart16_sa.ski")
+    prefix = str(tmp_path / "sa")
+    r = subprocess.run([exe, "-p", "500", "-o", prefix, ski], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert r.stdout.count("Self-absorption cycle") == 6, r.stdout
+    sed = F.read_text_table(prefix + "_i30_sed.dat")
+    assert sed[:, 4].sum() > 0 and sed[:, 5].sum() > 0  # dust emission: direct and scattered
+    assert os.path.exists(prefix + "_ds_isrf.dat")
