@@ -1556,18 +1556,32 @@ __global__ void __launch_bounds__(kBlock) cellBlockSumKernel(const EmisArgs e) {
     if (threadIdx.x == 0) e.blockSums[(size_t)ell * e.nblocks + b] = red[0];
 }
 
-// per wavelength (one block each): exclusive scan of the block sums and the total
+// per wavelength (one block each): exclusive scan of the block sums and the total. Each thread sums a
+// contiguous chunk of the block sums, the chunk sums are scanned in LDS, and each thread then writes its
+// chunk's exclusive prefixes (a single thread walking all block sums took 3 ms per call on C5).
 __global__ void __launch_bounds__(kBlock) cellScanBlocksKernel(const EmisArgs e) {
+    __shared__ double part[kBlock];
     const int ell = blockIdx.x;
-    if (threadIdx.x != 0) return;
-    double run = 0;
     double* bs = e.blockSums + (size_t)ell * e.nblocks;
-    for (int b = 0; b < e.nblocks; b++) {
+    const int per = (e.nblocks + kBlock - 1) / kBlock;
+    const int b0 = min(e.nblocks, (int)threadIdx.x * per), b1 = min(e.nblocks, b0 + per);
+    double sum = 0;
+    for (int b = b0; b < b1; b++) sum += bs[b];
+    part[threadIdx.x] = sum;
+    __syncthreads();
+    for (int off = 1; off < kBlock; off <<= 1) {  // inclusive Hillis-Steele scan of the chunk sums
+        const double v = threadIdx.x >= (unsigned)off ? part[threadIdx.x - off] : 0.0;
+        __syncthreads();
+        part[threadIdx.x] += v;
+        __syncthreads();
+    }
+    double run = threadIdx.x ? part[threadIdx.x - 1] : 0.0;
+    for (int b = b0; b < b1; b++) {
         const double v = bs[b];
         bs[b] = run;
         run += v;
     }
-    e.ltot[ell] = run;
+    if (threadIdx.x == kBlock - 1) e.ltot[ell] = part[kBlock - 1];
 }
 
 // the normalized cumulative distribution: X[0] = 0, X[m+1] = (sum of Lv[0..m]) / Ltot
@@ -3327,7 +3341,7 @@ int skirt_mcrt_compute_cell_sources(SkirtMcrt* c, int include_dust) {
     e.lv = c->dCellLv; e.cdf = c->dCellCdf; e.ltot = c->dCellLtot; e.blockSums = c->dEmisScratch; e.nblocks = nblocks;
     hipLaunchKernelGGL(cellSpectraKernel, dim3(nblocks), dim3(kBlock), 0, c->stream, e);
     hipLaunchKernelGGL(cellBlockSumKernel, dim3(nblocks, Nl), dim3(kBlock), 0, c->stream, e);
-    hipLaunchKernelGGL(cellScanBlocksKernel, dim3(Nl), dim3(64), 0, c->stream, e);
+    hipLaunchKernelGGL(cellScanBlocksKernel, dim3(Nl), dim3(kBlock), 0, c->stream, e);
     hipLaunchKernelGGL(cellCdfKernel, dim3(nblocks, Nl), dim3(kBlock), 0, c->stream, e);
     HIPCHECK(c, hipGetLastError());
     return SKIRT_OK;
@@ -3346,7 +3360,7 @@ int skirt_mcrt_dust_labs_total(SkirtMcrt* c, double* total) {
     e.nblocks = (int)((n + kBlock - 1) / kBlock);
     e.ltot = c->dEmisScratch + e.nblocks;  // one slot past the block sums
     hipLaunchKernelGGL(cellBlockSumKernel, dim3(e.nblocks, 1), dim3(kBlock), 0, c->stream, e);
-    hipLaunchKernelGGL(cellScanBlocksKernel, dim3(1), dim3(64), 0, c->stream, e);
+    hipLaunchKernelGGL(cellScanBlocksKernel, dim3(1), dim3(kBlock), 0, c->stream, e);
     HIPCHECK(c, hipGetLastError());
     HIPCHECK(c, hipMemcpyAsync(total, e.ltot, sizeof(double), hipMemcpyDeviceToHost, c->stream));
     HIPCHECK(c, hipStreamSynchronize(c->stream));

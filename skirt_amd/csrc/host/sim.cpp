@@ -1,5 +1,6 @@
 // Host driver: .ski -> Model -> device engine -> outputs (include/skirt_host.h).
 #include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <cmath>
 #include <memory>
@@ -25,6 +26,7 @@ struct SkirtSim {
     SkirtMcrt* eng = nullptr;
     std::vector<double> labs;                 // Ncells x Nlambda (stellar)
     std::vector<double> labsDust;             // Ncells x Nlambda (last self-absorption cycle)
+    bool dustLabsOnDevice = false;            // labsDust is still to be downloaded (skirt_sim_fetch)
     std::vector<double> dustTotals;           // Labsdusttot after every self-absorption cycle
     std::vector<double> instrAll;             // concatenated, per instrument frames [slot][lambda][pixel] + SEDs
     std::vector<size_t> instrOff;             // per instrument offset into instrAll
@@ -247,7 +249,18 @@ int skirt_sim_run_dust_shard(SkirtSim* s, int rank, int world) {
     try {
         int rc;
         const int Nl = m.wl.n();
+        // SKIRT_AMD_PHASE_TIMES: wall time of the host driver's stages (a stage ending in a device
+        // synchronization includes the device work queued before it)
+        static const bool timing = getenv("SKIRT_AMD_PHASE_TIMES") != nullptr;
+        auto t0 = std::chrono::steady_clock::now();
+        auto stage = [&](const char* what) {
+            if (!timing) return;
+            const auto t1 = std::chrono::steady_clock::now();
+            fprintf(stderr, "[dust] %-28s %8.3f ms\n", what, std::chrono::duration<double, std::milli>(t1 - t0).count());
+            t0 = t1;
+        };
         const std::vector<PlanckTable> tables = planckTables(m);
+        stage("planck tables");
         SkirtPhaseParams p{m.minWeightReduction, m.minScattEvents, m.scattBias, 0, 1, m.continuousScattering ? 1 : 0};
         // The cell sources between phases: on the device from the device tallies (default), or on the
         // host by the restatement the oracle shares (SKIRT_AMD_HOST_SOURCES=1)
@@ -271,6 +284,7 @@ int skirt_sim_run_dust_shard(SkirtSim* s, int rank, int world) {
                                    sigma.data(), mu.data(), tables[0].Tv.data(), planck.data(), m.wl.lambda.data(),
                                    m.wl.dlambda.data(), m.dustEmissionBias};
             if ((rc = check(s, skirt_mcrt_upload_emissivity(s->eng, &ed)))) return rc;
+            stage("emissivity upload");
         }
         auto prepare = [&](bool withDust) -> int {
             if (!hostSources) return check(s, skirt_mcrt_compute_cell_sources(s->eng, withDust ? 1 : 0));
@@ -309,13 +323,17 @@ int skirt_sim_run_dust_shard(SkirtSim* s, int rank, int world) {
                 }
                 s->dustTotals.push_back(total);
                 sched.finishCycle(total);
+                stage("self-absorption cycle");
             }
-            if (!hostSources && (rc = check(s, skirt_mcrt_download_dust_labs(s->eng, s->labsDust.data())))) return rc;
+            // the final dust Labs reach the host with the other tallies (skirt_sim_fetch), not here
+            s->dustLabsOnDevice = !hostSources;
         }
         // PanMonteCarloSimulation::rundustemission (PanMonteCarloSimulation.cpp:245-264)
         if ((rc = prepare(m.selfAbsorption))) return rc;
         uint64_t npp = (uint64_t)std::ceil(m.packages * m.emissionBoost);
-        return check(s, skirt_mcrt_run_phase_shard(s->eng, SKIRT_PHASE_DUST_EMISSION, 0, npp, rank, world, m.seed, &p));
+        rc = check(s, skirt_mcrt_run_phase_shard(s->eng, SKIRT_PHASE_DUST_EMISSION, 0, npp, rank, world, m.seed, &p));
+        stage("dust emission (launched)");
+        return rc;
     } catch (std::exception& e) {
         g_err = e.what();
         return SKIRT_ERR_ARG;
@@ -335,6 +353,10 @@ int skirt_sim_fetch(SkirtSim* s) {
     int rc = check(s, skirt_mcrt_download(s->eng, s->labs.empty() ? nullptr : s->labs.data(),
                                           s->instrAll.empty() ? nullptr : s->instrAll.data()));
     if (rc) return rc;
+    if (s->dustLabsOnDevice) {
+        if ((rc = check(s, skirt_mcrt_download_dust_labs(s->eng, s->labsDust.data())))) return rc;
+        s->dustLabsOnDevice = false;
+    }
     s->splitInstr();
     return SKIRT_OK;
 }
