@@ -65,8 +65,8 @@ constexpr int kPollEvery = 1;      // iterations between two counter copies of a
 constexpr int kPollRing = 3;       // copies in flight per half (the host reads each kPollRing copies late)
 // occupancy attribute of the trace kernel (a build knob for tuning variants, tools/build_variant.sh):
 // 3 waves per SIMD, i.e. at most 168 VGPRs (the grid entry on the pull path would otherwise take the
-// octree kernel to 175 and 2 waves; C3 1.91e8 -> 2.15e8 pkt/s at 3). The Voronoi step, at 4 entries per
-// load round, spills 60 B/lane at 3 waves and still runs fastest there (C4, profiles/r02_sweep_vor.txt).
+// octree kernel to 175 and 2 waves; C3 1.91e8 -> 2.15e8 pkt/s at 3). The Voronoi walk has its own
+// kernel and attribute below.
 // leaf-map step: check the estimated finest cell against the found leaf's faces instead of the finest
 // cell's own split coordinates (see LeafMapGrid::step; 0 restores the finest-cell check: C3 2.154e8 ->
 // 2.162e8, C5 1.071e8 -> 1.091e8 pkt/s with 1)
@@ -75,6 +75,11 @@ constexpr int kPollRing = 3;       // copies in flight per half (the host reads 
 #endif
 #ifndef SKIRT_TRACE_ATTR
 #define SKIRT_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(3)))
+#endif
+// the Voronoi trace kernel at 2 waves per SIMD: its branch-free bounds keep several entries in flight
+// and run without spills in 256 VGPRs (C4 5.72e7 pkt/s at 3 waves, 6.08e7 at 2)
+#ifndef SKIRT_VOR_TRACE_ATTR
+#define SKIRT_VOR_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(2)))
 #endif
 // the event kernel at 2 waves per SIMD: the Voronoi instantiation (cellIndex on the grid entry of every
 // queued ray) would otherwise take 256 VGPRs + AGPRs and run at 1
@@ -169,7 +174,11 @@ constexpr int kVorHead = 3;  // header slots
 #ifndef SKIRT_VOR_UNROLL
 #define SKIRT_VOR_UNROLL 4
 #endif
-constexpr int kVorUnroll = SKIRT_VOR_UNROLL;  // entries loaded per round trip (the slot array is padded)
+constexpr int kVorUnroll = SKIRT_VOR_UNROLL;
+#ifndef SKIRT_VOR_FALLBACK_GROUP
+#define SKIRT_VOR_FALLBACK_GROUP 2  // neighbour sites loaded together by the exact re-evaluation (<= kVorUnroll)
+#endif
+constexpr int kVorCand = 4;  // possible winners the exact re-evaluation collects before it takes the whole list  // entries loaded per round trip (the slot array is padded)
 // bound factor of the approximate (single-precision) plane distances: 16 x 2^-24
 constexpr float kVorEpsF = 1.0f / (1 << 20);
 
@@ -1074,23 +1083,12 @@ struct Grid<SKIRT_GRID_VORONOI> {
         const float Dx = (float)((pwx - r.x) * sc), Dy = (float)((pwy - r.y) * sc), Dz = (float)((pwz - r.z) * sc);
         const float fkx = (float)kx, fky = (float)ky, fkz = (float)kz;
         // bounds [lo, hi] of every neighbour's plane distance; U: the least upper bound of the certain
-        // exits; L1 < L2: the two least lower bounds of the possible exits, w1: the first one's `next`
+        // exits; L1 <= L2: the two least lower bounds of the possible exits, w1: the first one's `next`.
+        // Walls are stored as the bisector plane with the site's mirror image (the same plane), so every
+        // entry takes the same branch-free arithmetic; lo = hi = FLT_MAX: certainly no exit.
         float U = FLT_MAX, L1 = FLT_MAX, L2 = FLT_MAX;
         int w1 = 0;
-        // the bounds of one entry's plane distance; lo = FLT_MAX: certainly no exit
-        auto bound = [&](const VorEntry& en, float& lo, float& hi) {
-            lo = FLT_MAX; hi = 0.f;
-            const int nxt = en.next;
-            if (nxt < 0) {
-                const double si = wallDist(a, r, nxt);
-                if (si > 0) {
-                    const float v = (float)(si * sc);
-                    lo = v * (1.0f - kVorEpsF);
-                    hi = v * (1.0f + kVorEpsF);
-                }
-                return;
-            }
-            {
+        auto bounds = [&](const VorEntry& en, bool valid, float& lo, float& hi) {
 #if SKIRT_VOR_CONTRACT
             // FMA contraction in the bounds only: a fused operation rounds once where the bound counts
             // two roundings, so the intervals stay valid
@@ -1100,28 +1098,27 @@ struct Grid<SKIRT_GRID_VORONOI> {
             const float px = nx * fkx, py = ny * fky, pz = nz * fkz;
             const float den = px + py + pz;
             const float eA = kVorEpsF * (fabsf(px) + fabsf(py) + fabsf(pz));
-            if (den > -eA) {  // else moving away from this plane for certain: no exit
-                const float tx = Dx + 0.5f * nx, ty = Dy + 0.5f * ny, tz = Dz + 0.5f * nz;
-                const float qx = nx * tx, qy = ny * ty, qz = nz * tz;
-                const float num = qx + qy + qz;
-                const float eB = kVorEpsF * (fabsf(qx) + fabsf(qy) + fabsf(qz) + 0.5f * (nx * nx + ny * ny + nz * nz));
-                if (den > 2.0f * eA) {
-                    const float inv = __builtin_amdgcn_rcpf(den);
-                    const float sa = num * inv;
-                    const float err = 2.0f * (eB + fabsf(sa) * eA) * inv + fabsf(sa) * kVorEpsF;
-                    if (sa + err > 0.f) { lo = sa - err; hi = sa + err; }
-                } else {
-                    lo = -FLT_MAX; hi = FLT_MAX;  // the sign of n.k is uncertain
-                }
-            }
-            }
+            const float tx = Dx + 0.5f * nx, ty = Dy + 0.5f * ny, tz = Dz + 0.5f * nz;
+            const float qx = nx * tx, qy = ny * ty, qz = nz * tz;
+            const float num = qx + qy + qz;
+            const float eB = kVorEpsF * (fabsf(qx) + fabsf(qy) + fabsf(qz) + 0.5f * (nx * nx + ny * ny + nz * nz));
+            const float inv = __builtin_amdgcn_rcpf(den);
+            const float sa = num * inv;
+            const float err = 2.0f * (eB + fabsf(sa) * eA) * inv + fabsf(sa) * kVorEpsF;
+            // den > 2 eA: the sign of n.k and the interval are certain; den <= -eA: moving away for
+            // certain; otherwise (or NaN offsets: a degenerate wall) the sign is uncertain
+            const bool sure = den > 2.0f * eA;
+            const bool none = !valid || den <= -eA || (sure && !(sa + err > 0.f));
+            lo = none ? FLT_MAX : sure ? sa - err : -FLT_MAX;
+            hi = (none || !sure) ? FLT_MAX : sa + err;
         };
-        auto update = [&](int nxt, float lo, float hi) {
-            if (lo != FLT_MAX) {
-                if (lo > 0.f && hi < U) U = hi;
-                if (lo < L1) { L2 = L1; L1 = lo; w1 = nxt; }
-                else if (lo < L2) L2 = lo;
-            }
+        auto entry = [&](const VorEntry& en, bool valid) {
+            float lo, hi;
+            bounds(en, valid, lo, hi);
+            U = fminf(U, lo > 0.f ? hi : FLT_MAX);
+            w1 = lo < L1 ? en.next : w1;
+            L2 = __builtin_amdgcn_fmed3f(L1, L2, lo);
+            L1 = fminf(L1, lo);
         };
         for (int q0 = 0; q0 < cnt; q0 += kVorUnroll) {
             if (q0) {
@@ -1129,11 +1126,7 @@ struct Grid<SKIRT_GRID_VORONOI> {
                 for (int u = 0; u < kVorUnroll; u++) e[u] = B[kVorHead + q0 + u];
             }
 #pragma unroll
-            for (int u = 0; u < kVorUnroll; u++) {
-                float lo = FLT_MAX, hi = 0.f;
-                if (q0 + u < cnt) bound(e[u], lo, hi);
-                update(e[u].next, lo, hi);
-            }
+            for (int u = 0; u < kVorUnroll; u++) entry(e[u], q0 + u < cnt);
         }
         if (L1 != FLT_MAX && L2 > U) {
             if (w1 >= 0) {  // the exit: its exact distance when the next cell's header arrives
@@ -1146,21 +1139,60 @@ struct Grid<SKIRT_GRID_VORONOI> {
             seg(idw, rhow, wallDist(a, r, w1));  // leaves the grid through a wall
             return false;
         }
-        // no exit, or several possible exits: the reference's rule, exactly, over the whole list
+        // no exit, or several possible exits: the reference's rule, exactly, over the possible winners.
+        // An entry whose lower bound exceeds U lies beyond a certain exit, so it can neither win nor tie;
+        // a second pass over the (cached) entries collects the others in list order (the first of equal
+        // distances wins) and their sites arrive in one round trip. More than kVorCand of them: the whole
+        // list, in groups.
         constexpr int NO_INDEX = (int)0x80000000u;
         double sq = kDblMax;
         int mq = NO_INDEX;
+        auto consider = [&](int nxt, double pix, double piy, double piz) {
+            const double si = nxt < 0 ? wallDist(a, r, nxt) : planeDist(r, pwx, pwy, pwz, pix, piy, piz);
+            if (si > 0 && si < sq) { sq = si; mq = nxt; }
+        };
         if (L1 != FLT_MAX) {
-            for (int q = 0; q < cnt; q++) {
-                const int nxt = B[kVorHead + q].next;
-                double si;
-                if (nxt < 0) si = wallDist(a, r, nxt);
-                else {
-                    double pix, piy, piz;
-                    siteAt(a, nxt, pix, piy, piz);
-                    si = planeDist(r, pwx, pwy, pwz, pix, piy, piz);
+            int c0 = 0, c1 = 0, c2 = 0, c3 = 0, nc = 0;
+            for (int q0 = 0; q0 < cnt; q0 += kVorUnroll) {
+#pragma unroll
+                for (int u = 0; u < kVorUnroll; u++) e[u] = B[kVorHead + q0 + u];
+#pragma unroll
+                for (int u = 0; u < kVorUnroll; u++) {
+                    float lo, hi;
+                    bounds(e[u], q0 + u < cnt, lo, hi);
+                    if (lo < FLT_MAX && lo <= U) {
+                        const int nx = e[u].next;
+                        c0 = nc == 0 ? nx : c0; c1 = nc == 1 ? nx : c1; c2 = nc == 2 ? nx : c2; c3 = nc == 3 ? nx : c3;
+                        nc++;
+                    }
                 }
-                if (si > 0 && si < sq) { sq = si; mq = nxt; }
+            }
+            if (nc <= kVorCand) {
+                const int cs[kVorCand] = {c0, c1, c2, c3};
+                double pix[kVorCand], piy[kVorCand], piz[kVorCand];
+#pragma unroll
+                for (int u = 0; u < kVorCand; u++) {
+                    pix[u] = piy[u] = piz[u] = 0.0;
+                    if (u < nc && cs[u] >= 0) siteAt(a, cs[u], pix[u], piy[u], piz[u]);
+                }
+#pragma unroll
+                for (int u = 0; u < kVorCand; u++)
+                    if (u < nc) consider(cs[u], pix[u], piy[u], piz[u]);
+            } else {
+                constexpr int G = SKIRT_VOR_FALLBACK_GROUP;
+                for (int q0 = 0; q0 < cnt; q0 += G) {
+                    int nxt[G];
+                    double pix[G], piy[G], piz[G];
+#pragma unroll
+                    for (int u = 0; u < G; u++) {
+                        nxt[u] = B[kVorHead + q0 + u].next;
+                        pix[u] = piy[u] = piz[u] = 0.0;
+                        if (q0 + u < cnt && nxt[u] >= 0) siteAt(a, nxt[u], pix[u], piy[u], piz[u]);
+                    }
+#pragma unroll
+                    for (int u = 0; u < G; u++)
+                        if (q0 + u < cnt) consider(nxt[u], pix[u], piy[u], piz[u]);
+                }
             }
         }
         if (mq == NO_INDEX) {
@@ -1658,7 +1690,7 @@ __global__ void __launch_bounds__(kBlock) buildLeafMapKernel(LeafEntry* map, con
 // CONT: continuous scattering (the FILL rays record their dust segments); its own instantiations keep
 // the recording out of the other kernels' registers
 template <int GRID, bool ONECOMP, bool CONT>
-__global__ void __launch_bounds__(kBlock) SKIRT_TRACE_ATTR traceKernel(const Args a) {
+__device__ __forceinline__ void traceBody(const Args& a) {
     extern __shared__ __attribute__((aligned(16))) double lds[];
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         // reset the counters the next event iteration appends to (nobody else uses them now)
@@ -1736,6 +1768,17 @@ __global__ void __launch_bounds__(kBlock) SKIRT_TRACE_ATTR traceKernel(const Arg
     T.drain();
     const unsigned long long vals[8] = {0, T.segFill, T.segWalk, T.segPeel, 0, T.absorbs, T.laneSlots, T.requests};
     flushStats(a, vals);
+}
+
+template <int GRID, bool ONECOMP, bool CONT>
+__global__ void __launch_bounds__(kBlock) SKIRT_TRACE_ATTR traceKernel(const Args a) {
+    traceBody<GRID, ONECOMP, CONT>(a);
+}
+
+// the Voronoi walk at its own occupancy (SKIRT_VOR_TRACE_ATTR)
+template <bool ONECOMP, bool CONT>
+__global__ void __launch_bounds__(kBlock) SKIRT_VOR_TRACE_ATTR traceKernelVor(const Args a) {
+    traceBody<SKIRT_GRID_VORONOI, ONECOMP, CONT>(a);
 }
 
 // the detections of this iteration's peel-off rays (their optical depths are in the queue now)
@@ -3061,7 +3104,15 @@ int skirt_mcrt_upload_grid(SkirtMcrt* c, const SkirtGridDesc* g) {
                 const int id = g->cell_nbr_list[q];
                 VorEntry& e = blk[o];
                 if (id < 0) {
-                    e = VorEntry{0.f, 0.f, 0.f, id};
+                    // a wall (-1 xmin, -2 xmax, ... -6 zmax) is the bisector plane of the site and its mirror
+                    // image: the offset to the mirror site along the wall's axis (NaN when the site lies on
+                    // the wall: the step then evaluates the list exactly)
+                    const int axis = (-id - 1) / 2;
+                    const double lim[6] = {c->gx0, c->gx1, c->gy0, c->gy1, c->gz0, c->gz1};
+                    const double w = lim[-id - 1] - sm[axis];
+                    float o[3] = {0.f, 0.f, 0.f};
+                    o[axis] = w != 0.0 ? (float)(2.0 * w * c->vorScale) : NAN;
+                    e = VorEntry{o[0], o[1], o[2], id};
                 } else {
                     const double* si = g->site + 3 * (size_t)id;
                     e = VorEntry{(float)((si[0] - sm[0]) * c->vorScale), (float)((si[1] - sm[1]) * c->vorScale),
@@ -3628,7 +3679,8 @@ static int runPhase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, uint6
     else if (kind == SKIRT_GRID_OCTREE) SKIRT_PICK(SKIRT_GRID_OCTREE);
     else if (kind == kBinTreeMap) SKIRT_PICK(kBinTreeMap);
     else if (kind == kOctreeBookkeeping) SKIRT_PICK(kOctreeBookkeeping);
-    else if (kind == SKIRT_GRID_VORONOI) SKIRT_PICK(SKIRT_GRID_VORONOI);
+    else if (kind == SKIRT_GRID_VORONOI)
+        pick(traceKernelVor<true, false>, traceKernelVor<false, false>, traceKernelVor<true, true>, traceKernelVor<false, true>);
     else SKIRT_PICK(kOctreeNodes);
 #undef SKIRT_PICK
     if (ldsTrace > 64 * 1024)

@@ -1,0 +1,8 @@
+# round 2: the Voronoi trace kernel at 2 waves/SIMD -- GPU tests, C4 and C3 against the previous build
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+run() { local name=$1 t=$2; shift 2; echo "== $name"; timeout -k 10 $t "$@" > gpurun_out/$name.log 2>&1; local rc=$?; echo "rc=$rc"; tail -${TAILN:-1} gpurun_out/$name.log | cut -c1-200; return $rc; }
+TAILN=2 run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread &&
+run c4 300 python bench.py --config c4 --no-cpu-baseline &&
+run c3 300 python bench.py --no-cpu-baseline &&
+SKIRT_AMD_LIB=libskirt_amd_old.so run c3_old 300 python bench.py --no-cpu-baseline

@@ -22,6 +22,7 @@ constexpr double kEps = 1.0 / (1 << 21);  // bound factor: 8x the float rounding
 struct Mesh {
     SkirtGridDesc g;
     std::vector<float> off;  // per list entry: float(site_nbr - site_own), 3 per entry
+    std::vector<float> nmax;  // per cell: the longest scaled offset of its list
 };
 
 double wallDist(const SkirtGridDesc& g, int mi, const double r[3], const double k[3]) {
@@ -63,6 +64,10 @@ int refStep(const SkirtGridDesc& g, int m, const double r[3], const double k[3],
 // operation adds at most a few 2^-24 of the sum of absolute terms, covered by kEpsF
 constexpr float kEpsF = 1.0f / (1 << 20);
 float gScale = 1.0f;
+bool gCell = false, gEntry = false;  // per-cell / per-entry-norm error bounds instead of the device's
+long gSignFallbacks = 0;  // re-evaluations with an entry whose n.k sign is uncertain
+long gWholeList = 0;      // re-evaluations over the whole list (more than 4 possible winners)
+float gLo[4096];          // the step's lower bounds, per list entry
 
 // compact step: the same result from float offsets, exact only for the winner (or all possible winners)
 int compactStep(const Mesh& M, int m, const double r[3], const double k[3], double& sq, long& fallbacks) {
@@ -79,7 +84,8 @@ int compactStep(const Mesh& M, int m, const double r[3], const double k[3], doub
             if (!(si > 0)) continue;
             lo = hi = si;
         } else {
-            const double nx = M.off[3 * (size_t)q], ny = M.off[3 * (size_t)q + 1], nz = M.off[3 * (size_t)q + 2];
+            const double nx = M.off[3 * (size_t)q] / gScale, ny = M.off[3 * (size_t)q + 1] / gScale,
+                         nz = M.off[3 * (size_t)q + 2] / gScale;
             const double den = nx * k[0] + ny * k[1] + nz * k[2];
             const double eA = kEps * (fabs(nx * k[0]) + fabs(ny * k[1]) + fabs(nz * k[2]));
             if (den <= -eA) continue;  // moving away for certain: si = 0
@@ -120,6 +126,8 @@ int compactStep(const Mesh& M, int m, const double r[3], const double k[3], doub
 }
 }  // namespace
 
+// the device's step (Grid<SKIRT_GRID_VORONOI>::step): every entry, walls included (stored as the bisector
+// plane with the site's mirror image), through the same branch-free bounds
 static int compactStepF(const Mesh& M, int m, const double r[3], const double k[3], double& sq, long& fallbacks) {
     const SkirtGridDesc& g = M.g;
     const double* pr = g.site + 3 * (size_t)m;
@@ -128,39 +136,34 @@ static int compactStepF(const Mesh& M, int m, const double r[3], const double k[
     const float kx = (float)k[0], ky = (float)k[1], kz = (float)k[2];
     float U = FLT_MAX, L1 = FLT_MAX, L2 = FLT_MAX;
     int w1 = -99;
+    // per-cell bounds (Cauchy-Schwarz over the longest offset of the cell)
+    const float nm = M.nmax.empty() ? 0.f : M.nmax[m];
+    const float eAc = kEpsF * nm, eBc = kEpsF * nm * (fabsf(Dx) + fabsf(Dy) + fabsf(Dz) + nm);
     for (int q = g.cell_nbr_offset[m]; q < g.cell_nbr_offset[m + 1]; q++) {
         const int mi = g.cell_nbr_list[q];
-        float lo, hi;
-        if (mi < 0) {
-            const double si = wallDist(g, mi, r, k);
-            if (!(si > 0)) continue;
-            const float v = (float)(si * gScale);
-            lo = v * (1.0f - kEpsF);
-            hi = v * (1.0f + kEpsF);
-        } else {
-            const float nx = M.off[3 * (size_t)q] * gScale, ny = M.off[3 * (size_t)q + 1] * gScale,
-                        nz = M.off[3 * (size_t)q + 2] * gScale;
-            const float den = nx * kx + ny * ky + nz * kz;
-            const float eA = kEpsF * (fabsf(nx * kx) + fabsf(ny * ky) + fabsf(nz * kz));
-            if (den <= -eA) continue;
-            const float tx = Dx + 0.5f * nx, ty = Dy + 0.5f * ny, tz = Dz + 0.5f * nz;
-            const float num = nx * tx + ny * ty + nz * tz;
-            const float eB = kEpsF * (fabsf(nx * tx) + fabsf(ny * ty) + fabsf(nz * tz) + 0.5f * (nx * nx + ny * ny + nz * nz));
-            if (den > 2 * eA) {
-                const float inv = 1.0f / den;
-                const float s = num * inv;
-                const float err = 2.0f * (eB + fabsf(s) * eA) * inv + fabsf(s) * kEpsF;
-                lo = s - err;
-                hi = s + err;
-                if (hi <= 0) continue;
-            } else {
-                lo = -FLT_MAX;
-                hi = FLT_MAX;
-            }
-        }
-        if (lo > 0 && hi < U) U = hi;
-        if (lo < L1) { L2 = L1; L1 = lo; w1 = mi; }
-        else if (lo < L2) L2 = lo;
+        const float nx = M.off[3 * (size_t)q], ny = M.off[3 * (size_t)q + 1], nz = M.off[3 * (size_t)q + 2];
+        const float ne = sqrtf(nx * nx + ny * ny + nz * nz);
+        const float px = nx * kx, py = ny * ky, pz = nz * kz;
+        const float den = px + py + pz;
+        const float eA = gEntry ? kEpsF * ne : gCell ? eAc : kEpsF * (fabsf(px) + fabsf(py) + fabsf(pz));
+        const float tx = Dx + 0.5f * nx, ty = Dy + 0.5f * ny, tz = Dz + 0.5f * nz;
+        const float qx = nx * tx, qy = ny * ty, qz = nz * tz;
+        const float num = qx + qy + qz;
+        const float eB = gEntry ? kEpsF * ne * (fabsf(Dx) + fabsf(Dy) + fabsf(Dz) + ne)
+                         : gCell ? eBc
+                                 : kEpsF * (fabsf(qx) + fabsf(qy) + fabsf(qz) + 0.5f * (nx * nx + ny * ny + nz * nz));
+        const float inv = 1.0f / den;
+        const float sa = num * inv;
+        const float err = 2.0f * (eB + fabsf(sa) * eA) * inv + fabsf(sa) * kEpsF;
+        const bool sure = den > 2.0f * eA;
+        const bool none = den <= -eA || (sure && !(sa + err > 0.f));
+        const float lo = none ? FLT_MAX : sure ? sa - err : -FLT_MAX;
+        const float hi = (none || !sure) ? FLT_MAX : sa + err;
+        gLo[q - g.cell_nbr_offset[m]] = lo;
+        U = fminf(U, lo > 0.f ? hi : FLT_MAX);
+        w1 = lo < L1 ? mi : w1;
+        L2 = fmaxf(fminf(L1, L2), fminf(fmaxf(L1, L2), lo));  // median of L1 <= L2 and lo
+        L1 = fminf(L1, lo);
     }
     if (L1 == FLT_MAX) { sq = DBL_MAX; return -99; }
     if (L2 > U) {
@@ -168,7 +171,19 @@ static int compactStepF(const Mesh& M, int m, const double r[3], const double k[
         return w1;
     }
     fallbacks++;
-    return refStep(g, m, r, k, sq);
+    if (L1 == -FLT_MAX) gSignFallbacks++;
+    // the possible winners (lower bound <= U), exactly, in list order; more than 4: the whole list
+    std::vector<int> cand;
+    for (int q = g.cell_nbr_offset[m]; q < g.cell_nbr_offset[m + 1]; q++)
+        if (gLo[q - g.cell_nbr_offset[m]] < FLT_MAX && gLo[q - g.cell_nbr_offset[m]] <= U) cand.push_back(g.cell_nbr_list[q]);
+    if (cand.size() > 4) { gWholeList++; return refStep(g, m, r, k, sq); }
+    sq = DBL_MAX;
+    int mq = -99;
+    for (int mi : cand) {
+        const double si = exactDist(g, m, mi, r, k);
+        if (si > 0 && si < sq) { sq = si; mq = mi; }
+    }
+    return mq;
 }
 
 int main(int argc, char** argv) {
@@ -188,19 +203,40 @@ int main(int argc, char** argv) {
     }
     const double ext[6] = {-L, -L, -L, L, L, L};
     gScale = (float)(1.0 / L);
-    const bool f32 = argc > 3 && argv[3][0] == 'f';
+    const bool f32 = argc > 3 && (argv[3][0] == 'f' || argv[3][0] == 'c' || argv[3][0] == 'e');
+    gCell = argc > 3 && argv[3][0] == 'c';
+    gEntry = argc > 3 && argv[3][0] == 'e';
+    if (gEntry) gCell = true;
     SkirtVoronoi* v = skirt_host_voronoi_build(sites.data(), N, ext);
     if (!v) { fprintf(stderr, "voronoi: %s\n", skirt_sim_error()); return 1; }
     Mesh M{};
     skirt_host_voronoi_describe(v, &M.g);
     const SkirtGridDesc& g = M.g;
     const int nn = g.cell_nbr_offset[N];
+    for (int m = 0; m < N; m++)
+        if (g.cell_nbr_offset[m + 1] - g.cell_nbr_offset[m] > 4096) { fprintf(stderr, "neighbour list too long\n"); return 1; }
     M.off.assign(3 * (size_t)nn, 0.f);
+    // scaled float offsets as the device stores them (engine.hip, Voronoi upload): walls as the offset to
+    // the site's mirror image
     for (int m = 0; m < N; m++)
         for (int q = g.cell_nbr_offset[m]; q < g.cell_nbr_offset[m + 1]; q++) {
             const int mi = g.cell_nbr_list[q];
-            if (mi < 0) continue;
-            for (int d = 0; d < 3; d++) M.off[3 * (size_t)q + d] = (float)(g.site[3 * (size_t)mi + d] - g.site[3 * (size_t)m + d]);
+            const double* sm = g.site + 3 * (size_t)m;
+            if (mi < 0) {
+                const int axis = (-mi - 1) / 2;
+                const double lim = (-mi - 1) % 2 ? g.extent[3 + axis] : g.extent[axis];
+                const double w = lim - sm[axis];
+                for (int d = 0; d < 3; d++) M.off[3 * (size_t)q + d] = 0.f;
+                M.off[3 * (size_t)q + axis] = w != 0.0 ? (float)(2.0 * w * gScale) : NAN;
+                continue;
+            }
+            for (int d = 0; d < 3; d++) M.off[3 * (size_t)q + d] = (float)((g.site[3 * (size_t)mi + d] - sm[d]) * gScale);
+        }
+    M.nmax.assign(N, 0.f);
+    for (int m = 0; m < N; m++)
+        for (int q = g.cell_nbr_offset[m]; q < g.cell_nbr_offset[m + 1]; q++) {
+            const float x = M.off[3 * (size_t)q], y = M.off[3 * (size_t)q + 1], z = M.off[3 * (size_t)q + 2];
+            M.nmax[m] = fmaxf(M.nmax[m], sqrtf(x * x + y * y + z * z) * (1.0f + 4 * FLT_EPSILON));
         }
     long steps = 0, fallbacks = 0, mismatches = 0;
     for (int i = 0; i < R; i++) {
@@ -220,8 +256,9 @@ int main(int argc, char** argv) {
             m = a;
         }
     }
-    printf("%s: sites %d, rays %d, steps %ld, exact re-evaluations %ld (%.3g per step), mismatches %ld\n", f32 ? "f32 bounds" : "f64 bounds", N, R, steps,
+    printf("%s: sites %d, rays %d, steps %ld, exact re-evaluations %ld (%.3g per step), mismatches %ld\n", gEntry ? "f32 per-entry norm bounds" : gCell ? "f32 per-cell bounds" : f32 ? "f32 bounds" : "f64 bounds", N, R, steps,
            fallbacks, (double)fallbacks / steps, mismatches);
+    if (f32) printf("  of which with an uncertain n.k sign: %ld; over the whole list: %ld\n", gSignFallbacks, gWholeList);
     skirt_host_voronoi_free(v);
     return mismatches ? 1 : 0;
 }
