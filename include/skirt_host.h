@@ -39,6 +39,11 @@ typedef struct {
  * seed != 0 overrides its random seed. datadir NULL = the packaged skirt_amd/data. Returns NULL on
  * failure (skirt_sim_error). */
 SkirtSim* skirt_sim_load(const char* ski, const char* datadir, double packages, uint64_t seed);
+/* As skirt_sim_load; setup_device >= 0 runs the setup's density sampling (tree subdivision and cell
+ * densities, the setup's hot loop) on that HIP device through skirt_mcrt_sample_density. The host still
+ * draws the reference's random numbers and takes the subdivision decisions; densities may differ from the
+ * host's by an ulp (the device's exp/pow/log10). -1: on the host, bit-identical to the reference. */
+SkirtSim* skirt_sim_load_ex(const char* ski, const char* datadir, double packages, uint64_t seed, int setup_device);
 int skirt_sim_info(SkirtSim* sim, SkirtSimInfo* info);
 /* The seed of the photon phases' Philox streams (default: the setup seed). The grid, densities and every
  * other setup draw stay those of the setup seed, so runs that differ only in this seed are independent
@@ -70,6 +75,8 @@ int skirt_sim_selfabs_totals(SkirtSim* sim, const double** totals);
 int skirt_sim_fetch(SkirtSim* sim);
 /* host accumulators after skirt_sim_fetch (same layouts as include/skirt_mcrt.h) */
 const double* skirt_sim_labs(SkirtSim* sim);
+/* the cell densities of the setup, ncells x ncomp row-major (DustSystem::_rhovv); NULL without dust */
+const double* skirt_sim_density(SkirtSim* sim);
 const double* skirt_sim_instrument(SkirtSim* sim, int i, int* nslots, int* nframe, int* has_frames, int* has_seds);
 /* replaces the host accumulators (e.g. after an all-reduce done by the caller) */
 int skirt_sim_set_tallies(SkirtSim* sim, const double* labs, const double* instr);

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define SKIRT_MCRT_ABI_VERSION 7
+#define SKIRT_MCRT_ABI_VERSION 8
 
 enum {
     SKIRT_OK = 0,
@@ -246,7 +246,7 @@ int skirt_mcrt_reduce_instruments(SkirtMcrt* ctx);
 int skirt_mcrt_upload_cell_sources(SkirtMcrt* ctx, const SkirtCellSourceDesc* src);
 /* The same cell sources computed on the device from the current Labs tally (plus the dust Labs when
  * include_dust): grey-body spectra at the cells' equilibrium temperatures, cell luminosities and their
- * per-wavelength cumulative distribution (at most 64 wavelengths). Asynchronous on the engine stream. */
+ * per-wavelength cumulative distribution. Asynchronous on the engine stream. */
 int skirt_mcrt_upload_emissivity(SkirtMcrt* ctx, const SkirtEmissivityDesc* emis);
 int skirt_mcrt_compute_cell_sources(SkirtMcrt* ctx, int include_dust);
 /* PanDustSystem::Labsdusttot of the device dust Labs (waits for the engine stream) */
@@ -257,6 +257,32 @@ int skirt_mcrt_bind_dust_labs(SkirtMcrt* ctx, double* d_labs_dust);
 int skirt_mcrt_zero_dust_labs(SkirtMcrt* ctx);
 int skirt_mcrt_download_dust_labs(SkirtMcrt* ctx, double* labs_dust);
 int skirt_mcrt_synchronize(SkirtMcrt* ctx);
+
+/* Setup: density sampling on a device (no engine context needed). The host keeps the reference's random
+ * stream (it draws the Mersenne-twister words in the reference's order) and the decisions; the device
+ * evaluates the dust density at `nsample` positions per item, box_min + u * (box_max - box_min) with
+ * u = word / (2^32 - 1) (MTRandom, Random::position(Box)), three words per position, and reduces them in
+ * sample order:
+ *   SKIRT_DENS_COMPONENTS  out[n x ncomp]: per component the sum of its density over the samples (the cell
+ *                          densities, DustSystem::setupSelfAfter, DustSystem.cpp:152-178)
+ *   SKIRT_DENS_NODE        out[n x 6]: {sum rho, sum rho x, sum rho y, sum rho z, min rho, max rho} of the
+ *                          total density (TreeNodeSampleDensityCalculator: mass, barycentre and density
+ *                          dispersion of a tree node, TreeDustGrid.cpp:174-222)
+ * The density of component h is norm[h] times its geometry's (PlummerGeometry / ExpDiskGeometry /
+ * SersicGeometry / PointGeometry::density), in the host's operation order; the device's exp, pow and log10
+ * may differ from the host's by an ulp. Synchronous. */
+enum { SKIRT_DENS_COMPONENTS = 0, SKIRT_DENS_NODE = 1 };
+typedef struct {
+    int ncomp;
+    const int* geom_kind;       /* ncomp, SKIRT_GEOM_* */
+    const double* geom_param;   /* ncomp x 8, laid out as SkirtSourceDesc::geom_param */
+    const double* norm;         /* ncomp: the component's normalization (its dust mass) */
+    const double* dens_table;   /* ncomp x 2*ntab (NULL if no SersicGeometry): SersicFunction s_i, then S(s_i) */
+    int ntab;
+} SkirtDensityDesc;
+int skirt_mcrt_sample_density(int device, const SkirtDensityDesc* dens, const double* boxes, size_t n,
+                              const uint32_t* words, int nsample, int mode, double* out);
+
 /* Copies tallies to host (Labs converted to row-major cell x wavelength); either pointer may be NULL.
  * With a reducer set, the instrument tallies are summed over the processes first. */
 int skirt_mcrt_download(SkirtMcrt* ctx, double* labs, double* instr);

@@ -66,6 +66,7 @@ ABI_SYMBOLS = [
     "skirt_mcrt_run_phase_shard", "skirt_mcrt_shard_slice", "skirt_mcrt_set_reducer", "skirt_mcrt_reduce_instruments",
     "skirt_sim_run_stellar_shard", "skirt_sim_run_dust_shard", "skirt_sim_set_photon_seed",
     "skirt_host_voronoi_build", "skirt_host_voronoi_describe", "skirt_host_voronoi_free",
+    "skirt_sim_load_ex", "skirt_mcrt_sample_density", "skirt_sim_density",
 ]
 
 _lib = None
@@ -87,6 +88,8 @@ def lib():
         vp, c_int, c_u64, c_dbl = ctypes.c_void_p, ctypes.c_int, ctypes.c_uint64, ctypes.c_double
         L.skirt_sim_load.restype = vp
         L.skirt_sim_load.argtypes = [ctypes.c_char_p, ctypes.c_char_p, c_dbl, c_u64]
+        L.skirt_sim_load_ex.restype = vp
+        L.skirt_sim_load_ex.argtypes = [ctypes.c_char_p, ctypes.c_char_p, c_dbl, c_u64, c_int]
         L.skirt_sim_info.argtypes = [vp, ctypes.POINTER(SkirtSimInfo)]
         L.skirt_sim_attach.argtypes = [vp, c_int]
         L.skirt_sim_engine.restype = vp
@@ -106,6 +109,8 @@ def lib():
         L.skirt_sim_labs_dust.argtypes = [vp]
         L.skirt_sim_selfabs_totals.argtypes = [vp, ctypes.POINTER(ctypes.POINTER(c_dbl))]
         L.skirt_sim_labs.restype = ctypes.POINTER(c_dbl)
+        L.skirt_sim_density.restype = ctypes.POINTER(c_dbl)
+        L.skirt_sim_density.argtypes = [vp]
         L.skirt_sim_labs.argtypes = [vp]
         L.skirt_sim_instrument.restype = ctypes.POINTER(c_dbl)
         L.skirt_sim_instrument.argtypes = [vp, c_int] + [ctypes.POINTER(c_int)] * 4
@@ -129,9 +134,12 @@ def lib():
 class Simulation:
     """One SKIRT simulation (a .ski file) driven through the native host library."""
 
-    def __init__(self, ski, packages=0.0, seed=0, datadir=None):
+    def __init__(self, ski, packages=0.0, seed=0, datadir=None, setup_device=None):
+        """setup_device: a HIP device for the setup's density sampling (tree subdivision, cell densities);
+        None keeps the setup on the host, bit-identical to the reference."""
         L = lib()
-        self._h = L.skirt_sim_load(os.fspath(ski).encode(), (datadir or DATA_DIR).encode(), float(packages), int(seed))
+        self._h = L.skirt_sim_load_ex(os.fspath(ski).encode(), (datadir or DATA_DIR).encode(), float(packages),
+                                      int(seed), -1 if setup_device is None else int(setup_device))
         if not self._h:
             raise SkirtError(L.skirt_sim_error().decode())
         info = SkirtSimInfo()
@@ -243,6 +251,13 @@ class Simulation:
         s = SkirtStats()
         self._check_engine(lib().skirt_mcrt_stats(self.engine, ctypes.byref(s)))
         return s.as_dict()
+
+    def density(self):
+        """The setup's cell densities [ncells, ncomp] (None without dust)."""
+        p = lib().skirt_sim_density(self._h)
+        if not p:
+            return None
+        return np.ctypeslib.as_array(p, shape=(self.info.ncells, self.info.ncomp)).copy()
 
     def labs(self):
         p = lib().skirt_sim_labs(self._h)

@@ -2843,6 +2843,104 @@ int ensureLeafMap(SkirtMcrt* c) {
     return SKIRT_OK;
 }
 
+// ================================================================== setup: density sampling
+// The setup's hot loop (skirt_mcrt_sample_density): one thread per item (a cell or a tree node), its
+// samples in order, so that every sum is accumulated as the host loop accumulates it (build.cpp cell
+// densities and tree subdivision). The geometry densities follow the host's Geometry::density operation
+// for operation (PlummerGeometry.cpp:49-54, ExpDiskGeometry::density, SersicGeometry::density with the
+// SersicFunction log-log interpolation, PointGeometry).
+struct DensArgs {
+    int ncomp, ntab, nsample, mode;
+    const int* kind;
+    const double* param;  // ncomp x 8
+    const double* norm;   // ncomp
+    const double* table;  // ncomp x 2 ntab
+    const double* boxes;  // n x 6
+    const uint32_t* words;
+    double* out;
+    size_t n;
+};
+
+__device__ double geomDensity(const DensArgs& d, int h, double x, double y, double z) {
+    const double* p = d.param + 8 * h;
+    switch (d.kind[h]) {
+    case SKIRT_GEOM_PLUMMER: {
+        const double r = sqrt(x * x + y * y + z * z);
+        const double s = r / p[0];
+        return p[1] * pow(1.0 + s * s, -2.5);
+    }
+    case SKIRT_GEOM_EXPDISK: {
+        const double R = sqrt(x * x + y * y);
+        const double absz = fabs(z);
+        const double hR = p[0], hz = p[1], Rmax = p[2], zmax = p[3], Rmin = p[4], rho0 = p[5];
+        if (Rmax > 0.0 && R > Rmax) return 0.0;
+        if (zmax > 0.0 && absz > zmax) return 0.0;
+        if (R < Rmin) return 0.0;
+        return rho0 * exp(-R / hR) * exp(-absz / hz);
+    }
+    case SKIRT_GEOM_SERSIC: {
+        const double r = sqrt(x * x + y * y + z * z);
+        const double s = r / p[0];
+        const double* sv = d.table + (size_t)2 * d.ntab * h;
+        const double* Sv = sv + d.ntab;
+        const int Ns = d.ntab;
+        if (s <= sv[0]) return p[2] * Sv[0];
+        if (s >= sv[Ns - 1]) return p[2] * Sv[Ns - 1];
+        int jl = -1, ju = Ns - 1;  // NR::locate_clip (s >= sv[0] here)
+        while (ju - jl > 1) {
+            const int jm = (ju + jl) >> 1;
+            if (s < sv[jm]) ju = jm;
+            else jl = jm;
+        }
+        // NR::interpolate_loglog
+        const double lx = log10(s), x1 = log10(sv[jl]), x2 = log10(sv[jl + 1]);
+        double f1 = Sv[jl], f2 = Sv[jl + 1];
+        const bool logf = f1 > 0 && f2 > 0;
+        if (logf) { f1 = log10(f1); f2 = log10(f2); }
+        double fx = f1 + ((lx - x1) / (x2 - x1)) * (f2 - f1);
+        if (logf) fx = pow(10.0, fx);
+        return p[2] * fx;
+    }
+    default:  // SKIRT_GEOM_POINT
+        return (x * x + y * y + z * z) == 0 ? INFINITY : 0.0;
+    }
+}
+
+__global__ void __launch_bounds__(kBlock) densitySampleKernel(const DensArgs d) {
+    const size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= d.n) return;
+    const double* b = d.boxes + 6 * q;
+    const uint32_t* w = d.words + (size_t)3 * d.nsample * q;
+    constexpr double kWordMax = 4294967295.0;  // MTRandom::deviate
+    if (d.mode == SKIRT_DENS_COMPONENTS) {
+        double* o = d.out + (size_t)d.ncomp * q;
+        for (int h = 0; h < d.ncomp; h++) o[h] = 0.0;
+        for (int k = 0; k < d.nsample; k++) {
+            const double fx = (double)w[3 * k] / kWordMax, fy = (double)w[3 * k + 1] / kWordMax,
+                         fz = (double)w[3 * k + 2] / kWordMax;
+            const double x = b[0] + fx * (b[3] - b[0]), y = b[1] + fy * (b[4] - b[1]), z = b[2] + fz * (b[5] - b[2]);
+            for (int h = 0; h < d.ncomp; h++) o[h] += d.norm[h] * geomDensity(d, h, x, y, z);
+        }
+    } else {
+        double sum = 0, sx = 0, sy = 0, sz = 0, mn = 0, mx = 0;
+        for (int k = 0; k < d.nsample; k++) {
+            const double fx = (double)w[3 * k] / kWordMax, fy = (double)w[3 * k + 1] / kWordMax,
+                         fz = (double)w[3 * k + 2] / kWordMax;
+            const double x = b[0] + fx * (b[3] - b[0]), y = b[1] + fy * (b[4] - b[1]), z = b[2] + fz * (b[5] - b[2]);
+            double rho = 0;
+            for (int h = 0; h < d.ncomp; h++) rho += d.norm[h] * geomDensity(d, h, x, y, z);
+            sum += rho;
+            sx += rho * x;
+            sy += rho * y;
+            sz += rho * z;
+            if (k == 0 || rho < mn) mn = rho;  // std::min_element / max_element: the first extreme
+            if (k == 0 || mx < rho) mx = rho;
+        }
+        double* o = d.out + 6 * q;
+        o[0] = sum; o[1] = sx; o[2] = sy; o[3] = sz; o[4] = mn; o[5] = mx;
+    }
+}
+
 }  // namespace
 
 extern "C" {
@@ -3922,6 +4020,72 @@ void skirt_mcrt_destroy(SkirtMcrt* c) {
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->own) (void)hipStreamDestroy(c->own);
     delete c;
+}
+
+int skirt_mcrt_sample_density(int device, const SkirtDensityDesc* dens, const double* boxes, size_t n,
+                              const uint32_t* words, int nsample, int mode, double* out) {
+    if (!dens || dens->ncomp < 1 || !dens->geom_kind || !dens->geom_param || !dens->norm || nsample < 1 ||
+        (mode != SKIRT_DENS_COMPONENTS && mode != SKIRT_DENS_NODE) || (n && (!boxes || !words || !out)))
+        return SKIRT_ERR_ARG;
+    for (int h = 0; h < dens->ncomp; h++) {
+        const int k = dens->geom_kind[h];
+        if (k < SKIRT_GEOM_PLUMMER || k > SKIRT_GEOM_POINT) return SKIRT_ERR_ARG;
+        if (k == SKIRT_GEOM_SERSIC && (!dens->dens_table || dens->ntab < 2)) return SKIRT_ERR_ARG;
+    }
+    if (n == 0) return SKIRT_OK;
+    const size_t nout = n * (mode == SKIRT_DENS_NODE ? 6 : (size_t)dens->ncomp);
+    const size_t nw = n * 3 * (size_t)nsample;
+    const size_t ntable = dens->dens_table ? (size_t)2 * dens->ntab * dens->ncomp : 0;
+    if (hipSetDevice(device) != hipSuccess) return SKIRT_ERR_HIP;
+    hipStream_t st = nullptr;
+    char* buf = nullptr;
+    // one allocation: parameters, boxes, words, output
+    const size_t offParam = 0, offNorm = offParam + 8 * (size_t)dens->ncomp * sizeof(double);
+    const size_t offKind = offNorm + (size_t)dens->ncomp * sizeof(double);
+    const size_t offTable = (offKind + (size_t)dens->ncomp * sizeof(int) + 15) & ~(size_t)15;
+    const size_t offBoxes = (offTable + ntable * sizeof(double) + 15) & ~(size_t)15;
+    const size_t offOut = (offBoxes + 6 * n * sizeof(double) + 15) & ~(size_t)15;
+    const size_t offWords = (offOut + nout * sizeof(double) + 15) & ~(size_t)15;
+    const size_t total = offWords + nw * sizeof(uint32_t);
+    int rc = SKIRT_OK;
+    if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return SKIRT_ERR_HIP;
+    if (hipMalloc(&buf, total) != hipSuccess) {
+        (void)hipStreamDestroy(st);
+        return SKIRT_ERR_HIP;
+    }
+    DensArgs d{};
+    d.ncomp = dens->ncomp;
+    d.ntab = dens->ntab;
+    d.nsample = nsample;
+    d.mode = mode;
+    d.param = reinterpret_cast<const double*>(buf + offParam);
+    d.norm = reinterpret_cast<const double*>(buf + offNorm);
+    d.kind = reinterpret_cast<const int*>(buf + offKind);
+    d.table = ntable ? reinterpret_cast<const double*>(buf + offTable) : nullptr;
+    d.boxes = reinterpret_cast<const double*>(buf + offBoxes);
+    d.out = reinterpret_cast<double*>(buf + offOut);
+    d.words = reinterpret_cast<const uint32_t*>(buf + offWords);
+    d.n = n;
+    const size_t nblocks = (n + kBlock - 1) / kBlock;
+    if (hipMemcpyAsync(buf + offParam, dens->geom_param, 8 * (size_t)dens->ncomp * sizeof(double), hipMemcpyHostToDevice, st) != hipSuccess ||
+        hipMemcpyAsync(buf + offNorm, dens->norm, (size_t)dens->ncomp * sizeof(double), hipMemcpyHostToDevice, st) != hipSuccess ||
+        hipMemcpyAsync(buf + offKind, dens->geom_kind, (size_t)dens->ncomp * sizeof(int), hipMemcpyHostToDevice, st) != hipSuccess ||
+        (ntable && hipMemcpyAsync(buf + offTable, dens->dens_table, ntable * sizeof(double), hipMemcpyHostToDevice, st) != hipSuccess) ||
+        hipMemcpyAsync(buf + offBoxes, boxes, 6 * n * sizeof(double), hipMemcpyHostToDevice, st) != hipSuccess ||
+        hipMemcpyAsync(buf + offWords, words, nw * sizeof(uint32_t), hipMemcpyHostToDevice, st) != hipSuccess ||
+        nblocks > 0x7fffffffu) {
+        rc = SKIRT_ERR_HIP;
+    } else {
+        hipLaunchKernelGGL(densitySampleKernel, dim3((unsigned)nblocks), dim3(kBlock), 0, st, d);
+        if (hipGetLastError() != hipSuccess ||
+            hipMemcpyAsync(out, buf + offOut, nout * sizeof(double), hipMemcpyDeviceToHost, st) != hipSuccess ||
+            hipStreamSynchronize(st) != hipSuccess)
+            rc = SKIRT_ERR_HIP;
+    }
+    (void)hipStreamSynchronize(st);
+    (void)hipFree(buf);
+    (void)hipStreamDestroy(st);
+    return rc;
 }
 
 }  // extern "C"

@@ -19,6 +19,7 @@
 #include <cstring>
 #include <dlfcn.h>
 #include <fstream>
+#include <memory>
 #include <numeric>
 #include <sstream>
 #include <stdexcept>
@@ -454,7 +455,46 @@ struct Ctx {
     Units units;
     std::string datadir;
     UniformSource* rng;
+    DensitySampler* sampler = nullptr;  // device density sampling (null: host threads)
 };
+
+// The density sampling of n items on the sampler's device, when there is one and the setup stream is the
+// Mersenne twister: item q gets the 3 * nsample words the sequential loop would draw for it, in item
+// order; the items go in chunks, the next chunk's words drawn while the device samples the current one.
+// box(q, b) fills item q's box, apply(q, out) takes its sums. False: no device sampling (nothing drawn).
+template <class BoxFn, class ApplyFn>
+bool deviceSampling(const Ctx& c, const std::vector<DustComp>& dust, size_t n, int nsample, int mode, BoxFn box,
+                    ApplyFn apply) {
+    MTRandom* mt = dynamic_cast<MTRandom*>(c.rng);
+    if (!c.sampler || !mt || n == 0) return false;
+    const size_t per = 3 * (size_t)nsample;
+    const size_t chunk = std::max<size_t>(1, ((size_t)1 << 26) / per);  // 64 Mi words (256 MiB) per call
+    const size_t nout = mode == kDensNode ? 6 : dust.size();
+    std::vector<uint32_t> w[2];
+    std::vector<double> boxes, out;
+    auto draw = [&](int k, size_t q0) {
+        w[k].resize((std::min(n, q0 + chunk) - q0) * per);
+        mt->words(w[k].data(), w[k].size());
+    };
+    draw(0, 0);
+    for (size_t q0 = 0, k = 0; q0 < n; q0 += chunk, k ^= 1) {
+        const size_t q1 = std::min(n, q0 + chunk);
+        std::thread next;
+        if (q1 < n) next = std::thread(draw, (int)(k ^ 1), q1);
+        try {
+            boxes.resize(6 * (q1 - q0));
+            for (size_t q = q0; q < q1; q++) box(q, &boxes[6 * (q - q0)]);
+            out.resize(nout * (q1 - q0));
+            c.sampler->sample(dust, boxes.data(), q1 - q0, w[k].data(), nsample, mode, out.data());
+            for (size_t q = q0; q < q1; q++) apply(q, &out[nout * (q - q0)]);
+        } catch (...) {
+            if (next.joinable()) next.join();
+            throw;
+        }
+        if (next.joinable()) next.join();
+    }
+    return true;
+}
 
 double attr(const Ctx& c, const XmlElement* e, const char* key, const char* qty, double def) {
     if (!e->has(key)) return def;
@@ -1051,6 +1091,7 @@ void buildOctree(const Ctx& c, const XmlElement* e, const Model& model, OctreeGr
     // node order (parallelDraws), the subdivisions are then applied in node order, so that every node
     // number and every random draw is the reference's.
     const bool always = maxOpticalDepth == 0 && maxMassFraction == 0 && maxDensDispFraction == 0;
+    std::unique_ptr<StageTimer> stage(new StageTimer("octree subdivision"));
     for (size_t l0 = 0; l0 < t.firstChild.size();) {
         const size_t l1 = t.firstChild.size();
         std::vector<int> sampled;  // nodes that sample the density, in node order
@@ -1059,7 +1100,28 @@ void buildOctree(const Ctx& c, const XmlElement* e, const Model& model, OctreeGr
         std::vector<char> divide(l1 - l0, 0);
         std::vector<std::array<double, 3>> bc(bary ? l1 - l0 : 0);  // sampled barycentres
         for (size_t l = l0; l < l1; l++) divide[l - l0] = t.level[l] <= t.minLevel;
-        parallelDraws(*c.rng, sampled.size(), 3 * Nrandom, [&](size_t q, const double* u) {
+        // the subdivision criteria of a sampled node from its mass, barycentre and density range
+        auto decide = [&](int l, double sumrho, double sx, double sy, double sz, double mn, double mx) {
+            const double* b = tb.box(l);
+            if (bary) bc[l - l0] = {sx / sumrho, sy / sumrho, sz / sumrho};
+            double vol = (b[3] - b[0]) * (b[4] - b[1]) * (b[5] - b[2]);
+            double mass = sumrho / Nrandom * vol;
+            bool needDivision = always;
+            if (!needDivision && maxMassFraction > 0 && mass / totalmass >= maxMassFraction) needDivision = true;
+            if (!needDivision && maxOpticalDepth > 0 &&
+                constants::kappaV * mass / std::pow(vol, 2. / 3.) >= maxOpticalDepth)
+                needDivision = true;
+            if (!needDivision && maxDensDispFraction > 0) {
+                double disp = mx > 0 ? (mx - mn) / mx : 0;
+                if (disp >= maxDensDispFraction) needDivision = true;
+            }
+            divide[l - l0] = needDivision;
+        };
+        const bool onDevice = deviceSampling(
+            c, model.dust, sampled.size(), Nrandom, kDensNode,
+            [&](size_t q, double* b) { std::memcpy(b, tb.box(sampled[q]), 6 * sizeof(double)); },
+            [&](size_t q, const double* o) { decide(sampled[q], o[0], o[1], o[2], o[3], o[4], o[5]); });
+        if (!onDevice) parallelDraws(*c.rng, sampled.size(), 3 * Nrandom, [&](size_t q, const double* u) {
             // TreeNodeSampleDensityCalculator: Nrandom positions in the node, density of all components
             const int l = sampled[q];
             double b[6];
@@ -1077,21 +1139,9 @@ void buildOctree(const Ctx& c, const XmlElement* e, const Model& model, OctreeGr
                 sy += rho * y;
                 sz += rho * z;
             }
-            if (bary) bc[l - l0] = {sx / sumrho, sy / sumrho, sz / sumrho};
-            double vol = (b[3] - b[0]) * (b[4] - b[1]) * (b[5] - b[2]);
-            double mass = nr::sum(rhov) / Nrandom * vol;
-            bool needDivision = always;
-            if (!needDivision && maxMassFraction > 0 && mass / totalmass >= maxMassFraction) needDivision = true;
-            if (!needDivision && maxOpticalDepth > 0 &&
-                constants::kappaV * mass / std::pow(vol, 2. / 3.) >= maxOpticalDepth)
-                needDivision = true;
-            if (!needDivision && maxDensDispFraction > 0) {
-                double mn = *std::min_element(rhov.begin(), rhov.end());
-                double mx = *std::max_element(rhov.begin(), rhov.end());
-                double disp = mx > 0 ? (mx - mn) / mx : 0;
-                if (disp >= maxDensDispFraction) needDivision = true;
-            }
-            divide[l - l0] = needDivision;
+            // sumrho is nr::sum(rhov): the same values accumulated in the same order
+            decide(l, sumrho, sx, sy, sz, *std::min_element(rhov.begin(), rhov.end()),
+                   *std::max_element(rhov.begin(), rhov.end()));
         });
         for (size_t l = l0; l < l1; l++) {
             if (!divide[l - l0]) continue;
@@ -1120,6 +1170,7 @@ void buildOctree(const Ctx& c, const XmlElement* e, const Model& model, OctreeGr
         }
         l0 = l1;
     }
+    stage.reset(new StageTimer("octree neighbours"));
     int Nnodes = t.nnodes();
     t.cellnumber.assign(Nnodes, -1);
     t.idv.clear();
@@ -1135,7 +1186,20 @@ void buildOctree(const Ctx& c, const XmlElement* e, const Model& model, OctreeGr
         if (binary) tb.addneighborsBin(l);
         else tb.addneighbors(l);
     }
-    for (int l = 0; l < Nnodes; l++) tb.sortneighbors(l);
+    {
+        // every node's lists sort on their own (TreeNode::sortneighbors): worker threads over node ranges
+        stage.reset(new StageTimer("octree neighbour sort"));
+        const int T = std::max(1, std::min(16, (int)std::thread::hardware_concurrency()));
+        std::atomic<int> next{0};
+        std::vector<std::thread> th;
+        for (int w = 0; w < T; w++)
+            th.emplace_back([&] {
+                for (int l0; (l0 = next.fetch_add(4096)) < Nnodes;)
+                    for (int l = l0; l < std::min(Nnodes, l0 + 4096); l++) tb.sortneighbors(l);
+            });
+        for (auto& x : th) x.join();
+    }
+    stage.reset(new StageTimer("octree neighbour CSR"));
     t.nbrOffset.assign(6 * (size_t)Nnodes + 1, 0);
     size_t total = 0;
     for (size_t q = 0; q < 6 * (size_t)Nnodes; q++) total += tb.nb[q].size();
@@ -1281,7 +1345,7 @@ static void buildVoronoiGrid(const Ctx& c, const XmlElement* ge, Model& m, Unifo
     buildVoronoi(m.grid.vor, sites, xmin, xmax, ymin, ymax, zmin, zmax);
 }
 
-Model loadSki(const std::string& path, UniformSource& rng, const std::string& datadir) {
+Model loadSki(const std::string& path, UniformSource& rng, const std::string& datadir, DensitySampler* sampler) {
     auto doc = parseXmlFile(path);
     if (doc->children.empty()) throw std::runtime_error("empty ski file");
     const XmlElement* sim = doc->children.front().get();
@@ -1292,7 +1356,7 @@ Model loadSki(const std::string& path, UniformSource& rng, const std::string& da
 
     const XmlElement* unitsEl = sim->item("units");
     m.units_system = unitsEl ? unitsEl->name : "ExtragalacticUnits";
-    Ctx c{Units(m.units_system), datadir, &rng};
+    Ctx c{Units(m.units_system), datadir, &rng, sampler};
 
     if (const XmlElement* r = sim->item("random")) m.seed = (unsigned long)attrInt(r, "seed", 4357);
     m.packages = attr(c, sim, "packages", "", 1e6);
@@ -1501,7 +1565,13 @@ Model loadSki(const std::string& path, UniformSource& rng, const std::string& da
             }
         } else {
             // Random::position(box) per sample: three deviates, drawn ahead in cell order
-            parallelDraws(rng, (size_t)Ncells, 3 * m.sampleCount, [&](size_t cell, const double* u) {
+            const bool onDevice = deviceSampling(
+                c, m.dust, (size_t)Ncells, m.sampleCount, kDensComponents,
+                [&](size_t cell, double* b) { m.grid.cellBox((int)cell, b); },
+                [&](size_t cell, const double* sumv) {
+                    for (int h = 0; h < Ncomp; h++) m.rho[cell * Ncomp + h] = 1.0 * sumv[h] / m.sampleCount;
+                });
+            if (!onDevice) parallelDraws(rng, (size_t)Ncells, 3 * m.sampleCount, [&](size_t cell, const double* u) {
                 double b[6];
                 m.grid.cellBox((int)cell, b);
                 std::vector<double> sumv(Ncomp, 0.0);

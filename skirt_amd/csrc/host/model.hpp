@@ -239,9 +239,22 @@ struct Model {
     double kapparho(int m, int ell) const;
 };
 
+// The setup's density sampling on a device (skirt_mcrt_sample_density, supplied by the product library):
+// for n boxes (6 doubles each) and 3 * nsample Mersenne-twister words per box, the sums of mode
+// kDensComponents (ncomp per box) or kDensNode (6 per box). Throws on failure.
+enum DensityMode : int { kDensComponents = 0, kDensNode = 1 };  // SKIRT_DENS_COMPONENTS, SKIRT_DENS_NODE
+struct DensitySampler {
+    virtual ~DensitySampler() = default;
+    virtual void sample(const std::vector<DustComp>& dust, const double* boxes, size_t n, const uint32_t* words,
+                        int nsample, int mode, double* out) = 0;
+};
+
 // Builds the model from a .ski file; `rng` supplies the setup random numbers (octree subdivision
-// sampling, cell density sampling) in the reference's order. `datadir` holds SunSED.bin etc.
-Model loadSki(const std::string& path, UniformSource& rng, const std::string& datadir);
+// sampling, cell density sampling) in the reference's order. `datadir` holds SunSED.bin etc. With a
+// sampler (and a Mersenne-twister rng), the density sampling of the tree subdivision and of the cell
+// densities runs on its device; the host still draws every random number and takes every decision.
+Model loadSki(const std::string& path, UniformSource& rng, const std::string& datadir,
+              DensitySampler* sampler = nullptr);
 
 // directory holding the packaged resource tables (skirt_amd/data), located relative to this library
 std::string defaultDataDir();

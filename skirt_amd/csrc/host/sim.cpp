@@ -1,4 +1,5 @@
 // Host driver: .ski -> Model -> device engine -> outputs (include/skirt_host.h).
+#include <algorithm>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -69,13 +70,70 @@ extern "C" {
 
 const char* skirt_sim_error(void) { return g_err.c_str(); }
 
+namespace {
+// SkirtGeometry parameters as SkirtSourceDesc::geom_param lays them out; returns the SKIRT_GEOM_* kind
+int packGeometry(const Geometry& g, double* p) {
+    for (int q = 0; q < 8; q++) p[q] = 0.0;
+    switch (g.kind) {
+    case GeometryKind::Point: return SKIRT_GEOM_POINT;
+    case GeometryKind::Sersic: p[0] = g.reff; p[1] = g.n; p[2] = g.rho0; return SKIRT_GEOM_SERSIC;
+    case GeometryKind::ExpDisk: {
+        const double v[6] = {g.hR, g.hz, g.Rmax, g.zmax, g.Rmin, g.rho0};
+        for (int q = 0; q < 6; q++) p[q] = v[q];
+        return SKIRT_GEOM_EXPDISK;
+    }
+    default: p[0] = g.c; p[1] = g.rho0; return SKIRT_GEOM_PLUMMER;
+    }
+}
+
+static_assert((int)kDensComponents == (int)SKIRT_DENS_COMPONENTS && (int)kDensNode == (int)SKIRT_DENS_NODE,
+              "density sampling modes");
+
+// the setup's density sampling on a HIP device through skirt_mcrt_sample_density
+struct DeviceDensitySampler final : DensitySampler {
+    int device;
+    explicit DeviceDensitySampler(int d) : device(d) {}
+    void sample(const std::vector<DustComp>& dust, const double* boxes, size_t n, const uint32_t* words, int nsample,
+                int mode, double* out) override {
+        const int nc = (int)dust.size();
+        std::vector<int> kind(nc);
+        std::vector<double> param(8 * (size_t)nc), norm(nc), table;
+        int ntab = 0;
+        for (int h = 0; h < nc; h++)
+            if (dust[h].geom.kind == GeometryKind::Sersic) ntab = std::max(ntab, (int)dust[h].geom.sv.size());
+        if (ntab) table.assign(2 * (size_t)ntab * nc, 0.0);
+        for (int h = 0; h < nc; h++) {
+            const Geometry& g = dust[h].geom;
+            kind[h] = packGeometry(g, &param[8 * (size_t)h]);
+            norm[h] = dust[h].nf;
+            if (g.kind == GeometryKind::Sersic) {
+                if ((int)g.sv.size() != ntab || g.Sv.size() != g.sv.size())
+                    throw std::runtime_error("Sersic density tables of unequal lengths");
+                std::copy(g.sv.begin(), g.sv.end(), table.begin() + 2 * (size_t)ntab * h);
+                std::copy(g.Sv.begin(), g.Sv.end(), table.begin() + 2 * (size_t)ntab * h + ntab);
+            }
+        }
+        const SkirtDensityDesc d{nc, kind.data(), param.data(), norm.data(), ntab ? table.data() : nullptr, ntab};
+        const int rc = skirt_mcrt_sample_density(device, &d, boxes, n, words, nsample, mode, out);
+        if (rc) throw std::runtime_error("density sampling on device " + std::to_string(device) + " failed (error " +
+                                         std::to_string(rc) + ")");
+    }
+};
+}  // namespace
+
 SkirtSim* skirt_sim_load(const char* ski, const char* datadir, double packages, uint64_t seed) {
+    return skirt_sim_load_ex(ski, datadir, packages, seed, -1);
+}
+
+SkirtSim* skirt_sim_load_ex(const char* ski, const char* datadir, double packages, uint64_t seed, int setup_device) {
     try {
         auto s = std::make_unique<SkirtSim>();
         auto t0 = std::chrono::steady_clock::now();
         unsigned long theSeed = seed ? (unsigned long)seed : readSkiSeed(ski);
         MTRandom mt(theSeed);  // setup draws exactly like the reference (density / tree sampling)
-        s->m = loadSki(ski, mt, datadir && *datadir ? datadir : defaultDataDir());
+        std::unique_ptr<DeviceDensitySampler> sampler;
+        if (setup_device >= 0) sampler.reset(new DeviceDensitySampler(setup_device));
+        s->m = loadSki(ski, mt, datadir && *datadir ? datadir : defaultDataDir(), sampler.get());
         s->m.seed = theSeed;
         if (packages > 0) s->m.packages = packages;
         s->npp = (uint64_t)std::ceil(s->m.packages);
@@ -173,23 +231,13 @@ int skirt_sim_attach(SkirtSim* s, int device) {
     std::vector<double> gp(8 * ns, 0.0), lum(ns * Nl), cdf(Nl * (ns + 1)), gt;
     for (int h = 0; h < ns; h++) {
         const Geometry& g = m.starGeom[h];
-        if (g.kind == GeometryKind::Point) {
-            gk[h] = SKIRT_GEOM_POINT;
-        } else if (g.kind == GeometryKind::Sersic) {
-            gk[h] = SKIRT_GEOM_SERSIC;
-            gp[8 * h] = g.reff; gp[8 * h + 1] = g.n; gp[8 * h + 2] = g.rho0;
+        gk[h] = packGeometry(g, &gp[8 * h]);
+        if (g.kind == GeometryKind::Sersic) {
             gt.resize(202 * (size_t)ns, 0.0);
             for (int q = 0; q < 101; q++) {
                 gt[202 * (size_t)h + q] = g.sv[q];
                 gt[202 * (size_t)h + 101 + q] = g.Mv[q];
             }
-        } else if (g.kind == GeometryKind::ExpDisk) {
-            gk[h] = SKIRT_GEOM_EXPDISK;
-            const double v[6] = {g.hR, g.hz, g.Rmax, g.zmax, g.Rmin, g.rho0};
-            for (int q = 0; q < 6; q++) gp[8 * h + q] = v[q];
-        } else {
-            gp[8 * h] = g.c;
-            gp[8 * h + 1] = g.rho0;
         }
         for (int ell = 0; ell < Nl; ell++) lum[h * Nl + ell] = m.starL[h][ell];
     }
@@ -362,6 +410,7 @@ int skirt_sim_fetch(SkirtSim* s) {
 }
 
 const double* skirt_sim_labs(SkirtSim* s) { return s && !s->labs.empty() ? s->labs.data() : nullptr; }
+const double* skirt_sim_density(SkirtSim* s) { return s && !s->m.rho.empty() ? s->m.rho.data() : nullptr; }
 
 const double* skirt_sim_instrument(SkirtSim* s, int i, int* nslots, int* nframe, int* hasFrames, int* hasSeds) {
     if (!s || i < 0 || i >= (int)s->m.instruments.size()) return nullptr;
