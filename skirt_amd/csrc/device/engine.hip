@@ -523,27 +523,24 @@ struct Grid<SKIRT_GRID_CARTESIAN> {
         const double dsx = (r.ix != 0.0) ? (xE - r.x) * r.ix : kDblMax;
         const double dsy = (r.iy != 0.0) ? (yE - r.y) * r.iy : kDblMax;
         const double dsz = (r.iz != 0.0) ? (zE - r.z) * r.iz : kDblMax;
-        if (dsx <= dsy && dsx <= dsz) {
-            if (!seg(m, rho0, dsx)) return false;
-            const int ni = i + ((r.dx < 0.0) ? -1 : 1);
-            if (ni >= a.nx || ni < 0) return false;
-            r.ci = ni; r.x = xE; r.y += r.dy * dsx; r.z += r.dz * dsx;
-        } else if (dsy < dsx && dsy <= dsz) {
-            if (!seg(m, rho0, dsy)) return false;
-            const int nj = j + ((r.dy < 0.0) ? -1 : 1);
-            if (nj >= a.ny || nj < 0) return false;
-            r.cj = nj; r.x += r.dx * dsy; r.y = yE; r.z += r.dz * dsy;
-        } else if (dsz < dsx && dsz < dsy) {
-            if (!seg(m, rho0, dsz)) return false;
-            const int nk = k + ((r.dz < 0.0) ? -1 : 1);
-            if (nk >= a.nz || nk < 0) return false;
-            r.ck = nk; r.x += r.dx * dsz; r.y += r.dy * dsz; r.z = zE;
-        } else {
-            return false;  // NaN direction; the reference would loop forever
-        }
+        // the exit wall (the reference's order of comparisons), then one segment: lanes leaving through
+        // different walls share the segment code instead of running it once per wall
+        const bool ex = dsx <= dsy && dsx <= dsz;
+        const bool ey = !ex && dsy < dsx && dsy <= dsz;
+        const bool ez = !ex && !ey && dsz < dsx && dsz < dsy;
+        if (!(ex || ey || ez)) return false;  // NaN direction; the reference would loop forever
+        const double ds = ex ? dsx : ey ? dsy : dsz;
+        if (!seg(m, rho0, ds)) return false;
+        const int ni = i + (ex ? ((r.dx < 0.0) ? -1 : 1) : 0);
+        const int nj = j + (ey ? ((r.dy < 0.0) ? -1 : 1) : 0);
+        const int nk = k + (ez ? ((r.dz < 0.0) ? -1 : 1) : 0);
+        if (ni >= a.nx || ni < 0 || nj >= a.ny || nj < 0 || nk >= a.nz || nk < 0) return false;
+        r.ci = ni; r.cj = nj; r.ck = nk;
+        r.x = ex ? xE : r.x + r.dx * ds;
+        r.y = ey ? yE : r.y + r.dy * ds;
+        r.z = ez ? zE : r.z + r.dz * ds;
         return true;
     }
-
 
     __device__ static __forceinline__ int whichcell(const Args& a, const Shared& sh, double x, double y, double z) {
         const double* xv = sh.mesh;
