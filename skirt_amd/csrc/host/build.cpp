@@ -1552,16 +1552,76 @@ Model loadSki(const std::string& path, UniformSource& rng, const std::string& da
         for (int cell = 0; cell < Ncells; cell++) m.volume[cell] = m.grid.cellVolume(cell);
         m.rho.assign((size_t)Ncells * Ncomp, 0.0);
         if (m.grid.kind == GridKind::Voronoi) {
-            // rejection sampling draws a data-dependent number of deviates: one cell after the other
-            std::vector<double> sumv(Ncomp);
-            for (int cell = 0; cell < Ncells; cell++) {
-                std::fill(sumv.begin(), sumv.end(), 0.0);
-                for (int n = 0; n < m.sampleCount; n++) {
-                    double x, y, z;
-                    voronoiRandomPosition(m.grid.vor, rng, cell, x, y, z);  // VoronoiMesh::randomPosition
-                    for (int h = 0; h < Ncomp; h++) sumv[h] += m.dust[h].density(x, y, z);
+            // rejection sampling draws a data-dependent number of deviates, so the positions are drawn one
+            // cell after the other (VoronoiMesh::randomPosition, the cell's neighbour sites gathered once);
+            // their densities are then summed, in sample order, on worker threads, a chunk of cells at a time
+            const VoronoiGrid& g = m.grid.vor;
+            const int ns = m.sampleCount;
+            MTRandom* mtr = dynamic_cast<MTRandom*>(&rng);  // a final class: its uniform() inlines
+            auto uniform = [&]() { return mtr ? mtr->uniform() : rng.uniform(); };
+            const int chunk = std::max(1, (1 << 22) / std::max(1, ns));
+            std::vector<double> pos, nb;
+            for (int c0 = 0; c0 < Ncells; c0 += chunk) {
+                const int c1 = std::min(Ncells, c0 + chunk);
+                pos.resize(3 * (size_t)(c1 - c0) * ns);
+                std::unique_ptr<StageTimer> pst(new StageTimer("voronoi positions"));
+                for (int cell = c0; cell < c1; cell++) {
+                    nb.clear();
+                    for (int q = g.nbrOffset[cell]; q < g.nbrOffset[cell + 1]; q++) {
+                        const int id = g.nbrList[q];
+                        if (id >= 0) nb.insert(nb.end(), &g.site[3 * (size_t)id], &g.site[3 * (size_t)id] + 3);
+                    }
+                    const double* b = &g.bbox[6 * (size_t)cell];
+                    const double* sc = &g.site[3 * (size_t)cell];
+                    const size_t nn = nb.size() / 3;
+                    for (int n = 0; n < ns; n++) {
+                        double x = 0, y = 0, z = 0;
+                        bool in = false;
+                        for (int t = 0; t < 10000 && !in; t++) {
+                            // Random::position(box) then Box::fracpos; VoronoiMesh::isPointClosestTo (any
+                            // closer neighbour rejects, so the order of the checks is free: the neighbour that
+                            // rejected last is checked first)
+                            const double fx = uniform();
+                            const double fy = uniform();
+                            const double fz = uniform();
+                            x = b[0] + fx * (b[3] - b[0]);
+                            y = b[1] + fy * (b[4] - b[1]);
+                            z = b[2] + fz * (b[5] - b[2]);
+                            const double tx = x - sc[0], ty = y - sc[1], tz = z - sc[2];
+                            const double target = tx * tx + ty * ty + tz * tz;
+                            in = true;
+                            for (size_t q = 0; q < nn; q++) {
+                                const double dx = x - nb[3 * q], dy = y - nb[3 * q + 1], dz = z - nb[3 * q + 2];
+                                if (dx * dx + dy * dy + dz * dz < target) {
+                                    in = false;
+                                    if (q) for (int d = 0; d < 3; d++) std::swap(nb[3 * q + d], nb[d]);
+                                    break;
+                                }
+                            }
+                        }
+                        if (!in) throw std::runtime_error("Can't find random position in cell");
+                        double* o = &pos[3 * ((size_t)(cell - c0) * ns + n)];
+                        o[0] = x; o[1] = y; o[2] = z;
+                    }
                 }
-                for (int h = 0; h < Ncomp; h++) m.rho[(size_t)cell * Ncomp + h] = 1.0 * sumv[h] / m.sampleCount;
+                pst.reset(new StageTimer("voronoi densities"));
+                const int T = std::max(1, std::min(16, (int)std::thread::hardware_concurrency()));
+                std::atomic<int> next{c0};
+                std::vector<std::thread> th;
+                for (int w = 0; w < T; w++)
+                    th.emplace_back([&] {
+                        std::vector<double> sumv(Ncomp);
+                        for (int q0; (q0 = next.fetch_add(256)) < c1;)
+                            for (int cell = q0; cell < std::min(c1, q0 + 256); cell++) {
+                                std::fill(sumv.begin(), sumv.end(), 0.0);
+                                for (int n = 0; n < ns; n++) {
+                                    const double* o = &pos[3 * ((size_t)(cell - c0) * ns + n)];
+                                    for (int h = 0; h < Ncomp; h++) sumv[h] += m.dust[h].density(o[0], o[1], o[2]);
+                                }
+                                for (int h = 0; h < Ncomp; h++) m.rho[(size_t)cell * Ncomp + h] = 1.0 * sumv[h] / ns;
+                            }
+                    });
+                for (auto& x : th) x.join();
             }
         } else {
             // Random::position(box) per sample: three deviates, drawn ahead in cell order
