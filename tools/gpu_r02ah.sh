@@ -1,0 +1,7 @@
+# round 2, check of the committed build: smoke, the GPU suite, the default bench line
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+run() { local name=$1 t=$2; shift 2; echo "== $name"; timeout -k 10 $t "$@" > gpurun_out/$name.log 2>&1; local rc=$?; echo "rc=$rc"; tail -${TAILN:-1} gpurun_out/$name.log | cut -c1-160; return $rc; }
+run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" &&
+TAILN=2 run pytest_gpu 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread &&
+run bench_default 600 python bench.py
