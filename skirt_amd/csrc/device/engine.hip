@@ -172,7 +172,7 @@ constexpr int kVorHead = 3;  // header slots
 #define SKIRT_VOR_CONTRACT 1
 #endif
 #ifndef SKIRT_VOR_UNROLL
-#define SKIRT_VOR_UNROLL 4
+#define SKIRT_VOR_UNROLL 8  // at 2 waves/SIMD, no spills (C4 6.17e7 pkt/s; 4: 6.07e7, 2: 5.29e7)
 #endif
 constexpr int kVorUnroll = SKIRT_VOR_UNROLL;
 #ifndef SKIRT_VOR_FALLBACK_GROUP
