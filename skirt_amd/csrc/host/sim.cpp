@@ -130,6 +130,9 @@ SkirtSim* skirt_sim_load_ex(const char* ski, const char* datadir, double package
         auto s = std::make_unique<SkirtSim>();
         auto t0 = std::chrono::steady_clock::now();
         unsigned long theSeed = seed ? (unsigned long)seed : readSkiSeed(ski);
+        // a seed of 0 (mod 2^32) fills the generator's state with zeros: it emits only zeros, which the
+        // deviates reject forever (the reference hangs in its setup); refuse it
+        if ((theSeed & 0xffffffffUL) == 0) throw std::runtime_error("random seed 0 (mod 2^32) is not usable");
         MTRandom mt(theSeed);  // setup draws exactly like the reference (density / tree sampling)
         std::unique_ptr<DeviceDensitySampler> sampler;
         if (setup_device >= 0) sampler.reset(new DeviceDensitySampler(setup_device));
