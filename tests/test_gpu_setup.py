@@ -50,3 +50,21 @@ def test_device_setup_c3_tree():
     print("C3 setup: host %.2f s, device density sampling %.2f s" % (t1 - t0, t2 - t1))
     assert dev.info.nnodes == host.info.nnodes and dev.info.ncells == host.info.ncells
     np.testing.assert_allclose(dev.density(), host.density(), rtol=1e-13, atol=0)
+
+
+def test_device_setup_then_photon_phase_matches_host_setup():
+    """A simulation set up with device sampling runs its photon phase like one set up on the host (the
+    same tree; densities equal to an ulp, so the tallies agree to the same-stream tolerance)."""
+    from parity import STELLAR_OUTLIERS, assert_parity
+    path = os.path.join(SKI, "pan_oct.ski")
+    out = []
+    for dev in (None, 0):
+        sim = S.Simulation(path, packages=2000, setup_device=dev)
+        sim.attach(0)
+        sim.run_stellar()
+        sim.fetch()
+        out.append((sim.labs(), sim.instrument(0)[1]))
+    (la, sa), (lb, sb) = out
+    np.testing.assert_allclose(lb.sum(axis=0), la.sum(axis=0), rtol=1e-9)
+    assert_parity(lb, la, 1e-9, STELLAR_OUTLIERS, "labs (device setup)")
+    np.testing.assert_allclose(sb, sa, rtol=1e-9, atol=1e-300)
