@@ -59,6 +59,13 @@ constexpr int kStepsPerPull = SKIRT_STEPS_PER_PULL;  // grid steps between two r
 #define SKIRT_HALVES 1
 #endif
 constexpr int kHalves = SKIRT_HALVES;
+// Experiment: the detect kernel of iteration i on the aux stream, beside the event and trace kernels of
+// iteration i+1 (detection records double-buffered by parity; the detect stream zeroes its record counter
+// after it, instead of the next trace kernel). One pipeline only.
+#ifndef SKIRT_DETECT_OVERLAP
+#define SKIRT_DETECT_OVERLAP 0
+#endif
+static_assert(!SKIRT_DETECT_OVERLAP || SKIRT_HALVES == 1, "detect overlap uses the aux stream of one pipeline");
 constexpr int kSersicTable = 202;  // SersicFunction: 101 radii, then 101 cumulative masses
 constexpr int kDetectCopies = 8;   // most LDS copies of the SED sums in the detect kernel (one per 8 lanes)
 constexpr int kPollEvery = 1;      // iterations between two counter copies of a half
@@ -1692,7 +1699,7 @@ __device__ __forceinline__ void traceBody(const Args& a) {
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         // reset the counters the next event iteration appends to (nobody else uses them now)
         a.ctr[1 - a.parity] = 0;  // ray count of the next iteration
-        a.ctr[5 + (1 - a.parity)] = 0;  // and its detection records (the last ones were detected already)
+        if (!SKIRT_DETECT_OVERLAP) a.ctr[5 + (1 - a.parity)] = 0;  // and its detection records (the last ones were detected already)
         a.ctr[2 + a.parity] = 0;  // active list just consumed by the event kernel
     }
     if (a.ctr[a.parity] == 0) return;  // an iteration after the end of the phase
@@ -2712,7 +2719,7 @@ int ensurePool(SkirtMcrt* c, int nslots, bool continuous) {
     if (rays >= (size_t)INT32_MAX) return fail(c, SKIRT_ERR_UNSUPPORTED, "ray queue too large");
     const int rayCap = (int)rays;
     const size_t path = continuous ? (size_t)nslots * (kPathCap * sizeof(PathRec) + sizeof(int)) : 0;
-    const size_t half = (size_t)rayCap * sizeof(RayRec) + (size_t)(rayCap - nslots) * sizeof(DetRec) +
+    const size_t half = (size_t)rayCap * sizeof(RayRec) + (1 + SKIRT_DETECT_OVERLAP) * (size_t)(rayCap - nslots) * sizeof(DetRec) +
                         (size_t)nslots * (10 * 8 + 4 * 4 + 6 * 4 + 2 * 4) + path + 4096;
     if (c->dPool && c->nslots == nslots && c->rayCap == rayCap && c->poolPath == (path > 0)) return SKIRT_OK;
     c->poolPath = path > 0;
@@ -2733,7 +2740,7 @@ void carvePool(SkirtMcrt* c, Args& a, int h) {
     a.rays = reinterpret_cast<RayRec*>(p);
     p += (size_t)c->rayCap * sizeof(RayRec);
     a.det = reinterpret_cast<DetRec*>(p);  // at most one peel-off per instrument and slot per iteration
-    p += (size_t)(c->rayCap - c->nslots) * sizeof(DetRec);
+    p += (1 + SKIRT_DETECT_OVERLAP) * (size_t)(c->rayCap - c->nslots) * sizeof(DetRec);
     takeD(a.srx); takeD(a.sry); takeD(a.srz); takeD(a.skx); takeD(a.sky); takeD(a.skz); takeD(a.sL); takeD(a.sLth);
     takeD(a.resA); takeD(a.resB);
     takeI(a.sell); takeI(a.snscatt); takeI(a.sstellar); takeI(a.sstate);
@@ -3844,6 +3851,14 @@ static int runPhase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, uint6
         ah[h] = a;
         carvePool(c, ah[h], h);
     }
+#if SKIRT_DETECT_OVERLAP
+    DetRec* const detBase = ah[0].det;
+    const size_t detHalf = (size_t)(c->rayCap - c->nslots);
+    hipEvent_t trDone, detDone[2];
+    HIPCHECK(c, hipEventCreateWithFlags(&trDone, hipEventDisableTiming));
+    HIPCHECK(c, hipEventCreateWithFlags(&detDone[0], hipEventDisableTiming));
+    HIPCHECK(c, hipEventCreateWithFlags(&detDone[1], hipEventDisableTiming));
+#endif
     int total = 0;
     while (true) {
         bool all = true;
@@ -3854,6 +3869,11 @@ static int runPhase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, uint6
             hipStream_t st = streams[h];
             aa.parity = its[h] & 1;
             aa.init = (its[h] == 0) ? 1 : 0;
+#if SKIRT_DETECT_OVERLAP
+            // this parity's records and counter are free once the detect kernel of two iterations ago ends
+            aa.det = detBase + (size_t)aa.parity * detHalf;
+            if (its[h] >= 2) HIPCHECK(c, hipStreamWaitEvent(st, detDone[aa.parity], 0));
+#endif
             if (aa.continuous && !aa.init) {  // the continuous peel-offs of the FILL rays that just returned
                 launchCont(aa, st);
                 HIPCHECK(c, hipGetLastError());
@@ -3874,8 +3894,17 @@ static int runPhase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, uint6
             HIPCHECK(c, hipEventRecord(c->traceEv[2 * c->traceLaunches + 1], st));
             c->traceLaunches++;
             if (a.ninstr > 0) {
+#if SKIRT_DETECT_OVERLAP
+                HIPCHECK(c, hipEventRecord(trDone, st));
+                HIPCHECK(c, hipStreamWaitEvent(c->aux, trDone, 0));
+                hipLaunchKernelGGL(detectKernel, dim3(dgrid), dim3(kBlock), ldsDetect, c->aux, aa);
+                HIPCHECK(c, hipGetLastError());
+                HIPCHECK(c, hipMemsetAsync(aa.ctr + 5 + aa.parity, 0, sizeof(unsigned int), c->aux));
+                HIPCHECK(c, hipEventRecord(detDone[aa.parity], c->aux));
+#else
                 hipLaunchKernelGGL(detectKernel, dim3(dgrid), dim3(kBlock), ldsDetect, st, aa);
                 HIPCHECK(c, hipGetLastError());
+#endif
             }
             its[h]++;
             total++;
@@ -3902,6 +3931,11 @@ static int runPhase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, uint6
     HIPCHECK(c, hipEventRecord(c->evJoin, c->aux));
     HIPCHECK(c, hipStreamWaitEvent(c->stream, c->evJoin, 0));
     HIPCHECK(c, hipEventRecord(c->ev1, c->stream));
+#if SKIRT_DETECT_OVERLAP
+    (void)hipEventDestroy(trDone);
+    (void)hipEventDestroy(detDone[0]);
+    (void)hipEventDestroy(detDone[1]);
+#endif
     return SKIRT_OK;
 }
 
