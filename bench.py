@@ -234,6 +234,7 @@ def main():
             "segments_per_packet": segs / max(1, delta["packets"]),
             "lane_use": (delta["segments_fill"] + delta["segments_walk"] + delta["segments_peel"]) / max(1, delta["lane_slots"]),
             "iterations": s1["iterations"],
+            "trace_blocks_per_cu": s1["trace_blocks_per_cu"],
             "host_setup_s": round(setup_s, 3),
             "per_packet": {k: delta[k] / max(1, delta["packets"]) for k in
                            ("segments_fill", "segments_walk", "segments_peel", "absorb_adds", "detects")},

@@ -67,7 +67,8 @@ int skirt_sim_run_dust(SkirtSim* sim);
  * read, so every rank follows the same self-absorption schedule as one process would. */
 int skirt_sim_run_stellar_shard(SkirtSim* sim, int rank, int world);
 int skirt_sim_run_dust_shard(SkirtSim* sim, int rank, int world);
-/* dust Labs of the last self-absorption cycle (row-major cell x wavelength), or NULL */
+/* dust Labs of the last self-absorption cycle (row-major cell x wavelength), or NULL; downloads it
+ * (waiting for the device) when skirt_sim_fetch has not done so since the last skirt_sim_run_dust */
 const double* skirt_sim_labs_dust(SkirtSim* sim);
 /* Labsdusttot after every self-absorption cycle; returns the number of cycles */
 int skirt_sim_selfabs_totals(SkirtSim* sim, const double** totals);

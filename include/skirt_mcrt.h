@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define SKIRT_MCRT_ABI_VERSION 8
+#define SKIRT_MCRT_ABI_VERSION 9
 
 enum {
     SKIRT_OK = 0,
@@ -184,6 +184,7 @@ typedef struct {
     uint64_t labs_requests;     /* 64-byte atomic requests carrying the Labs adds (adds sharing a line in
                                    one wave instruction share a request) */
     uint64_t device_cells;      /* device cell numbers, >= ncells (octree sibling groups start on a line) */
+    uint64_t trace_blocks_per_cu; /* trace-kernel workgroups per CU the last phase ran (register and LDS bound) */
 } SkirtStats;
 
 /* grid walks of the trace kernel (SkirtStats::grid_walk) */
@@ -287,6 +288,13 @@ int skirt_mcrt_sample_density(int device, const SkirtDensityDesc* dens, const do
  * With a reducer set, the instrument tallies are summed over the processes first. */
 int skirt_mcrt_download(SkirtMcrt* ctx, double* labs, double* instr);
 int skirt_mcrt_stats(SkirtMcrt* ctx, SkirtStats* out);
+/* DustSystem's cells-crossed statistics (writeCellsCrossed; the _crossed histogram of
+ * DustSystem::fillOpticalDepth / opticaldepth, DustSystem.cpp:959-1000): with bins > 0 every FILL path and
+ * every peel-off path of the following phases counts one in bin min(segments, bins - 1), its number of
+ * segments including those before the grid; zeroed by skirt_mcrt_zero_tallies; bins = 0 turns it off. */
+int skirt_mcrt_set_crossed(SkirtMcrt* ctx, int bins);
+/* the histogram summed over the device copies: hist[b] for b < bins (waits for the engine's stream) */
+int skirt_mcrt_download_crossed(SkirtMcrt* ctx, uint64_t* hist, int bins);
 /* engine knobs (0 = default): packet slots in flight, trace-kernel workgroups, and the number of idle
  * lanes at which a trace wave pulls new rays (1..64) */
 int skirt_mcrt_configure(SkirtMcrt* ctx, int slots, int grid, int pull_threshold);

@@ -472,6 +472,16 @@ inline void lockFreeAdd(double* p, double v) {
     }
 }
 
+constexpr size_t kCrossedBins = 1 << 16;
+
+// Test switch (oracle_set_engine_attenuation): exp(-tau_{n-1}) of the absorption sum as the GPU engine
+// carries it, the running product of 1 - (-expm1(-dtau)) over the path's dust segments, instead of the
+// reference's exp(-taustart) per segment (MonteCarloSimulation.cpp:458-462). The two part in the last digits
+// only behind optically thick segments, where 1 - (1 - exp(-dtau)) cancels; tests/test_gpu_parity.py uses
+// the switch to show that this is the whole of the engine's deep-cell differences on thick models.
+static std::atomic<bool> g_engineAttenuation{false};
+static bool engineAttenuation() { return g_engineAttenuation.load(std::memory_order_relaxed); }
+
 struct Tallies {
     bool shared = false;       // threaded mode: one set of arrays updated with lock-free adds
     void add(std::vector<double>& v, size_t i, double x) {
@@ -482,6 +492,12 @@ struct Tallies {
     std::vector<double> labsDust;
     std::vector<std::vector<double>> frames, seds;  // per instrument
     std::atomic<uint64_t> segments{0};
+    // the counts behind the engine's statistics: segments of the FILL paths (fillOpticalDepth) and of the
+    // peel-off paths (opticaldepth), Labs adds; and DustSystem's _crossed histogram (DustSystem.cpp:959-1000):
+    // paths per number of segments (cells crossed, including those outside the grid), last bin = overflow
+    std::atomic<uint64_t> segFill{0}, segPeel{0}, absorbs{0};
+    std::vector<uint64_t> crossed = std::vector<uint64_t>(kCrossedBins, 0);
+    void cross(size_t n) { __atomic_fetch_add(&crossed[std::min(n, crossed.size() - 1)], 1, __ATOMIC_RELAXED); }
 };
 
 class Sim {
@@ -529,6 +545,8 @@ public:
             Vec3 ko{ins.kobs[0], ins.kobs[1], ins.kobs[2]};
             path(pp.r, ko, tmp);
             t.segments.fetch_add(tmp.v.size(), std::memory_order_relaxed);
+            t.segPeel.fetch_add(tmp.v.size(), std::memory_order_relaxed);
+            t.cross(tmp.v.size());
             for (auto& s : tmp.v) taupath += M.kapparho(s.m, ell) * s.ds;
         }
         double extf = exp(-taupath);
@@ -618,6 +636,8 @@ public:
             // DustSystem::fillOpticalDepth
             path(pp.r, pp.k, p);
             t.segments.fetch_add(p.v.size(), std::memory_order_relaxed);
+            t.segFill.fetch_add(p.v.size(), std::memory_order_relaxed);
+            t.cross(p.v.size());
             double tau = 0;
             for (auto& s : p.v) {
                 double dtau = M.kapparho(s.m, pp.ell) * s.ds;
@@ -636,14 +656,18 @@ public:
                 double expfactor = -expm1(-taupath);
                 if (store) {
                     int N = (int)p.v.size();
+                    const bool product = engineAttenuation();
+                    double att = 1.0;  // (product mode) exp(-taustart) as the running product
                     for (int n = 0; n < N; n++) {
                         int m = p.v[n].m;
                         if (m != -1) {
                             double taustart = (n == 0) ? 0.0 : p.v[n - 1].tau;
                             double expfactorm = -expm1(-p.v[n].dtau);
-                            double Lintm = L * exp(-taustart) * expfactorm;
+                            double Lintm = L * (product ? att : exp(-taustart)) * expfactorm;
+                            att = att * (1.0 - expfactorm);
                             double Labsm = (1.0 - albedo) * Lintm;
                             t.add(*labs, (size_t)m * Nl + pp.ell, Labsm);
+                            t.absorbs.fetch_add(1, std::memory_order_relaxed);
                         }
                     }
                 }
@@ -651,6 +675,8 @@ public:
             } else {
                 double Lsca = 0.0;
                 int N = (int)p.v.size();
+                const bool product = engineAttenuation();
+                double att = 1.0;
                 for (int n = 0; n < N; n++) {
                     int m = p.v[n].m;
                     if (m != -1) {
@@ -663,9 +689,13 @@ public:
                         double albedo = (kext > 0.0) ? ksca / kext : 0.0;
                         double taustart = (n == 0) ? 0.0 : p.v[n - 1].tau;
                         double expfactorm = -expm1(-p.v[n].dtau);
-                        double Lintm = L * exp(-taustart) * expfactorm;
+                        double Lintm = L * (product ? att : exp(-taustart)) * expfactorm;
+                        att = att * (1.0 - expfactorm);
                         Lsca += albedo * Lintm;
-                        if (store) t.add(*labs, (size_t)m * Nl + pp.ell, (1.0 - albedo) * Lintm);
+                        if (store) {
+                            t.add(*labs, (size_t)m * Nl + pp.ell, (1.0 - albedo) * Lintm);
+                            t.absorbs.fetch_add(1, std::memory_order_relaxed);
+                        }
                     }
                 }
                 pp.L = Lsca;
@@ -887,6 +917,8 @@ extern "C" {
 
 const char* oracle_last_error(void) { return g_error.c_str(); }
 
+void oracle_set_engine_attenuation(int on) { g_engineAttenuation = on != 0; }
+
 void oracle_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) { philox(ctr, key, out); }
 
 OracleRun* oracle_run(const char* ski, const char* datadir, int rngKind, int nthreads, double packages,
@@ -1065,6 +1097,7 @@ OracleRun* oracle_run_shard(const char* ski, const char* datadir, int rngKind, i
         if (outprefix && *outprefix) {
             const std::vector<double>* dust = run->tal.labsDust.empty() ? nullptr : &run->tal.labsDust;
             writeOutputs(M, outprefix, run->tal.frames, run->tal.seds, totalLabs(M, run->tal.labs, dust));
+            if (M.hasDust && M.writeCellsCrossed) writeCellsCrossed(M, outprefix, run->tal.crossed);
         }
         return run.release();
     } catch (std::exception& ex) {
@@ -1186,6 +1219,17 @@ int oracle_star_positions(const char* ski, const char* datadir, int comp, int n,
 double oracle_seconds(OracleRun* r) { return r->seconds; }
 uint64_t oracle_packets(OracleRun* r) { return r->packets; }
 uint64_t oracle_segments(OracleRun* r) { return r->tal.segments; }
+void oracle_counts(OracleRun* r, uint64_t out[3]) {
+    out[0] = r->tal.segFill;
+    out[1] = r->tal.segPeel;
+    out[2] = r->tal.absorbs;
+}
+int oracle_crossed(OracleRun* r, const uint64_t** hist) {
+    int n = (int)r->tal.crossed.size();
+    while (n > 0 && r->tal.crossed[n - 1] == 0) n--;
+    *hist = r->tal.crossed.data();
+    return n;
+}
 void oracle_free(OracleRun* r) { delete r; }
 
 }  // extern "C"

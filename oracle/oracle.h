@@ -93,7 +93,18 @@ int oracle_star_positions(const char* ski, const char* datadir, int comp, int n,
 double oracle_seconds(OracleRun* r);
 uint64_t oracle_packets(OracleRun* r);
 uint64_t oracle_segments(OracleRun* r);
+/* out = {segments of the FILL paths (fillOpticalDepth), segments of the peel-off paths (opticaldepth),
+ * absorption adds into Labs}: the counts behind the engine's statistics (SkirtStats) */
+void oracle_counts(OracleRun* r, uint64_t out[3]);
+/* DustSystem's _crossed histogram (DustSystem.cpp:959-1000): hist[n] = paths (FILL and peel-off) of n
+ * segments; returns the number of bins up to the last nonzero one (the last of 65536 bins counts longer
+ * paths) */
+int oracle_crossed(OracleRun* r, const uint64_t** hist);
 void oracle_free(OracleRun* r);
+
+/* test switch: with on != 0 the absorption sums evaluate exp(-tau_{n-1}) as the GPU engine does, as the
+ * running product of 1 - (-expm1(-dtau)) along the path, instead of the reference's exp(-taustart) */
+void oracle_set_engine_attenuation(int on);
 
 /* Philox4x32-10 known-answer access for tests: out[4] = philox(ctr[4], key[2]) */
 void oracle_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);

@@ -38,7 +38,8 @@ class SkirtStats(ctypes.Structure):
                 ("detects", ctypes.c_uint64), ("absorb_adds", ctypes.c_uint64), ("lane_slots", ctypes.c_uint64),
                 ("iterations", ctypes.c_uint64), ("kernel_ms", ctypes.c_double), ("trace_ms", ctypes.c_double),
                 ("trace_launches", ctypes.c_uint64), ("grid_walk", ctypes.c_int32), ("map_level", ctypes.c_int32),
-                ("labs_requests", ctypes.c_uint64), ("device_cells", ctypes.c_uint64)]
+                ("labs_requests", ctypes.c_uint64), ("device_cells", ctypes.c_uint64),
+                ("trace_blocks_per_cu", ctypes.c_uint64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -67,6 +68,7 @@ ABI_SYMBOLS = [
     "skirt_sim_run_stellar_shard", "skirt_sim_run_dust_shard", "skirt_sim_set_photon_seed",
     "skirt_host_voronoi_build", "skirt_host_voronoi_describe", "skirt_host_voronoi_free",
     "skirt_sim_load_ex", "skirt_mcrt_sample_density", "skirt_sim_density",
+    "skirt_mcrt_set_crossed", "skirt_mcrt_download_crossed",
 ]
 
 _lib = None
@@ -127,6 +129,8 @@ def lib():
         L.skirt_mcrt_zero_tallies.argtypes = [vp]
         L.skirt_mcrt_synchronize.argtypes = [vp]
         L.skirt_mcrt_configure.argtypes = [vp, c_int, c_int, c_int]
+        L.skirt_mcrt_set_crossed.argtypes = [vp, c_int]
+        L.skirt_mcrt_download_crossed.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64), c_int]
         _lib = L
     return _lib
 
@@ -246,6 +250,18 @@ class Simulation:
 
     def fetch(self):
         self._check(lib().skirt_sim_fetch(self._h))
+
+    def set_crossed(self, bins=16384):
+        """Turn on DustSystem's cells-crossed histogram (writeCellsCrossed) for the following phases:
+        every FILL and peel-off path counts in bin min(segments, bins - 1); 0 turns it off."""
+        self._check_engine(lib().skirt_mcrt_set_crossed(self.engine, int(bins)))
+
+    def crossed(self, bins=16384):
+        """The cells-crossed histogram: paths per number of segments (waits for the device)."""
+        h = np.zeros(int(bins), dtype=np.uint64)
+        self._check_engine(lib().skirt_mcrt_download_crossed(self.engine, h.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)),
+                                                             int(bins)))
+        return h
 
     def stats(self):
         s = SkirtStats()

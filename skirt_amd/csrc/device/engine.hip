@@ -52,20 +52,10 @@ constexpr int kStepsPerPull = SKIRT_STEPS_PER_PULL;  // grid steps between two r
 #ifndef SKIRT_PULL_CHUNK
 #define SKIRT_PULL_CHUNK 64        // queue ids a trace wave reserves at once (0: exactly its idle lanes; >= 64)
 #endif
-// The slot pool runs as kHalves independent pipelines on their own streams: while one half's trace
-// kernel drains its queue, the other half's event and detect kernels (and its trace kernel's first
-// waves) fill the CUs the finishing waves leave idle.
-#ifndef SKIRT_HALVES
-#define SKIRT_HALVES 1
-#endif
-constexpr int kHalves = SKIRT_HALVES;
-// Experiment: the detect kernel of iteration i on the aux stream, beside the event and trace kernels of
-// iteration i+1 (detection records double-buffered by parity; the detect stream zeroes its record counter
-// after it, instead of the next trace kernel). One pipeline only.
-#ifndef SKIRT_DETECT_OVERLAP
-#define SKIRT_DETECT_OVERLAP 0
-#endif
-static_assert(!SKIRT_DETECT_OVERLAP || SKIRT_HALVES == 1, "detect overlap uses the aux stream of one pipeline");
+// The slot pool runs as one or two independent pipelines ("halves", SkirtMcrt::halves): with two, one
+// half's event and detect kernels run beside the other half's trace kernel, on CUs of their own (CU-masked
+// streams, see runPhase).
+constexpr int kMaxHalves = 2;
 constexpr int kSersicTable = 202;  // SersicFunction: 101 radii, then 101 cumulative masses
 constexpr int kDetectCopies = 8;   // most LDS copies of the SED sums in the detect kernel (one per 8 lanes)
 constexpr int kPollEvery = 1;      // iterations between two counter copies of a half
@@ -139,6 +129,10 @@ constexpr int kContSlots = 1 << 15;  // packet slots in flight with continuous s
 enum ErrorBits : unsigned { ERR_TAU = 1u, ERR_PATH_CAP = 2u, ERR_QUEUE = 4u };
 template <int GRID>
 constexpr bool kEnterInEvent = GRID == SKIRT_GRID_VORONOI;
+// a ray entered by the event kernel carries the number of its segments before the grid in the top bits
+// of its first cell (Voronoi device cells < 2^28)
+constexpr int kOutsideShift = 28;
+constexpr int kCellMaskOut = (1 << kOutsideShift) - 1;
 // most segments one Grid<GRID>::step adds (the Voronoi step may add a pending and a new segment)
 template <int GRID>
 constexpr int kSegsPerStep = GRID == SKIRT_GRID_VORONOI ? 2 : 1;
@@ -264,6 +258,10 @@ struct Args {
     double* tally;
     unsigned int* error;
     unsigned long long* stats;   // packets, seg_fill, seg_walk, seg_peel, detects, absorbs, lane slots
+    // DustSystem's _crossed histogram (DustSystem.cpp:959-1000), or null: per FILL and PEEL path one count in
+    // bin min(segments, crossedBins - 1), kCrossedCopies copies (by wave) against same-address contention
+    unsigned long long* crossed;
+    int crossedBins;
     // slot pool (structure of arrays) and queues
     int nslots;
     double *srx, *sry, *srz, *skx, *sky, *skz, *sL, *sLth;
@@ -283,7 +281,22 @@ struct Args {
     int* pathCnt;
     int ldsMeshOff, ldsOptOff, ldsInstrOff, ldsSedOff;  // in doubles
     int detCopies;  // detect kernel: LDS copies of the SED sums (8, 4, 2, 1), 0 = SEDs straight to the tally
+#ifdef SKIRT_EXPERIMENT_TIMELINE
+    // tuning experiment only: per wave {start, queue found exhausted, end, rays} in 100 MHz ticks, per
+    // kernel kind (0 trace, 1 event, 2 detect) and iteration (< kTlLaunches)
+    unsigned long long* tl;
+    int tlLaunch;
+#endif
 };
+#ifdef SKIRT_EXPERIMENT_TIMELINE
+constexpr int kTlLaunches = 64, kTlWaves = 4096, kTlWords = 8;
+__device__ __forceinline__ unsigned long long* tlSlot(const Args& a, int kind) {
+    if (!a.tl || a.tlLaunch >= kTlLaunches) return nullptr;
+    const int wave = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
+    if (wave >= kTlWaves) return nullptr;
+    return a.tl + (((size_t)kind * kTlLaunches + a.tlLaunch) * kTlWaves + wave) * kTlWords;
+}
+#endif
 
 // One finest-level cell of the octree leaf map: the leaf node that covers it, that leaf's dust cell
 // number and level, and the leaf's density of dust component 0 (the one-component kernels need no
@@ -401,6 +414,11 @@ __device__ __forceinline__ constexpr int gridParts() {
 // The counters live in kStatCopies copies of one 64-byte line each (summed by the host): the waves of a
 // launch end together, and same-line atomics from all of them would queue on one L2 channel.
 constexpr int kStatCopies = 64;
+constexpr int kCrossedCopies = 64;
+__device__ __forceinline__ void crossedAdd(const Args& a, unsigned n) {
+    const unsigned wave = (blockIdx.x * (kBlock / 64) + threadIdx.x / 64) & (kCrossedCopies - 1);
+    atomicAdd(a.crossed + (size_t)wave * a.crossedBins + min(n, (unsigned)a.crossedBins - 1u), 1ull);
+}
 __device__ __forceinline__ void flushStats(const Args& a, const unsigned long long (&vals)[8]) {
     const int lane = threadIdx.x & 63;
     unsigned long long* dst = a.stats + 8 * ((blockIdx.x * (kBlock / 64) + threadIdx.x / 64) & (kStatCopies - 1));
@@ -1244,8 +1262,12 @@ template <int GRID, bool ONECOMP, bool CONT>
 struct Tracer {
     const Args& a;
     const Shared& sh;
-    unsigned int segFill = 0, segWalk = 0, segPeel = 0, absorbs = 0, laneSlots = 0;
-    unsigned int requests = 0;  // 64-byte atomic requests of the Labs adds (lane 0 of each wave counts)
+    // statistics, kept out of the walk's registers: the lane's segments of its current ray (added per ray
+    // to the wave's FILL / WALK / PEEL totals in LDS when the ray ends), and wave-uniform counts of the
+    // Labs adds, lane-steps and 64-byte atomic requests (lane 0's values are the wave's)
+    unsigned int nseg = 0;
+    unsigned int absorbs = 0, laneSlots = 0, requests = 0;
+    unsigned* waveSegs;  // LDS, [kBlock / 64][3]: FILL, WALK, PEEL segments of the wave's finished rays
     // Labs adds of this lane not yet issued. f64 atomics execute memory-side at a fixed chip-wide rate
     // of 64-byte requests; lanes of one wave instruction that hit the same 64-byte line share a
     // request. A lane's consecutive adds are consecutive cells of one ray -- spatial neighbours, and
@@ -1294,7 +1316,8 @@ struct Tracer {
                 if (i < npend && !dupAddr[i]) na++;
             }
             for (int off = 32; off > 0; off >>= 1) { nl += __shfl_xor(nl, off); na += __shfl_xor(na, off); }
-            if (lane == 0) { requests += nl; laneSlots += na; }
+            requests += nl;
+            laneSlots += na;
         }
 #endif
 #pragma unroll
@@ -1308,8 +1331,9 @@ struct Tracer {
             const unsigned line = (unsigned)(reinterpret_cast<size_t>(a.labs + idx) >> 6);
             const unsigned prev = __shfl(line, lane - 1);
             const unsigned long long starts = __ballot(j < n && (j == 0 || prev != line));
+            absorbs += (unsigned)__popcll(__ballot(j < n));
 #ifndef SKIRT_EXPERIMENT_LINE_COUNT
-            if (lane == 0) requests += (unsigned)__popcll(starts);
+            requests += (unsigned)__popcll(starts);
 #endif
 #ifdef SKIRT_EXPERIMENT_NO_LABS_ATOMICS  // tuning experiment only: the cost of the Labs atomics
             if (j < n && pendVal[q] == -1.0) atomicAddF64(a.labs + idx, pendVal[q]);
@@ -1344,10 +1368,15 @@ struct Tracer {
         }
         r.s += ds;
         r.tau += dtau;
+        nseg++;
         if (r.mode == RAY_FILL) {
-            segFill++;
             if (m >= 0 && (!ONECOMP || a.store)) {
-                // L_abs = (1-albedo) L exp(-tau_{n-1}) (1 - exp(-dtau_n)); exp(-tau_{n-1}) is carried in f1
+                // L_abs = (1-albedo) L exp(-tau_{n-1}) (1 - exp(-dtau_n)) (MonteCarloSimulation.cpp:458-462);
+                // exp(-tau_{n-1}) is carried in f1 as the running product of 1 - (1 - exp(-dtau)). Behind an
+                // optically thick segment that product is exact only to about 1e-16 / exp(-dtau) relative
+                // (dtau = 30: 1.7e-4), where the reference evaluates exp(-tau) afresh: the named cause of the
+                // deep-cell differences on the thick pan_oct_sa models (tests/parity.py). Evaluating exp
+                // here instead costs the octree walk ~80 B/lane of register spills.
                 const double ef = -expm1(-dtau);
                 const double Lintm = r.param * r.f1 * ef;
                 r.f1 = r.f1 * (1.0 - ef);
@@ -1366,16 +1395,12 @@ struct Tracer {
                     pendVal[npend * kBlock + threadIdx.x] = (1.0 - albedo) * Lintm;
                     pendIdx[npend * kBlock + threadIdx.x] = (unsigned)r.ell * (unsigned)a.labsStride + (unsigned)m;
                     npend++;
-                    absorbs++;
                 }
             }
         } else if (r.mode == RAY_WALK) {
-            segWalk++;
             if (r.tau > r.param) return false;  // the interaction point lies in this segment
             r.f1 = r.tau;
             r.f2 = r.s;
-        } else {
-            segPeel++;
         }
         return true;
     }
@@ -1405,8 +1430,11 @@ struct Tracer {
         // FILL: f1 = exp(-tau) = 1, f2 = scattered luminosity; WALK: tau and s at the last segment end
         r.f1 = (r.mode == RAY_FILL) ? 1.0 : 0.0;
         r.f2 = (r.mode == RAY_WALK) ? c3.x : 0.0;
+        // the segments before the grid of a ray the event kernel entered travel in the first cell's top bits
+        // (a ray the event kernel entered brings its segments before the grid in the first cell's top bits)
+        nseg = kEnterInEvent<GRID> ? ((unsigned)c6.z >> kOutsideShift) : 0u;
         if (kEnterInEvent<GRID>) {  // entered by the event kernel: the cell and its neighbour list
-            r.ci = c6.z;
+            r.ci = c6.z & kCellMaskOut;
             r.cj = c6.w;
             r.ck = 0;
         } else if (r.mode != RAY_NONE &&
@@ -1418,6 +1446,8 @@ struct Tracer {
 
     // the ray ended (grid edge or WALK target reached): deliver its result
     __device__ __forceinline__ void finish(const Ray& r) {
+        atomicAdd(&waveSegs[(threadIdx.x >> 6) * 3 + (r.mode == RAY_FILL ? 0 : r.mode == RAY_WALK ? 1 : 2)], nseg);
+        if (a.crossed && r.mode != RAY_WALK) crossedAdd(a, nseg);
         if (r.mode == RAY_PEEL) {
             a.det[r.idx].tau = r.tau;  // detectKernel turns it into a detection
         } else if (r.mode == RAY_FILL) {
@@ -1699,15 +1729,22 @@ __device__ __forceinline__ void traceBody(const Args& a) {
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         // reset the counters the next event iteration appends to (nobody else uses them now)
         a.ctr[1 - a.parity] = 0;  // ray count of the next iteration
-        if (!SKIRT_DETECT_OVERLAP) a.ctr[5 + (1 - a.parity)] = 0;  // and its detection records (the last ones were detected already)
+        a.ctr[5 + (1 - a.parity)] = 0;  // and its detection records (the last ones were detected already)
         a.ctr[2 + a.parity] = 0;  // active list just consumed by the event kernel
     }
     if (a.ctr[a.parity] == 0) return;  // an iteration after the end of the phase
+#ifdef SKIRT_EXPERIMENT_TIMELINE
+    const unsigned long long tlStart = __builtin_amdgcn_s_memrealtime();
+    unsigned long long tlExhausted = 0, tlRays = 0;
+#endif
     Shared sh = stageTables(a, lds, gridParts<GRID>() | STAGE_OPTICS);
 
     Tracer<GRID, ONECOMP, CONT> T{a, sh};
     T.pendVal = lds + a.ldsInstrOff;  // after the grid and optics tables
     T.pendIdx = reinterpret_cast<unsigned*>(lds + a.ldsInstrOff + kLabsBuf * kBlock);
+    T.waveSegs = T.pendIdx + kLabsBuf * kBlock;
+    if (threadIdx.x < 3 * (kBlock / 64)) T.waveSegs[threadIdx.x] = 0;
+    __syncthreads();
     const int lane = threadIdx.x & 63;
     const unsigned int nrays = a.ctr[a.parity];
     Ray r;
@@ -1752,12 +1789,16 @@ __device__ __forceinline__ void traceBody(const Args& a) {
                 if (id >= nrays) done = true;
                 else T.load(r, id);  // a RAY_NONE record (empty path) leaves the lane idle
             }
+#ifdef SKIRT_EXPERIMENT_TIMELINE
+            tlRays += (unsigned long long)__popcll(__ballot(idle && id < nrays));
+            if (!tlExhausted && __ballot(idle && id >= nrays)) tlExhausted = __builtin_amdgcn_s_memrealtime();
+#endif
         }
 #pragma unroll 1
         for (int it = 0; it < kStepsPerPull; it++) {
             if (__ballot(r.mode != RAY_NONE) == 0) break;
 #ifndef SKIRT_EXPERIMENT_LINE_COUNT
-            T.laneSlots++;
+            T.laneSlots += 64;
 #endif
             if (r.mode != RAY_NONE) {
                 if (!Grid<GRID>::step(a, sh, r, [&](int m, double rho0, double ds) { return T.segment(r, m, rho0, ds); })) {
@@ -1770,7 +1811,17 @@ __device__ __forceinline__ void traceBody(const Args& a) {
         }
     }
     T.drain();
-    const unsigned long long vals[8] = {0, T.segFill, T.segWalk, T.segPeel, 0, T.absorbs, T.laneSlots, T.requests};
+#ifdef SKIRT_EXPERIMENT_TIMELINE
+    if (unsigned long long* t = tlSlot(a, 0)) {
+        const unsigned long long tEnd = __builtin_amdgcn_s_memrealtime();
+        if (lane == 0) { t[0] = tlStart; t[1] = tlExhausted; t[2] = tEnd; t[3] = tlRays; }
+    }
+#endif
+    // (wave totals: lane 0 contributes them)
+    const unsigned* ws = T.waveSegs + (threadIdx.x >> 6) * 3;
+    const bool l0 = lane == 0;
+    const unsigned long long vals[8] = {0, l0 ? ws[0] : 0u, l0 ? ws[1] : 0u, l0 ? ws[2] : 0u, 0,
+                                        l0 ? T.absorbs : 0u, l0 ? T.laneSlots : 0u, l0 ? T.requests : 0u};
     flushStats(a, vals);
 }
 
@@ -1790,6 +1841,9 @@ __global__ void __launch_bounds__(kBlock) detectKernel(const Args a) {
     extern __shared__ __attribute__((aligned(16))) double lds[];
     const unsigned int nrays = a.ctr[5 + a.parity];  // this iteration's detection records
     if (nrays == 0) return;
+#ifdef SKIRT_EXPERIMENT_TIMELINE
+    const unsigned long long tlStart = __builtin_amdgcn_s_memrealtime();
+#endif
     Shared sh = stageTables(a, lds, STAGE_INSTR);
     const int copies = a.detCopies;
     for (int q = threadIdx.x; q < copies * a.nsed; q += blockDim.x) sh.sed[q] = 0.0;
@@ -1834,6 +1888,12 @@ __global__ void __launch_bounds__(kBlock) detectKernel(const Args a) {
             atomicAddF64(a.tally + sh.instr[ii].sedBase + (q - sh.instr[ii].sedOff), v);
         }
     }
+#ifdef SKIRT_EXPERIMENT_TIMELINE
+    if (unsigned long long* t = tlSlot(a, 2)) {
+        const unsigned long long tEnd = __builtin_amdgcn_s_memrealtime();
+        if (lane == 0) { t[0] = tlStart; t[1] = 0; t[2] = tEnd; t[3] = nrays; }
+    }
+#endif
     const unsigned long long vals[8] = {0, 0, 0, 0, detects, 0, 0, 0};
     flushStats(a, vals);
 }
@@ -1869,15 +1929,16 @@ struct Events {
         const unsigned mode = rayMode(flags);
         int4* dst = reinterpret_cast<int4*>(a.rays + pos);
         bool entered = a.hasDust;
+        unsigned nseg = 0;
         if (kEnterInEvent<GRID> && entered) {
-            unsigned nseg = 0;
             entered = Grid<GRID>::begin(a, sh, r, [&](int, double, double ds) {
                 if (ds > 0) { r.s += ds; nseg++; }  // outside the grid: no optical depth
                 return true;
             });
-            if (mode == RAY_FILL) segFill += nseg;
-            else if (mode == RAY_WALK) segWalk += nseg;
-            else segPeel += nseg;
+            // (the trace kernel counts them with the ray's other segments: they travel in the record)
+        }
+        if (kEnterInEvent<GRID> && a.crossed && mode != RAY_WALK && a.hasDust) {
+            if (!entered) crossedAdd(a, 0);  // (a path that misses the grid has no segments)
         }
         if (!entered) {
             if (mode != RAY_PEEL) {  // a peel-off's detection record already holds tau = 0
@@ -1893,7 +1954,8 @@ struct Events {
         d2[1] = make_double2(r.z, dx);
         d2[2] = make_double2(dy, dz);
         d2[3] = make_double2(r.s, prm);
-        dst[4] = make_int4(idx, (int)flags, r.ci, r.cj);
+        // (the segments before the grid, for the cells-crossed histogram, in the first cell's top bits)
+        dst[4] = make_int4(idx, (int)flags, r.ci | (int)(min(nseg, 7u) << kOutsideShift), r.cj);
     }
 
     __device__ __forceinline__ void load(int s, Packet& p) const {
@@ -2333,6 +2395,19 @@ __global__ void __launch_bounds__(kBlock) SKIRT_EVENT_ATTR eventKernel(const Arg
     extern __shared__ __attribute__((aligned(16))) double lds[];
     if (blockIdx.x == 0 && threadIdx.x == 0) a.ctr[4] = 0;  // the trace kernel's pull counter
     if (!a.init && a.ctr[2 + a.parity] == 0) return;  // an iteration after the end of the phase
+#ifdef SKIRT_EXPERIMENT_TIMELINE
+    const unsigned long long tlStart = __builtin_amdgcn_s_memrealtime();
+    // shader-clock cycles per part of a round: state loads + the FILL/WALK events, packet claims and launches,
+    // the block reservations, the ray and state writes
+    unsigned long long tlPart[4] = {0, 0, 0, 0};
+    auto stamp = [] {
+        unsigned long long t;
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+        __builtin_amdgcn_sched_barrier(0);
+        return t;
+    };
+#endif
     Shared sh = stageTables(a, lds, gridParts<GRID>() | STAGE_OPTICS | STAGE_INSTR);
     Events<GRID, ONECOMP> E{a, sh};
     const int lane = threadIdx.x & 63;
@@ -2346,6 +2421,9 @@ __global__ void __launch_bounds__(kBlock) SKIRT_EVENT_ATTR eventKernel(const Arg
     for (unsigned int round = 0; round < rounds; round++) {
         const unsigned int w = round * stride + blockIdx.x * blockDim.x + threadIdx.x;
         const bool valid = w < nwork;
+#ifdef SKIRT_EXPERIMENT_TIMELINE
+        unsigned long long ts0 = stamp();
+#endif
         const int slot = valid ? (a.init ? (int)w : actIn[w]) : 0;
         Packet p;
         p.state = S_NEW;
@@ -2393,6 +2471,11 @@ __global__ void __launch_bounds__(kBlock) SKIRT_EVENT_ATTR eventKernel(const Arg
         }
         // slots without a packet claim the next global packet indices (one atomic per block)
         bool need = valid && p.state == S_NEW && mainMode == RAY_NONE;
+#ifdef SKIRT_EXPERIMENT_TIMELINE
+        { const bool any = __ballot(need) != 0; (void)any; }
+        unsigned long long ts1 = stamp();
+        tlPart[0] += ts1 - ts0;
+#endif
         while (__syncthreads_or(need)) {
             unsigned long long idx = 0;
             unsigned int unused = 0;
@@ -2400,9 +2483,11 @@ __global__ void __launch_bounds__(kBlock) SKIRT_EVENT_ATTR eventKernel(const Arg
             if (need) {
                 if (idx >= total) need = false;  // exhausted: the slot retires
                 else if (E.launch(p, globalPacket(a, a.first + idx))) {
-                    if (!(p.L > 0)) {
+                    if (!(p.L > 0) && !a.crossed) {
                         // a zero-weight dust packet (a cell without emission drawn uniformly): every
-                        // tally it would touch receives 0, so it ends here
+                        // tally it would touch receives 0, so it ends here -- unless the cells-crossed
+                        // statistics are on: the reference still traces its paths (dodustemissionchunk,
+                        // PanMonteCarloSimulation.cpp:316-329), which count in ds_crossed
                     } else if (a.hasDust) {
                         peel = (a.ninstr > 0 && a.peel) ? PEEL_EMISSION : PEEL_NONE;
                         mainMode = RAY_FILL;
@@ -2421,6 +2506,10 @@ __global__ void __launch_bounds__(kBlock) SKIRT_EVENT_ATTR eventKernel(const Arg
                 }
             }
         }
+#ifdef SKIRT_EXPERIMENT_TIMELINE
+        unsigned long long ts2 = stamp();
+        tlPart[1] += ts2 - ts1;
+#endif
         // rays this lane queues: its peel-offs and its next FILL/WALK ray
         int nray = 0;
         if (peel != PEEL_NONE) {
@@ -2438,6 +2527,10 @@ __global__ void __launch_bounds__(kBlock) SKIRT_EVENT_ATTR eventKernel(const Arg
         unsigned int pos = 0, apos = 0, dpos = 0;
         blockReserve3(a.ctr + a.parity, (unsigned)nray, pos, a.ctr + 2 + (1 - a.parity), active ? 1u : 0u, apos,
                       a.ctr + 5 + a.parity, (unsigned)npeel, dpos, resv);
+#ifdef SKIRT_EXPERIMENT_TIMELINE
+        unsigned long long ts3 = stamp();
+        tlPart[2] += ts3 - ts2;
+#endif
         int inext = 0;  // next instrument to consider for a peel-off
         for (int k = 0; k < nray; k++) {
             double dx, dy, dz, prm;
@@ -2482,7 +2575,19 @@ __global__ void __launch_bounds__(kBlock) SKIRT_EVENT_ATTR eventKernel(const Arg
         // the slot stays active while it has a FILL/WALK ray in flight
         if (active) actOut[apos] = slot;
         if (valid) E.store(slot, p);
+#ifdef SKIRT_EXPERIMENT_TIMELINE
+        tlPart[3] += stamp() - ts3;
+#endif
     }
+#ifdef SKIRT_EXPERIMENT_TIMELINE
+    if (unsigned long long* t = tlSlot(a, 1)) {
+        const unsigned long long tEnd = __builtin_amdgcn_s_memrealtime();
+        if (lane == 0) {
+            t[0] = tlStart; t[1] = 0; t[2] = tEnd; t[3] = rounds;
+            for (int q = 0; q < 4; q++) t[4 + q] = tlPart[q];
+        }
+    }
+#endif
     const unsigned long long vals[8] = {E.packets, E.segFill, E.segWalk, E.segPeel, E.detects, 0, 0, 0};
     flushStats(a, vals);
 }
@@ -2660,17 +2765,26 @@ struct SkirtMcrt {
     double *dLabs = nullptr, *dTally = nullptr;
     bool ownLabs = true, ownTally = true;
     unsigned long long *dClaim = nullptr, *dStats = nullptr;
-    unsigned int *dError = nullptr, *dCtr = nullptr, *hCtr = nullptr;  // kHalves x 8 counters; hCtr: poll ring
-    hipStream_t aux = nullptr;           // the second pipeline half's stream
-    hipEvent_t evFork = nullptr, evJoin = nullptr;
-    std::vector<hipEvent_t> pollEv;      // kHalves x kPollRing events behind the counter copies
+    unsigned long long* dCrossed = nullptr;  // kCrossedCopies x crossedBins (skirt_mcrt_set_crossed)
+    int crossedBins = 0;
+    unsigned int *dError = nullptr, *dCtr = nullptr, *hCtr = nullptr;  // kMaxHalves x 8 counters; hCtr: poll ring
+    // the pipeline's streams: sE runs the event, continuous peel-off and detect kernels, sT[h] the trace
+    // kernels of half h; with CU masks (cusT, cusE) they run on disjoint sets of CUs. One half without
+    // masks runs everything on the caller's stream.
+    int halves = 1, cusT = 0, cusE = 0;  // requested (SKIRT_AMD_HALVES, SKIRT_AMD_TRACE_CUS, SKIRT_AMD_EVENT_CUS)
+    hipStream_t sE = nullptr, sT[kMaxHalves] = {};
+    int streamCusT = -1, streamCusE = -1;  // the masks the owned streams were created with
+    int nCusT = 0, nCusE = 0;              // CUs behind each stream (grid sizes)
+    hipEvent_t evFork = nullptr, evJoin[1 + kMaxHalves] = {}, evE[kMaxHalves] = {}, evT[kMaxHalves] = {};
+    std::vector<hipEvent_t> pollEv;      // kMaxHalves x kPollRing events behind the counter copies
     // slot pool
-    int nslots = 0, rayCap = 0;
+    int nslots = 0, rayCap = 0, poolHalves = 0;
     bool poolPath = false;  // the pool holds the continuous-scattering path records
-    void* dPool = nullptr;               // kHalves pools of nslots / kHalves slots each
+    void* dPool = nullptr;               // one pool of nslots slots per half
     size_t poolBytes = 0;
     // config
     int traceGrid = 0, threshold = 8, slotsWanted = 0;
+    int traceBlocksPerCU = 0;  // the occupancy the last trace launch was sized for
     int lastDetCopies = 0;  // SED copies of the last run's detect kernel
     double lastMs = 0;
     std::vector<hipEvent_t> traceEv;  // pairs around the trace launches not yet timed
@@ -2709,25 +2823,68 @@ int upload(SkirtMcrt* c, T*& dst, const T* src, size_t n) {
     return SKIRT_OK;
 }
 
-// slot pool: kHalves independent pipelines, each with its ray queue, SoA packet state, per-slot
+// slot pool: one pool per pipeline half, each with its ray queue, SoA packet state, per-slot
 // results and two active lists; nslots counts the slots of one half
 // With continuous scattering every slot may also queue one peel-off per instrument and recorded path
 // segment in one iteration, and keeps the dust segments of its last path (kPathCap each).
-int ensurePool(SkirtMcrt* c, int nslots, bool continuous) {
+int ensurePool(SkirtMcrt* c, int nslots, bool continuous, int halves) {
     const int ninstr = (int)c->instr.size();
     const size_t rays = (size_t)nslots * (1 + ninstr) + (continuous ? (size_t)nslots * kPathCap * ninstr : 0);
     if (rays >= (size_t)INT32_MAX) return fail(c, SKIRT_ERR_UNSUPPORTED, "ray queue too large");
     const int rayCap = (int)rays;
     const size_t path = continuous ? (size_t)nslots * (kPathCap * sizeof(PathRec) + sizeof(int)) : 0;
-    const size_t half = (size_t)rayCap * sizeof(RayRec) + (1 + SKIRT_DETECT_OVERLAP) * (size_t)(rayCap - nslots) * sizeof(DetRec) +
+    const size_t half = (size_t)rayCap * sizeof(RayRec) + (size_t)(rayCap - nslots) * sizeof(DetRec) +
                         (size_t)nslots * (10 * 8 + 4 * 4 + 6 * 4 + 2 * 4) + path + 4096;
-    if (c->dPool && c->nslots == nslots && c->rayCap == rayCap && c->poolPath == (path > 0)) return SKIRT_OK;
+    if (c->dPool && c->nslots == nslots && c->rayCap == rayCap && c->poolPath == (path > 0) && c->poolHalves == halves)
+        return SKIRT_OK;
     c->poolPath = path > 0;
     if (c->dPool) { (void)hipFree(c->dPool); c->dPool = nullptr; }
-    HIPCHECK(c, hipMalloc(&c->dPool, kHalves * half));
+    HIPCHECK(c, hipMalloc(&c->dPool, halves * half));
     c->poolBytes = half;
     c->nslots = nslots;
     c->rayCap = rayCap;
+    c->poolHalves = halves;
+    return SKIRT_OK;
+}
+
+// A stream restricted to `want` CUs (0: all), spread evenly over the XCDs: CU k of the mask is taken when
+// k mod 32 < want / 8 (or, for the complementary set, k mod 32 >= 32 - want / 8), so that each XCD
+// contributes the same share whether the runtime numbers CUs XCD by XCD or round-robin.
+int makeStream(SkirtMcrt* c, hipStream_t* s, int want, bool high, int* got) {
+    if (want <= 0 || want >= c->numCUs) {
+        *got = c->numCUs;
+        HIPCHECK(c, hipStreamCreateWithFlags(s, hipStreamNonBlocking));
+        return SKIRT_OK;
+    }
+    const int words = (c->numCUs + 31) / 32;
+    std::vector<uint32_t> mask(words, 0u);
+    const int per = std::max(1, want * 32 / std::max(32, c->numCUs));
+    int n = 0;
+    for (int k = 0; k < c->numCUs; k++) {
+        const int r = k % 32;
+        if (high ? r >= 32 - per : r < per) { mask[k / 32] |= 1u << (k % 32); n++; }
+    }
+    *got = n;
+    HIPCHECK(c, hipExtStreamCreateWithCUMask(s, (uint32_t)words, mask.data()));
+    return SKIRT_OK;
+}
+
+// the pipeline streams for the requested halves and CU masks (created once per mask configuration)
+int ensureStreams(SkirtMcrt* c) {
+    if (c->halves == 1 && c->cusT == 0 && c->cusE == 0) {
+        c->nCusT = c->nCusE = c->numCUs;
+        return SKIRT_OK;  // everything on the caller's stream
+    }
+    if (c->sE && c->streamCusT == c->cusT && c->streamCusE == c->cusE) return SKIRT_OK;
+    (void)hipStreamSynchronize(c->stream);
+    if (c->sE) { (void)hipStreamDestroy(c->sE); c->sE = nullptr; }
+    for (auto& s : c->sT)
+        if (s) { (void)hipStreamDestroy(s); s = nullptr; }
+    int rc = makeStream(c, &c->sE, c->cusE, true, &c->nCusE);
+    for (int h = 0; h < kMaxHalves && !rc; h++) rc = makeStream(c, &c->sT[h], c->cusT, false, &c->nCusT);
+    if (rc) return rc;
+    c->streamCusT = c->cusT;
+    c->streamCusE = c->cusE;
     return SKIRT_OK;
 }
 
@@ -2740,7 +2897,7 @@ void carvePool(SkirtMcrt* c, Args& a, int h) {
     a.rays = reinterpret_cast<RayRec*>(p);
     p += (size_t)c->rayCap * sizeof(RayRec);
     a.det = reinterpret_cast<DetRec*>(p);  // at most one peel-off per instrument and slot per iteration
-    p += (1 + SKIRT_DETECT_OVERLAP) * (size_t)(c->rayCap - c->nslots) * sizeof(DetRec);
+    p += (size_t)(c->rayCap - c->nslots) * sizeof(DetRec);
     takeD(a.srx); takeD(a.sry); takeD(a.srz); takeD(a.skx); takeD(a.sky); takeD(a.skz); takeD(a.sL); takeD(a.sLth);
     takeD(a.resA); takeD(a.resB);
     takeI(a.sell); takeI(a.snscatt); takeI(a.sstellar); takeI(a.sstate);
@@ -2961,14 +3118,27 @@ int skirt_mcrt_create(int device, SkirtMcrt** out) {
         hipMalloc(&c->dClaim, sizeof(unsigned long long)) != hipSuccess ||
         hipMalloc(&c->dStats, 8 * kStatCopies * sizeof(unsigned long long)) != hipSuccess ||
         hipMalloc(&c->dError, sizeof(unsigned int)) != hipSuccess ||
-        hipMalloc(&c->dCtr, kHalves * 8 * sizeof(unsigned int)) != hipSuccess ||
-        hipHostMalloc(&c->hCtr, kHalves * kPollRing * 8 * sizeof(unsigned int)) != hipSuccess ||
-        hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreateWithFlags(&c->evFork, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->evJoin, hipEventDisableTiming) != hipSuccess) {
+        hipMalloc(&c->dCtr, kMaxHalves * 8 * sizeof(unsigned int)) != hipSuccess ||
+        hipHostMalloc(&c->hCtr, kMaxHalves * kPollRing * 8 * sizeof(unsigned int)) != hipSuccess ||
+        hipEventCreateWithFlags(&c->evFork, hipEventDisableTiming) != hipSuccess) {
         delete c;
         return SKIRT_ERR_HIP;
     }
+    for (int h = 0; h < kMaxHalves; h++)
+        if (hipEventCreateWithFlags(&c->evE[h], hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&c->evT[h], hipEventDisableTiming) != hipSuccess) {
+            delete c;
+            return SKIRT_ERR_HIP;
+        }
+    for (auto& e : c->evJoin)
+        if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
+            delete c;
+            return SKIRT_ERR_HIP;
+        }
+    // pipeline layout (tuning knobs; see runPhase)
+    if (const char* s = getenv("SKIRT_AMD_HALVES")) c->halves = std::max(1, std::min(kMaxHalves, atoi(s)));
+    if (const char* s = getenv("SKIRT_AMD_TRACE_CUS")) c->cusT = std::max(0, atoi(s));
+    if (const char* s = getenv("SKIRT_AMD_EVENT_CUS")) c->cusE = std::max(0, atoi(s));
     c->stream = c->own;
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) == hipSuccess) {
@@ -3140,6 +3310,7 @@ int skirt_mcrt_upload_grid(SkirtMcrt* c, const SkirtGridDesc* g) {
         if (N < 1 || !g->site || !g->cell_nbr_offset || !g->cell_nbr_list || !g->cell_bbox || g->nblocks < 1 ||
             !g->block_offset || !g->block_list)
             return fail(c, SKIRT_ERR_ARG, "bad Voronoi grid");
+        if (N > kCellMaskOut) return fail(c, SKIRT_ERR_UNSUPPORTED, "more than 2^28 Voronoi cells");
         const int nnbr = g->cell_nbr_offset[N];
         for (int m = 0; m < N; m++)
             if (g->cell_nbr_offset[m] < 0 || g->cell_nbr_offset[m] > g->cell_nbr_offset[m + 1])
@@ -3407,6 +3578,8 @@ int skirt_mcrt_zero_tallies(SkirtMcrt* c) {
     if (c->dTally && c->nInstrTally) HIPCHECK(c, hipMemsetAsync(c->dTally, 0, c->nInstrTally * sizeof(double), c->stream));
     HIPCHECK(c, hipMemsetAsync(c->dStats, 0, 8 * kStatCopies * sizeof(unsigned long long), c->stream));
     HIPCHECK(c, hipMemsetAsync(c->dError, 0, sizeof(unsigned int), c->stream));
+    if (c->dCrossed)
+        HIPCHECK(c, hipMemsetAsync(c->dCrossed, 0, (size_t)kCrossedCopies * c->crossedBins * sizeof(unsigned long long), c->stream));
     c->instrReduced = false;
     return SKIRT_OK;
 }
@@ -3613,9 +3786,10 @@ int skirt_mcrt_reduce_instruments(SkirtMcrt* c) {
     if (!c) return SKIRT_ERR_ARG;
     if (!c->reduce || c->instrReduced || !c->dTally || !c->nInstrTally) return SKIRT_OK;
     HIPCHECK(c, hipSetDevice(c->device));
-    c->instrReduced = true;
+    // marked summed only once the reducer succeeded: a failed reduction can be retried
     if (c->reduce(c->reduceUser, SKIRT_TALLY_INSTRUMENTS, c->dTally, c->nInstrTally, (void*)c->stream))
         return fail(c, SKIRT_ERR_STATE, "the instrument reduction failed");
+    c->instrReduced = true;
     return SKIRT_OK;
 }
 
@@ -3674,10 +3848,17 @@ static int runPhase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, uint6
     // of every path replace the ones at the interaction points; fewer slots, each with a longer queue
     const bool continuous = p->continuous_scattering && phase != SKIRT_PHASE_DUST_SELFABS && p->has_dust &&
                             !c->instr.empty();
-    if (continuous) slots = std::min(slots, kContSlots);
+    // (the queue holds kPathCap peel-offs per instrument and slot: the slots shrink with the instruments)
+    if (continuous) slots = std::min(slots, std::max(64, kContSlots / std::max(1, (int)c->instr.size())));
     if ((uint64_t)slots > count) slots = (int)count;
-    slots = std::max(slots, 64 * kHalves) / kHalves;  // per half
-    if ((rc = ensurePool(c, slots, continuous))) return rc;
+    const int halves = (continuous || !p->has_dust || slots < 2 * 64 * kMaxHalves) ? 1 : c->halves;
+    slots = std::max(slots, 64 * halves) / halves;  // per half
+    if ((rc = ensurePool(c, slots, continuous, halves))) return rc;
+    if ((rc = ensureStreams(c))) return rc;
+    const bool forked = c->halves > 1 || c->cusT || c->cusE;  // the pipeline runs on the owned streams
+    hipStream_t sE = forked ? c->sE : c->stream;
+    hipStream_t sT[kMaxHalves];
+    for (int h = 0; h < kMaxHalves; h++) sT[h] = forked ? c->sT[h] : c->stream;
 
     Args a{};
     a.ncells = c->ncells;
@@ -3725,6 +3906,7 @@ static int runPhase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, uint6
     a.labs = phase == SKIRT_PHASE_DUST_SELFABS ? c->dLabsDust : c->dLabs;
     a.tally = c->dTally;
     a.error = c->dError; a.stats = c->dStats;
+    a.crossed = c->dCrossed; a.crossedBins = c->crossedBins;
     a.claim = c->dClaim;
     a.threshold = c->threshold;
     // LDS layout (doubles): mesh | optics | instruments | SED sums
@@ -3741,7 +3923,8 @@ static int runPhase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, uint6
     a.ldsSedOff = off;
     off += c->nsed;
     const size_t ldsTrace = (size_t)a.ldsInstrOff * sizeof(double)          // grid tables + optics
-                            + (size_t)kLabsBuf * kBlock * (sizeof(double) + sizeof(unsigned));  // + Labs buffers
+                            + (size_t)kLabsBuf * kBlock * (sizeof(double) + sizeof(unsigned))  // + Labs buffers
+                            + (size_t)3 * (kBlock / 64) * sizeof(unsigned);               // + segment counts
     const size_t ldsEvent = (size_t)a.ldsSedOff * sizeof(double);           // + instruments
     // budget: what one workgroup may allocate (160 KiB on gfx950). The trace and event kernels need their
     // tables; the detect kernel keeps as many SED copies as fit (8, 4, 2, 1), or none (SEDs to the tally)
@@ -3791,19 +3974,22 @@ static int runPhase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, uint6
     if (tgrid <= 0) {
         int per = 0;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, traceFn, kBlock, ldsTrace) != hipSuccess || per < 1) per = 2;
-        tgrid = std::max(1, c->numCUs) * per;
+        tgrid = std::max(1, c->nCusT) * per;
+        c->traceBlocksPerCU = per;
     }
     // event kernel blocks per CU (SKIRT_AMD_EVENT_BPC: tuning knob)
     static const int ebpc = getenv("SKIRT_AMD_EVENT_BPC") ? std::max(1, atoi(getenv("SKIRT_AMD_EVENT_BPC"))) : 2;
-    const int egrid = std::max(1, std::min((slots + kBlock - 1) / kBlock, std::max(1, c->numCUs) * ebpc));
-    const int dgrid = std::max(1, std::max(1, c->numCUs) * 4);
+    const int egrid = std::max(1, std::min((slots + kBlock - 1) / kBlock, std::max(1, c->nCusE) * ebpc));
+    const int dgrid = std::max(1, std::max(1, c->nCusE) * 4);
 
     HIPCHECK(c, hipMemsetAsync(c->dClaim, 0, sizeof(unsigned long long), c->stream));
-    HIPCHECK(c, hipMemsetAsync(c->dCtr, 0, kHalves * 8 * sizeof(unsigned int), c->stream));
+    HIPCHECK(c, hipMemsetAsync(c->dCtr, 0, kMaxHalves * 8 * sizeof(unsigned int), c->stream));
     HIPCHECK(c, hipEventRecord(c->ev0, c->stream));
-    HIPCHECK(c, hipEventRecord(c->evFork, c->stream));
-    HIPCHECK(c, hipStreamWaitEvent(c->aux, c->evFork, 0));
-    hipStream_t streams[2] = {c->stream, c->aux};
+    if (forked) {  // the pipeline streams start after the caller's stream
+        HIPCHECK(c, hipEventRecord(c->evFork, c->stream));
+        HIPCHECK(c, hipStreamWaitEvent(sE, c->evFork, 0));
+        for (int h = 0; h < halves; h++) HIPCHECK(c, hipStreamWaitEvent(sT[h], c->evFork, 0));
+    }
     auto launchEvent = [&](const Args& aa, hipStream_t st) {
 #define SKIRT_EVENT(G, O) hipLaunchKernelGGL((eventKernel<G, O>), dim3(egrid), dim3(kBlock), ldsEvent, st, aa)
         if (kind == SKIRT_GRID_CARTESIAN) { if (one) SKIRT_EVENT(SKIRT_GRID_CARTESIAN, true); else SKIRT_EVENT(SKIRT_GRID_CARTESIAN, false); }
@@ -3829,8 +4015,8 @@ static int runPhase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, uint6
         void* args[] = {const_cast<Args*>(&aa)};
         return hipLaunchKernel(traceFn, dim3(tgrid), dim3(kBlock), args, ldsTrace, st);
     };
-    if ((int)c->pollEv.size() < kHalves * kPollRing) {
-        while ((int)c->pollEv.size() < kHalves * kPollRing) {
+    if ((int)c->pollEv.size() < kMaxHalves * kPollRing) {
+        while ((int)c->pollEv.size() < kMaxHalves * kPollRing) {
             hipEvent_t e;
             HIPCHECK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
             c->pollEv.push_back(e);
@@ -3839,76 +4025,54 @@ static int runPhase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, uint6
     // Per half, iteration it (parity q = it & 1): the event kernel consumes active list ctr[2+q] and
     // queues rays into ctr[q] and the next active list into ctr[2+1-q]; the trace kernel walks the
     // ctr[q] rays and resets ctr[1-q] and ctr[2+q] for the next iteration; the detect kernel turns the
-    // finished peel-off rays into detections. Every kPollEvery iterations the half's counters are
-    // copied to pinned memory behind an event; the host reads each copy kPollRing copies later (by
-    // then long complete), so it never drains a stream. A half whose active count was 0 is finished;
-    // the few iterations launched after that point find no work and exit at once.
-    Args ah[kHalves];
-    int its[kHalves] = {0}, polls[kHalves] = {0};
-    int pollIt[kHalves][kPollRing] = {};  // the iteration count each copy was taken at
-    bool done[kHalves] = {false};
-    for (int h = 0; h < kHalves; h++) {
+    // finished peel-off rays into detections. After every detect kernel the half's counters are copied
+    // to pinned memory behind an event; the host reads each copy kPollRing copies later (by then long
+    // complete), so it never drains a stream. A half whose active count was 0 is finished; the few
+    // iterations launched after that point find no work and exit at once.
+    // Stream order: sE runs, per half in turn, the detect kernel of the half's last iteration and the
+    // event kernel of its next one; sT[h] runs the half's trace kernels. With two halves, one half's
+    // detect + event kernels thus run while the other half's trace kernel runs (on CUs of their own when
+    // the streams are CU-masked): sE = ev0(0) ev1(0) det0(0) ev0(1) det1(0) ev1(1) ...; sT[0] = tr0(0)
+    // tr0(1) ...; each kernel waits only for its own half's previous kernel on the other stream.
+#ifdef SKIRT_EXPERIMENT_TIMELINE
+    // the timeline of the phase call number SKIRT_AMD_TIMELINE_CALL (default 2: after a warm-up call)
+    static int tlCall = 0;
+    const char* tlOut = getenv("SKIRT_AMD_TIMELINE_OUT");
+    const int tlWant = getenv("SKIRT_AMD_TIMELINE_CALL") ? atoi(getenv("SKIRT_AMD_TIMELINE_CALL")) : 2;
+    unsigned long long* dTl = nullptr;
+    const size_t tlWords = (size_t)3 * kTlLaunches * kTlWaves * kTlWords;
+    if (tlOut && ++tlCall == tlWant) {
+        HIPCHECK(c, hipMalloc(&dTl, tlWords * 8));
+        HIPCHECK(c, hipMemsetAsync(dTl, 0, tlWords * 8, c->stream));
+    }
+    a.tl = dTl;
+    a.tlLaunch = 0;
+#endif
+    Args ah[kMaxHalves], prev[kMaxHalves];
+    int its[kMaxHalves] = {0}, polls[kMaxHalves] = {0};
+    int pollIt[kMaxHalves][kPollRing] = {};  // the iteration count each copy was taken at
+    bool done[kMaxHalves] = {false}, pendingDet[kMaxHalves] = {false};
+    for (int h = 0; h < halves; h++) {
         ah[h] = a;
         carvePool(c, ah[h], h);
     }
-#if SKIRT_DETECT_OVERLAP
-    DetRec* const detBase = ah[0].det;
-    const size_t detHalf = (size_t)(c->rayCap - c->nslots);
-    hipEvent_t trDone, detDone[2];
-    HIPCHECK(c, hipEventCreateWithFlags(&trDone, hipEventDisableTiming));
-    HIPCHECK(c, hipEventCreateWithFlags(&detDone[0], hipEventDisableTiming));
-    HIPCHECK(c, hipEventCreateWithFlags(&detDone[1], hipEventDisableTiming));
-#endif
+    // the detect kernel of half h's last trace launch (on sE, after that launch), then the counter copy
+    auto detect = [&](int h) -> int {
+        pendingDet[h] = false;
+        if (sE != sT[h]) HIPCHECK(c, hipStreamWaitEvent(sE, c->evT[h], 0));
+        hipLaunchKernelGGL(detectKernel, dim3(dgrid), dim3(kBlock), ldsDetect, sE, prev[h]);
+        HIPCHECK(c, hipGetLastError());
+        return SKIRT_OK;
+    };
     int total = 0;
     while (true) {
         bool all = true;
-        for (int h = 0; h < kHalves; h++) {
+        for (int h = 0; h < halves; h++) {
             if (done[h]) continue;
             all = false;
             Args& aa = ah[h];
-            hipStream_t st = streams[h];
-            aa.parity = its[h] & 1;
-            aa.init = (its[h] == 0) ? 1 : 0;
-#if SKIRT_DETECT_OVERLAP
-            // this parity's records and counter are free once the detect kernel of two iterations ago ends
-            aa.det = detBase + (size_t)aa.parity * detHalf;
-            if (its[h] >= 2) HIPCHECK(c, hipStreamWaitEvent(st, detDone[aa.parity], 0));
-#endif
-            if (aa.continuous && !aa.init) {  // the continuous peel-offs of the FILL rays that just returned
-                launchCont(aa, st);
-                HIPCHECK(c, hipGetLastError());
-            }
-            launchEvent(aa, st);
-            HIPCHECK(c, hipGetLastError());
-            if (!a.hasDust) { done[h] = true; its[h]++; continue; }  // every packet completes in the event kernel
-            if ((int)c->traceEv.size() < 2 * (c->traceLaunches + 1)) {
-                hipEvent_t e0, e1;
-                HIPCHECK(c, hipEventCreate(&e0));
-                HIPCHECK(c, hipEventCreate(&e1));
-                c->traceEv.push_back(e0);
-                c->traceEv.push_back(e1);
-            }
-            HIPCHECK(c, hipEventRecord(c->traceEv[2 * c->traceLaunches], st));
-            HIPCHECK(c, launchTrace(aa, st));
-            HIPCHECK(c, hipGetLastError());
-            HIPCHECK(c, hipEventRecord(c->traceEv[2 * c->traceLaunches + 1], st));
-            c->traceLaunches++;
-            if (a.ninstr > 0) {
-#if SKIRT_DETECT_OVERLAP
-                HIPCHECK(c, hipEventRecord(trDone, st));
-                HIPCHECK(c, hipStreamWaitEvent(c->aux, trDone, 0));
-                hipLaunchKernelGGL(detectKernel, dim3(dgrid), dim3(kBlock), ldsDetect, c->aux, aa);
-                HIPCHECK(c, hipGetLastError());
-                HIPCHECK(c, hipMemsetAsync(aa.ctr + 5 + aa.parity, 0, sizeof(unsigned int), c->aux));
-                HIPCHECK(c, hipEventRecord(detDone[aa.parity], c->aux));
-#else
-                hipLaunchKernelGGL(detectKernel, dim3(dgrid), dim3(kBlock), ldsDetect, st, aa);
-                HIPCHECK(c, hipGetLastError());
-#endif
-            }
-            its[h]++;
-            total++;
-            if (its[h] % kPollEvery == 0) {
+            if (pendingDet[h] && (rc = detect(h))) return rc;
+            if (its[h] > 0 && its[h] % kPollEvery == 0) {
                 const int slot = polls[h] % kPollRing;
                 unsigned int* hc = c->hCtr + (h * kPollRing + slot) * 8;
                 hipEvent_t pe = c->pollEv[h * kPollRing + slot];
@@ -3917,24 +4081,73 @@ static int runPhase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, uint6
                     HIPCHECK(c, hipEventSynchronize(pe));
                     if (hc[2 + (pollIt[h][slot] & 1)] == 0) { done[h] = true; continue; }
                 }
-                HIPCHECK(c, hipMemcpyAsync(hc, aa.ctr, 8 * sizeof(unsigned int), hipMemcpyDeviceToHost, st));
-                HIPCHECK(c, hipEventRecord(pe, st));
+                HIPCHECK(c, hipMemcpyAsync(hc, aa.ctr, 8 * sizeof(unsigned int), hipMemcpyDeviceToHost, sE));
+                HIPCHECK(c, hipEventRecord(pe, sE));
                 pollIt[h][slot] = its[h];
                 polls[h]++;
             }
             if (its[h] > 10000000) return fail(c, SKIRT_ERR_STATE, "photon phase did not terminate");
+            aa.parity = its[h] & 1;
+            aa.init = (its[h] == 0) ? 1 : 0;
+#ifdef SKIRT_EXPERIMENT_TIMELINE
+            aa.tlLaunch = its[h] * halves + h;
+#endif
+            if (aa.continuous && !aa.init) {  // the continuous peel-offs of the FILL rays that just returned
+                launchCont(aa, sE);
+                HIPCHECK(c, hipGetLastError());
+            }
+            launchEvent(aa, sE);
+            HIPCHECK(c, hipGetLastError());
+            if (!a.hasDust) { done[h] = true; its[h]++; continue; }  // every packet completes in the event kernel
+            if (sE != sT[h]) {
+                HIPCHECK(c, hipEventRecord(c->evE[h], sE));
+                HIPCHECK(c, hipStreamWaitEvent(sT[h], c->evE[h], 0));
+            }
+            if ((int)c->traceEv.size() < 2 * (c->traceLaunches + 1)) {
+                hipEvent_t e0, e1;
+                HIPCHECK(c, hipEventCreate(&e0));
+                HIPCHECK(c, hipEventCreate(&e1));
+                c->traceEv.push_back(e0);
+                c->traceEv.push_back(e1);
+            }
+            HIPCHECK(c, hipEventRecord(c->traceEv[2 * c->traceLaunches], sT[h]));
+            HIPCHECK(c, launchTrace(aa, sT[h]));
+            HIPCHECK(c, hipGetLastError());
+            HIPCHECK(c, hipEventRecord(c->traceEv[2 * c->traceLaunches + 1], sT[h]));
+            c->traceLaunches++;
+            if (sE != sT[h]) HIPCHECK(c, hipEventRecord(c->evT[h], sT[h]));
+            if (a.ninstr > 0) { prev[h] = aa; pendingDet[h] = true; }
+            its[h]++;
+            total++;
         }
         if (all) break;
     }
+    for (int h = 0; h < halves; h++)
+        if (pendingDet[h] && (rc = detect(h))) return rc;
     int it = total;
     c->lastIterations = it;
-    HIPCHECK(c, hipEventRecord(c->evJoin, c->aux));
-    HIPCHECK(c, hipStreamWaitEvent(c->stream, c->evJoin, 0));
+    if (forked) {  // the caller's stream continues after the pipeline streams
+        HIPCHECK(c, hipEventRecord(c->evJoin[0], sE));
+        HIPCHECK(c, hipStreamWaitEvent(c->stream, c->evJoin[0], 0));
+        for (int h = 0; h < halves; h++) {
+            HIPCHECK(c, hipEventRecord(c->evJoin[1 + h], sT[h]));
+            HIPCHECK(c, hipStreamWaitEvent(c->stream, c->evJoin[1 + h], 0));
+        }
+    }
     HIPCHECK(c, hipEventRecord(c->ev1, c->stream));
-#if SKIRT_DETECT_OVERLAP
-    (void)hipEventDestroy(trDone);
-    (void)hipEventDestroy(detDone[0]);
-    (void)hipEventDestroy(detDone[1]);
+#ifdef SKIRT_EXPERIMENT_TIMELINE
+    if (dTl) {
+        std::vector<unsigned long long> h(tlWords);
+        HIPCHECK(c, hipStreamSynchronize(c->stream));
+        HIPCHECK(c, hipMemcpy(h.data(), dTl, tlWords * 8, hipMemcpyDeviceToHost));
+        (void)hipFree(dTl);
+        if (FILE* f = fopen(tlOut, "wb")) {
+            const int hdr[5] = {3, kTlLaunches, kTlWaves, it, kTlWords};
+            fwrite(hdr, sizeof hdr, 1, f);
+            fwrite(h.data(), 8, tlWords, f);
+            fclose(f);
+        }
+    }
 #endif
     return SKIRT_OK;
 }
@@ -3996,6 +4209,38 @@ int skirt_mcrt_download(SkirtMcrt* c, double* labs, double* instr) {
     return SKIRT_OK;
 }
 
+int skirt_mcrt_set_crossed(SkirtMcrt* c, int bins) {
+    if (!c || bins < 0 || bins > (1 << 20)) return SKIRT_ERR_ARG;
+    HIPCHECK(c, hipSetDevice(c->device));
+    if (c->dCrossed) {
+        HIPCHECK(c, hipStreamSynchronize(c->stream));
+        (void)hipFree(c->dCrossed);
+        c->dCrossed = nullptr;
+    }
+    c->crossedBins = bins;
+    if (!bins) return SKIRT_OK;
+    const size_t n = (size_t)kCrossedCopies * bins;
+    HIPCHECK(c, hipMalloc(&c->dCrossed, n * sizeof(unsigned long long)));
+    HIPCHECK(c, hipMemsetAsync(c->dCrossed, 0, n * sizeof(unsigned long long), c->stream));
+    return SKIRT_OK;
+}
+
+int skirt_mcrt_download_crossed(SkirtMcrt* c, uint64_t* hist, int bins) {
+    if (!c || !hist || bins < 0) return SKIRT_ERR_ARG;
+    if (!c->dCrossed) return fail(c, SKIRT_ERR_STATE, "the cells-crossed histogram is off (skirt_mcrt_set_crossed)");
+    HIPCHECK(c, hipSetDevice(c->device));
+    HIPCHECK(c, hipStreamSynchronize(c->stream));
+    std::vector<unsigned long long> h((size_t)kCrossedCopies * c->crossedBins);
+    HIPCHECK(c, hipMemcpy(h.data(), c->dCrossed, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    for (int b = 0; b < bins; b++) {
+        uint64_t v = 0;
+        if (b < c->crossedBins)
+            for (int k = 0; k < kCrossedCopies; k++) v += h[(size_t)k * c->crossedBins + b];
+        hist[b] = v;
+    }
+    return SKIRT_OK;
+}
+
 int skirt_mcrt_stats(SkirtMcrt* c, SkirtStats* out) {
     if (!c || !out) return SKIRT_ERR_ARG;
     HIPCHECK(c, hipSetDevice(c->device));
@@ -4020,6 +4265,7 @@ int skirt_mcrt_stats(SkirtMcrt* c, SkirtStats* out) {
     out->map_level = c->mapL;
     out->labs_requests = v[7];
     out->device_cells = c->ndev;
+    out->trace_blocks_per_cu = (uint64_t)c->traceBlocksPerCU;
     return SKIRT_OK;
 }
 
@@ -4035,7 +4281,7 @@ void skirt_mcrt_destroy(SkirtMcrt* c) {
                     c->dEmisScratch, c->dDevCell, c->dSite, c->dCellBbox, c->dVorStart, c->dVorSlots,
                     c->dBlockOffset, c->dBlockList, c->dRho,
                     c->dOptics, c->dGeomParam, c->dGeomTable, c->dLum, c->dLumtot, c->dCdf, c->dInstr,
-                    c->dClaim, c->dStats, c->dError, c->dCtr, c->dPool};
+                    c->dClaim, c->dStats, c->dError, c->dCtr, c->dPool, c->dCrossed};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     if (c->hCtr) (void)hipHostFree(c->hCtr);
@@ -4045,8 +4291,14 @@ void skirt_mcrt_destroy(SkirtMcrt* c) {
     for (hipEvent_t e : c->traceEv) (void)hipEventDestroy(e);
     for (hipEvent_t e : c->pollEv) (void)hipEventDestroy(e);
     if (c->evFork) (void)hipEventDestroy(c->evFork);
-    if (c->evJoin) (void)hipEventDestroy(c->evJoin);
-    if (c->aux) (void)hipStreamDestroy(c->aux);
+    for (hipEvent_t e : c->evJoin)
+        if (e) (void)hipEventDestroy(e);
+    for (int h = 0; h < kMaxHalves; h++) {
+        if (c->evE[h]) (void)hipEventDestroy(c->evE[h]);
+        if (c->evT[h]) (void)hipEventDestroy(c->evT[h]);
+        if (c->sT[h]) (void)hipStreamDestroy(c->sT[h]);
+    }
+    if (c->sE) (void)hipStreamDestroy(c->sE);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->own) (void)hipStreamDestroy(c->own);

@@ -1423,6 +1423,7 @@ Model loadSki(const std::string& path, UniformSource& rng, const std::string& da
         m.sampleCount = attrInt(ds, "sampleCount", 100);
         m.writeConvergence = attrBool(ds, "writeConvergence", true);
         m.writeCellProperties = attrBool(ds, "writeCellProperties", false);
+        m.writeCellsCrossed = attrBool(ds, "writeCellsCrossed", false);
         if (pds) {
             m.dustEmission = ds->item("dustEmissivity") != nullptr;
             m.selfAbsorption = m.dustEmission && attrBool(ds, "selfAbsorption", false);

@@ -229,6 +229,7 @@ struct Model {
     double emissionBoost = 1;
     int cycles = 0;
     bool writeISRF = false, writeCellProperties = false, writeMeanIntensity = false, writeConvergence = false;
+    bool writeCellsCrossed = false;  // DustSystem writeCellsCrossed: the ds_crossed path histogram
     int sampleCount = 100;
 
     std::vector<Instrument> instruments;

@@ -308,4 +308,14 @@ void writeOutputs(const Model& m, const std::string& prefix, const std::vector<s
     }
 }
 
+void writeCellsCrossed(const Model& m, const std::string& prefix, const std::vector<uint64_t>& hist) {
+    size_t n = hist.size();
+    while (n > 0 && hist[n - 1] == 0) n--;
+    TextOut f(prefix + "_ds_crossed.dat");
+    f.line("# total number of cells in grid: " + std::to_string(m.ncells()));
+    f.column("number of cells crossed", 'd');
+    f.column("number of paths that crossed this number of cells", 'd');
+    for (size_t i = 0; i < n; i++) f.row({(double)i, (double)hist[i]});
+}
+
 }  // namespace skirt

@@ -9,6 +9,7 @@
 //   TextOutFile column formats (TextOutFile.cpp:46-90, Qt QString::number formatting).
 #pragma once
 
+#include <cstdint>
 #include <string>
 #include <vector>
 
@@ -21,6 +22,10 @@ namespace skirt {
 // <prefix>_<instr>_<name>.fits, and <prefix>_ds_isrf.dat / _ds_cellprops.dat when the model asks for them.
 void writeOutputs(const Model& m, const std::string& prefix, const std::vector<std::vector<double>>& frames,
                   const std::vector<std::vector<double>>& seds, const std::vector<double>& labs);
+
+// DustSystem::write (DustSystem.cpp:1004-1024): <prefix>_ds_crossed.dat, hist[n] = paths that crossed n
+// cells, written up to the last nonzero bin
+void writeCellsCrossed(const Model& m, const std::string& prefix, const std::vector<uint64_t>& hist);
 
 // Qt-compatible number formatting: QString::number(v, 'e', prec) and QString::number(v, 'g', prec)
 std::string qtNumber(double v, char fmt, int prec);

@@ -17,6 +17,8 @@
 using namespace skirt;
 
 namespace {
+
+constexpr int kCrossedBins = 16384;  // cells-crossed histogram bins (ds_crossed; the last counts longer paths)
 thread_local std::string g_err;
 }
 
@@ -266,6 +268,8 @@ int skirt_sim_attach(SkirtSim* s, int device) {
     skirt_mcrt_tally_sizes(s->eng, &nl, &ni);
     // the device tally pads each frame pixel's slots to a 64-byte line; downloads restore this layout
     if (ni < s->instrAll.size()) { g_err = "instrument tally size mismatch"; return SKIRT_ERR_STATE; }
+    // DustSystem writeCellsCrossed: the engine keeps the cells-crossed histogram for ds_crossed
+    if (m.hasDust && m.writeCellsCrossed && (rc = check(s, skirt_mcrt_set_crossed(s->eng, kCrossedBins)))) return rc;
     return check(s, skirt_mcrt_zero_tallies(s->eng));
 }
 
@@ -391,7 +395,14 @@ int skirt_sim_run_dust_shard(SkirtSim* s, int rank, int world) {
     }
 }
 
-const double* skirt_sim_labs_dust(SkirtSim* s) { return s && !s->labsDust.empty() ? s->labsDust.data() : nullptr; }
+const double* skirt_sim_labs_dust(SkirtSim* s) {
+    if (!s || s->labsDust.empty()) return nullptr;
+    if (s->dustLabsOnDevice) {  // still on the device (skirt_sim_fetch not called yet): download it now
+        if (!s->eng || check(s, skirt_mcrt_download_dust_labs(s->eng, s->labsDust.data()))) return nullptr;
+        s->dustLabsOnDevice = false;
+    }
+    return s->labsDust.data();
+}
 
 int skirt_sim_selfabs_totals(SkirtSim* s, const double** totals) {
     if (!s || !totals) return -1;
@@ -444,6 +455,12 @@ int skirt_sim_write(SkirtSim* s, const char* prefix) {
     try {
         writeOutputs(s->m, prefix, s->frames, s->seds,
                      totalLabs(s->m, s->labs, s->labsDust.empty() ? nullptr : &s->labsDust));
+        if (s->m.hasDust && s->m.writeCellsCrossed && s->eng) {
+            std::vector<uint64_t> hist(kCrossedBins);
+            int rc = check(s, skirt_mcrt_download_crossed(s->eng, hist.data(), kCrossedBins));
+            if (rc) return rc;
+            writeCellsCrossed(s->m, prefix, hist);
+        }
     } catch (std::exception& e) {
         g_err = e.what();
         return SKIRT_ERR_ARG;

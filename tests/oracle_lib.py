@@ -50,6 +50,9 @@ def lib():
         L.oracle_segments.restype = ctypes.c_uint64
         L.oracle_segments.argtypes = [ctypes.c_void_p]
         L.oracle_free.argtypes = [ctypes.c_void_p]
+        L.oracle_set_engine_attenuation.argtypes = [ctypes.c_int]
+        L.oracle_counts.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64)]
+        L.oracle_crossed.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.POINTER(ctypes.c_uint64))]
         L.oracle_labs_dust.restype = ctypes.POINTER(ctypes.c_double)
         L.oracle_labs_dust.argtypes = [ctypes.c_void_p]
         L.oracle_selfabs_cycles.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.POINTER(ctypes.c_double))]
@@ -85,6 +88,25 @@ class OracleResult:
         self.seconds = L.oracle_seconds(handle)
         self.packets = L.oracle_packets(handle)
         self.segments = L.oracle_segments(handle)
+        c = (ctypes.c_uint64 * 3)()
+        L.oracle_counts(handle, c)
+        # segments of the FILL paths and of the peel-off paths, Labs adds (the engine's statistics)
+        self.segments_fill, self.segments_peel, self.absorb_adds = int(c[0]), int(c[1]), int(c[2])
+        hp = ctypes.POINTER(ctypes.c_uint64)()
+        n = L.oracle_crossed(handle, ctypes.byref(hp))
+        # DustSystem's _crossed histogram: paths per number of segments
+        self.crossed = np.ctypeslib.as_array(hp, shape=(n,)).copy() if n > 0 else np.zeros(0, np.uint64)
+
+
+class engine_attenuation:
+    """Context: the oracle evaluates the absorption's exp(-tau_{n-1}) as the engine's running product (see
+    oracle_set_engine_attenuation), to separate that arithmetic from everything else in a comparison."""
+
+    def __enter__(self):
+        lib().oracle_set_engine_attenuation(1)
+
+    def __exit__(self, *exc):
+        lib().oracle_set_engine_attenuation(0)
 
 
 def run(ski, rng=RNG_MT, threads=1, packages=0.0, seed=0, packet_begin=0, packet_end=0, outprefix=None,

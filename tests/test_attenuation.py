@@ -1,0 +1,47 @@
+"""The named cause of the engine's deep-cell differences on optically thick models (tests/parity.py).
+
+The reference sums a packet's absorption along a path with exp(-taustart) per segment
+(MonteCarloSimulation.cpp:458-462). The engine carries exp(-tau) as the running product of
+1 - (-expm1(-dtau)) over the path. Both agree to a few ulp per factor while dtau is small. Behind an
+optically thick segment, 1 - (1 - exp(-dtau)) cancels: the product keeps only about 1e-16 / exp(-dtau) relative
+accuracy (dtau = 30: 1.7e-4). These tests reproduce that on the CPU, with the oracle switched to the engine's
+form (oracle_set_engine_attenuation). The differences it makes there match the GPU's (test_gpu_parity.py):
+a few tens of deep cells on the 3e6 Msun pan_oct_sa models, with a mass below 1e-18 of the table. The
+thin models show none. With the switch on, the engine equals the oracle on the thick models too
+(test_dust_phases_match_oracle_same_streams)."""
+import os
+
+import numpy as np
+
+import oracle_lib as O
+from parity import outliers
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "ski")
+
+
+def test_product_of_complements_cancels_behind_thick_segments():
+    rel = []
+    for dtau in (1.0, 10.0, 20.0, 30.0):
+        prod = 1.0 - (-np.expm1(-dtau))
+        rel.append(abs(prod - np.exp(-dtau)) / np.exp(-dtau))
+    assert rel[0] < 1e-15 and rel[1] < 1e-12
+    assert 1e-9 < rel[2] < 1e-6 and rel[3] > 1e-5
+
+
+def _labs(name, product):
+    path = os.path.join(GOLD, name + ".ski")
+    if product:
+        with O.engine_attenuation():
+            return O.run(path, rng=O.RNG_PHILOX, threads=8, packages=300).labs
+    return O.run(path, rng=O.RNG_PHILOX, threads=8, packages=300).labs
+
+
+def test_engine_attenuation_form_changes_only_deep_cells_of_thick_models():
+    # thin octree model: the two forms agree to rounding
+    n, _, worst, _, _ = outliers(_labs("pan_oct", False), _labs("pan_oct", True), 1e-9)
+    assert n == 0 and worst < 1e-12
+    # the thick (3e6 Msun) self-absorption model: outliers, all in cells of negligible mass
+    n, drift, worst, mass, cmp = outliers(_labs("pan_oct_sa", False), _labs("pan_oct_sa", True), 1e-9)
+    assert 0 < n + drift < 0.01 * cmp
+    assert 1e-7 < worst < 1e-2
+    assert mass < 1e-18

@@ -1,0 +1,91 @@
+"""The inputs of the roofline, pinned: bench.py prices a trace launch from the engine's own counters
+(segments of the FILL, WALK and peel-off paths, Labs adds), so these counters must equal
+what the reference's algorithm does on the same packets. On the same Philox streams the oracle counts
+the segments of every path it builds (DustSystem::fillOpticalDepth and ::opticaldepth, i.e. DustGrid::path,
+DustSystem.cpp:959-1000) and every absorption add (simulateescapeandabsorption, MonteCarloSimulation.cpp:
+438-515); the engine's device counters must give the same numbers, and its cells-crossed histogram
+(DustSystem's _crossed, written as ds_crossed, DustSystem.cpp:1004-1024) the same histogram.
+
+The engine's WALK rays (the walk to the interaction point) have no counterpart in the reference, which
+interpolates in the stored FILL path (DustGridPath::pathlength): they are bounded, not compared."""
+import os
+
+import numpy as np
+import pytest
+
+import oracle_lib as O
+import skirt_amd as S
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+GOLD = os.path.join(HERE, "golden", "ski")
+BENCH = os.path.join(HERE, "..", "benchmarks")
+BINS = 4096
+
+
+def _ski(name):
+    return os.path.join(BENCH if name == "c3_oct128" else GOLD, name + ".ski")
+
+
+CASES = [
+    # name, packets per wavelength, with the dust phases
+    ("pan_cart16", 3000, False),
+    ("pan_oct", 3000, False),
+    ("vor_pan", 1000, False),
+    ("pan_cart16_sa", 1000, True),
+    ("c3_oct128", 20, False),  # the headline workload at full grid size (622,490 leaves)
+]
+
+
+@pytest.mark.parametrize("name,packages,dust", CASES, ids=[c[0] for c in CASES])
+def test_engine_counts_equal_oracle_counts(name, packages, dust):
+    path = _ski(name)
+    sim = S.Simulation(path, packages=packages)
+    sim.attach(0)
+    sim.set_crossed(BINS)
+    sim.zero_tallies()
+    sim.run_stellar()
+    if dust:
+        sim.run_dust()
+    sim.fetch()
+    st = sim.stats()
+    hist = sim.crossed(BINS)
+    orc = O.run(path, rng=O.RNG_PHILOX, threads=16, packages=packages,
+                phases=O.PHASES_ALL if dust else O.PHASES_STELLAR)
+    assert st["packets"] == orc.packets
+    got = {k: st[k] for k in ("segments_fill", "segments_peel", "absorb_adds")}
+    want = {"segments_fill": orc.segments_fill, "segments_peel": orc.segments_peel, "absorb_adds": orc.absorb_adds}
+    print(name, "engine", got, "walk", st["segments_walk"], "oracle", want)
+    assert got == want
+    assert want["absorb_adds"] > 0 and want["segments_peel"] > 0
+    # the walk to the interaction point crosses at most the FILL path's segments
+    assert 0 < st["segments_walk"] <= st["segments_fill"]
+    # the histogram of segments per path: every FILL and peel-off path once
+    n = len(orc.crossed)
+    assert n < BINS
+    np.testing.assert_array_equal(hist[:n], orc.crossed)
+    assert hist[n:].sum() == 0
+    assert int(hist.sum()) > 0
+    assert int((hist * np.arange(BINS, dtype=np.uint64)).sum()) == orc.segments_fill + orc.segments_peel
+
+
+def test_ds_crossed_file_matches_oracle(tmp_path):
+    """writeCellsCrossed="true": the host driver writes <prefix>_ds_crossed.dat from the engine's histogram,
+    in DustSystem::write's format, identical to the oracle's file for the same packets."""
+    text = open(os.path.join(GOLD, "pan_oct.ski")).read().replace('writeCellsCrossed="false"', 'writeCellsCrossed="true"')
+    path = os.path.join(tmp_path, "pan_oct_crossed.ski")
+    with open(path, "w") as f:
+        f.write(text)
+    sim = S.Simulation(path, packages=500)
+    sim.attach(0)
+    sim.run_stellar()
+    sim.run_dust()
+    sim.fetch()
+    sim.write(os.path.join(tmp_path, "gpu"))
+    O.run(path, rng=O.RNG_PHILOX, threads=16, packages=500, phases=O.PHASES_ALL,
+          outprefix=os.path.join(tmp_path, "orc"))
+    gpu = open(os.path.join(tmp_path, "gpu_ds_crossed.dat")).read()
+    orc = open(os.path.join(tmp_path, "orc_ds_crossed.dat")).read()
+    assert gpu.startswith("# total number of cells in grid: ")
+    assert "# column 2: number of paths that crossed this number of cells" in gpu
+    assert gpu == orc

@@ -2,7 +2,12 @@
 every wavelength of every phase (stellar emission, self-absorption cycles, dust emission;
 skirt_mcrt_run_phase_shard), with the engine's reducer summing the tallies where the reference sums them
 (bench.py reduces over RCCL; here gloo on host copies, since both ranks sit on one device). The result
-must equal one unsharded run."""
+must equal one unsharded run.
+
+Two reducer paths run: staged through host copies, and the stream-ordered one bench.py uses -- the
+collective on CUDA tensors inside torch.cuda.stream(ExternalStream(engine stream)), so it is ordered
+after the phase's kernels without a host synchronisation (sharding.py, TallyReducer's ExternalStream
+branch; gloo's CUDA all-reduce here, RCCL in bench.py)."""
 import os
 import socket
 
@@ -27,7 +32,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, outdir):
+def _worker(rank, world, port, outdir, via_host):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -43,7 +48,7 @@ def _worker(rank, world, port, outdir):
         dust = torch.zeros(n_labs, dtype=torch.float64, device="cuda")
         sim.bind_tallies(labs.data_ptr(), instr.data_ptr())
         sim.bind_dust_labs(dust.data_ptr())
-        red = TallyReducer(labs, instr, dust, via_host=True)
+        red = TallyReducer(labs, instr, dust, via_host=via_host)
         sim.set_reducer(red)
         sim.zero_tallies()
         sim.run_stellar_shard(rank, world)  # + Labs summed at the phase end
@@ -63,8 +68,9 @@ def _worker(rank, world, port, outdir):
         dist.destroy_process_group()
 
 
-def test_two_ranks_equal_one_run(tmp_path):
-    mp.spawn(_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+@pytest.mark.parametrize("via_host", [True, False], ids=["host_staged", "stream_ordered"])
+def test_two_ranks_equal_one_run(tmp_path, via_host):
+    mp.spawn(_worker, args=(2, _free_port(), str(tmp_path), via_host), nprocs=2, join=True)
     full = S.Simulation(SKI, packages=PACKAGES)
     full.attach(0)
     full.run_stellar()
