@@ -34,7 +34,8 @@ CONFIGS = {
     "c2": ("benchmarks/c2_cart64.ski", 1000000, 0, "C2 Cartesian 64^3, 10 lambda, peel-off"),
     "c4": ("benchmarks/c4_vor1e5.ski", 200000, 438,
            "C4 Voronoi 1e5 sites (DustDensity), 25 lambda, peel-off"),
-    "c5": ("benchmarks/c5_oct128_sa.ski", 400000, 56,
+    # C5 at its per-GPU share of the 1e9-packet configuration, like C3 (round 2 ran 4e5 per wavelength)
+    "c5": ("benchmarks/c5_oct128_sa.ski", 5000000, 56,
            "C5 = C3 + dust self-absorption (3 cycles) + dust emission, all phases per step"),
 }
 DUST_CONFIGS = ("c5",)

@@ -4,8 +4,8 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 CFG=${CFG:-c3}
-ARGS="bench.py --config $CFG --steps 5 --warmup 1 --no-cpu-baseline"
-OUT=gpurun_out/prof_$CFG
+ARGS="bench.py --config $CFG --steps ${STEPS:-5} --warmup 1 --no-cpu-baseline $BENCH_ARGS"
+OUT=gpurun_out/prof_$CFG${TAG}
 mkdir -p $OUT && rm -rf $OUT/* && echo "python3 $ARGS" > $OUT/cmd.txt
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python3 $ARGS > $OUT/trace.log 2>&1 && echo trace ok &&
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o run -- python3 $ARGS > $OUT/fetch.log 2>&1 && echo fetch ok &&
