@@ -168,10 +168,8 @@ struct alignas(16) VorEntry {
     int next;
 };
 constexpr int kVorHead = 3;  // header slots
-// FMA contraction in the Voronoi step's single-precision bounds (C4 5.33e7 -> 5.45e7 pkt/s)
-#ifndef SKIRT_VOR_CONTRACT
-#define SKIRT_VOR_CONTRACT 1
-#endif
+// bound factor of the approximate (single-precision) plane distances: 16 x 2^-24
+constexpr float kVorEpsF = 1.0f / (1 << 20);
 #ifndef SKIRT_VOR_UNROLL
 #define SKIRT_VOR_UNROLL 8  // at 2 waves/SIMD, no spills (C4 6.17e7 pkt/s; 4: 6.07e7, 2: 5.29e7)
 #endif
@@ -179,9 +177,7 @@ constexpr int kVorUnroll = SKIRT_VOR_UNROLL;
 #ifndef SKIRT_VOR_FALLBACK_GROUP
 #define SKIRT_VOR_FALLBACK_GROUP 2  // neighbour sites loaded together by the exact re-evaluation (<= kVorUnroll)
 #endif
-constexpr int kVorCand = 4;  // possible winners the exact re-evaluation collects before it takes the whole list  // entries loaded per round trip (the slot array is padded)
-// bound factor of the approximate (single-precision) plane distances: 16 x 2^-24
-constexpr float kVorEpsF = 1.0f / (1 << 20);
+constexpr int kVorCand = 4;  // possible winners the exact re-evaluation collects before it takes the whole list
 
 // grid kinds of the kernels: SKIRT_GRID_CARTESIAN, SKIRT_GRID_OCTREE (leaf-map walk), the k-d tree
 // through its leaf map, and any tree walked through the node arrays (trees deeper than the leaf maps
@@ -1091,6 +1087,7 @@ struct Grid<SKIRT_GRID_VORONOI> {
         for (int u = 0; u < kVorUnroll; u++) e[u] = B[kVorHead + u];
         const double pwx = h0.x, pwy = h0.y, pwz = h1.x, rhow = h1.y;
         const int idw = h2.x, cnt = h2.y;
+
         if (r.ck) {
             const double sq = planeDist(r, r.bx0, r.by0, r.bz0, pwx, pwy, pwz);
             if (!seg(r.ci, r.rho0, sq)) return false;
@@ -1103,6 +1100,7 @@ struct Grid<SKIRT_GRID_VORONOI> {
         // kVorEpsF covers with margin; an approximate reciprocal (1 ulp) is covered by the |s| term
         const float sc = a.vorScale;
         const float Dx = (float)((pwx - r.x) * sc), Dy = (float)((pwy - r.y) * sc), Dz = (float)((pwz - r.z) * sc);
+        const float Dn = fabsf(Dx) + fabsf(Dy) + fabsf(Dz);  // >= |D|
         const float fkx = (float)kx, fky = (float)ky, fkz = (float)kz;
         // bounds [lo, hi] of every neighbour's plane distance; U: the least upper bound of the certain
         // exits; L1 <= L2: the two least lower bounds of the possible exits, w1: the first one's `next`.
@@ -1111,22 +1109,20 @@ struct Grid<SKIRT_GRID_VORONOI> {
         float U = FLT_MAX, L1 = FLT_MAX, L2 = FLT_MAX;
         int w1 = 0;
         auto bounds = [&](const VorEntry& en, bool valid, float& lo, float& hi) {
-#if SKIRT_VOR_CONTRACT
-            // FMA contraction in the bounds only: a fused operation rounds once where the bound counts
-            // two roundings, so the intervals stay valid
-#pragma clang fp contract(fast)
-#endif
+            // the plane distance s = (n.D + |n|^2/2) / (n.k) with per-entry Cauchy-Schwarz error terms:
+            // |d(n.k)| <= eA = kVorEpsF |n|_1 and |d(n.D + |n|^2/2)| <= eA |D|_1 + kVorEpsF |n|^2, several
+            // times the float roundings of the offsets, D, k and the fused operations (round 2 summed the
+            // absolute terms of each product instead: 55 operations per entry against 38;
+            // tools/vor_compact_check.cpp, mode d, checks the resulting steps against the reference's)
             const float nx = en.ox, ny = en.oy, nz = en.oz;
-            const float px = nx * fkx, py = ny * fky, pz = nz * fkz;
-            const float den = px + py + pz;
-            const float eA = kVorEpsF * (fabsf(px) + fabsf(py) + fabsf(pz));
-            const float tx = Dx + 0.5f * nx, ty = Dy + 0.5f * ny, tz = Dz + 0.5f * nz;
-            const float qx = nx * tx, qy = ny * ty, qz = nz * tz;
-            const float num = qx + qy + qz;
-            const float eB = kVorEpsF * (fabsf(qx) + fabsf(qy) + fabsf(qz) + 0.5f * (nx * nx + ny * ny + nz * nz));
+            const float n2 = fmaf(nz, nz, fmaf(ny, ny, nx * nx));
+            const float den = fmaf(nz, fkz, fmaf(ny, fky, nx * fkx));
+            const float num = fmaf(n2, 0.5f, fmaf(nz, Dz, fmaf(ny, Dy, nx * Dx)));
+            const float eA = kVorEpsF * (fabsf(nx) + fabsf(ny) + fabsf(nz));
+            const float eB = fmaf(eA, Dn, kVorEpsF * n2);
             const float inv = __builtin_amdgcn_rcpf(den);
             const float sa = num * inv;
-            const float err = 2.0f * (eB + fabsf(sa) * eA) * inv + fabsf(sa) * kVorEpsF;
+            const float err = fmaf(2.0f * fmaf(fabsf(sa), eA, eB), inv, fabsf(sa) * kVorEpsF);
             // den > 2 eA: the sign of n.k and the interval are certain; den <= -eA: moving away for
             // certain; otherwise (or NaN offsets: a degenerate wall) the sign is uncertain
             const bool sure = den > 2.0f * eA;

@@ -23,10 +23,11 @@ def checker(tmp_path_factory):
     return exe
 
 
-@pytest.mark.parametrize("mode", ["f64", "f32"])
+# the checker's modes: n -- double bounds; f -- the round-2 float bounds; d -- the device's step (per-entry
+# Cauchy-Schwarz bounds, engine.hip Grid<SKIRT_GRID_VORONOI>::step)
+@pytest.mark.parametrize("mode", ["n", "f", "d"], ids=["f64", "f32_r2", "device"])
 def test_compact_voronoi_step_is_exact(checker, mode):
-    r = subprocess.run([checker, "20000", "3000", "f" if mode == "f32" else "d"], capture_output=True, text=True,
-                       timeout=300)
+    r = subprocess.run([checker, "20000", "3000", mode], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "mismatches 0" in r.stdout, r.stdout
     steps = int(r.stdout.split("steps ")[1].split(",")[0])

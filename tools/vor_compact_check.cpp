@@ -5,7 +5,8 @@
 // exact re-evaluation of every possible winner when the bounds cannot separate them), and requires the
 // same cells and bitwise equal segment lengths. Reports how often the exact re-evaluation was needed.
 //   g++ -O2 -std=c++17 -ffp-contract=off -I include tools/vor_compact_check.cpp -L skirt_amd -lskirt_amd \
-//       -Wl,-rpath,$PWD/skirt_amd -o /tmp/vor_compact_check && /tmp/vor_compact_check 100000 20000
+//       -Wl,-rpath,$PWD/skirt_amd -o /tmp/vor_compact_check && /tmp/vor_compact_check 100000 20000 d
+// (mode d: the device's round-3 bounds; f / e / c: round-2 float variants; none: double bounds)
 #include <cfloat>
 #include <cmath>
 #include <cstdint>
@@ -64,7 +65,8 @@ int refStep(const SkirtGridDesc& g, int m, const double r[3], const double k[3],
 // operation adds at most a few 2^-24 of the sum of absolute terms, covered by kEpsF
 constexpr float kEpsF = 1.0f / (1 << 20);
 float gScale = 1.0f;
-bool gCell = false, gEntry = false;  // per-cell / per-entry-norm error bounds instead of the device's
+bool gCell = false, gEntry = false;  // per-cell / per-entry-norm error bounds instead of the round-2 device's
+bool gDevice = false;                // the round-3 device step: per-entry Cauchy-Schwarz error terms
 long gSignFallbacks = 0;  // re-evaluations with an entry whose n.k sign is uncertain
 long gWholeList = 0;      // re-evaluations over the whole list (more than 4 possible winners)
 float gLo[4096];          // the step's lower bounds, per list entry
@@ -142,6 +144,28 @@ static int compactStepF(const Mesh& M, int m, const double r[3], const double k[
     for (int q = g.cell_nbr_offset[m]; q < g.cell_nbr_offset[m + 1]; q++) {
         const int mi = g.cell_nbr_list[q];
         const float nx = M.off[3 * (size_t)q], ny = M.off[3 * (size_t)q + 1], nz = M.off[3 * (size_t)q + 2];
+        if (gDevice) {
+            // Grid<SKIRT_GRID_VORONOI>::step (engine.hip) operation for operation
+            const float Dn = fabsf(Dx) + fabsf(Dy) + fabsf(Dz);
+            const float n2 = fmaf(nz, nz, fmaf(ny, ny, nx * nx));
+            const float den = fmaf(nz, kz, fmaf(ny, ky, nx * kx));
+            const float num = fmaf(n2, 0.5f, fmaf(nz, Dz, fmaf(ny, Dy, nx * Dx)));
+            const float eA = kEpsF * (fabsf(nx) + fabsf(ny) + fabsf(nz));
+            const float eB = fmaf(eA, Dn, kEpsF * n2);
+            const float inv = 1.0f / den;
+            const float sa = num * inv;
+            const float err = fmaf(2.0f * fmaf(fabsf(sa), eA, eB), inv, fabsf(sa) * kEpsF);
+            const bool sure = den > 2.0f * eA;
+            const bool none = den <= -eA || (sure && !(sa + err > 0.f));
+            const float lo = none ? FLT_MAX : sure ? sa - err : -FLT_MAX;
+            const float hi = (none || !sure) ? FLT_MAX : sa + err;
+            gLo[q - g.cell_nbr_offset[m]] = lo;
+            U = fminf(U, lo > 0.f ? hi : FLT_MAX);
+            w1 = lo < L1 ? mi : w1;
+            L2 = fmaxf(fminf(L1, L2), fminf(fmaxf(L1, L2), lo));
+            L1 = fminf(L1, lo);
+            continue;
+        }
         const float ne = sqrtf(nx * nx + ny * ny + nz * nz);
         const float px = nx * kx, py = ny * ky, pz = nz * kz;
         const float den = px + py + pz;
@@ -203,7 +227,8 @@ int main(int argc, char** argv) {
     }
     const double ext[6] = {-L, -L, -L, L, L, L};
     gScale = (float)(1.0 / L);
-    const bool f32 = argc > 3 && (argv[3][0] == 'f' || argv[3][0] == 'c' || argv[3][0] == 'e');
+    const bool f32 = argc > 3 && (argv[3][0] == 'f' || argv[3][0] == 'c' || argv[3][0] == 'e' || argv[3][0] == 'd');
+    gDevice = argc > 3 && argv[3][0] == 'd';
     gCell = argc > 3 && argv[3][0] == 'c';
     gEntry = argc > 3 && argv[3][0] == 'e';
     if (gEntry) gCell = true;
@@ -256,7 +281,8 @@ int main(int argc, char** argv) {
             m = a;
         }
     }
-    printf("%s: sites %d, rays %d, steps %ld, exact re-evaluations %ld (%.3g per step), mismatches %ld\n", gEntry ? "f32 per-entry norm bounds" : gCell ? "f32 per-cell bounds" : f32 ? "f32 bounds" : "f64 bounds", N, R, steps,
+    printf("%s: sites %d, rays %d, steps %ld, exact re-evaluations %ld (%.3g per step), mismatches %ld\n",
+           gDevice ? "f32 device bounds (per-entry Cauchy-Schwarz, round 3)" : gEntry ? "f32 per-entry norm bounds" : gCell ? "f32 per-cell bounds" : f32 ? "f32 bounds" : "f64 bounds", N, R, steps,
            fallbacks, (double)fallbacks / steps, mismatches);
     if (f32) printf("  of which with an uncertain n.k sign: %ld; over the whole list: %ld\n", gSignFallbacks, gWholeList);
     skirt_host_voronoi_free(v);
