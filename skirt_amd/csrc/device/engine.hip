@@ -178,6 +178,15 @@ constexpr int kVorUnroll = SKIRT_VOR_UNROLL;
 #define SKIRT_VOR_FALLBACK_GROUP 2  // neighbour sites loaded together by the exact re-evaluation (<= kVorUnroll)
 #endif
 constexpr int kVorCand = 4;  // possible winners the exact re-evaluation collects before it takes the whole list
+#ifndef SKIRT_VOR_WIDE
+// live rays at most for the neighbour-parallel drain step; 0 (off) is the default, as measured on C4:
+// lane-serial 6.69e7 pkt/s against 6.63e7 (16), 6.64e7 (8), 6.62e7 (4) (profiles/r03_vor_wide.txt)
+#define SKIRT_VOR_WIDE 0
+#endif
+constexpr int kVorWideMax = SKIRT_VOR_WIDE;
+// slots after the last cell's block: a step loads whole groups of entries (kVorUnroll lane-serial, 16
+// for the first round of a neighbour-parallel step)
+constexpr int kVorPad = kVorUnroll > 16 ? kVorUnroll : 16;
 
 // grid kinds of the kernels: SKIRT_GRID_CARTESIAN, SKIRT_GRID_OCTREE (leaf-map walk), the k-d tree
 // through its leaf map, and any tree walked through the node arrays (trees deeper than the leaf maps
@@ -1070,115 +1079,123 @@ struct Grid<SKIRT_GRID_VORONOI> {
         x = h0.x; y = h0.y; z = h1.x;
     }
 
-    // One step (VoronoiMesh::path, VoronoiMesh.cpp:749-844). r.cj: the block of the cell the ray is in.
-    // r.ck = 1: the previous cell's segment (cell r.ci, density r.rho0, site r.bx0..bz0) is still to be
-    // added; it ends on the bisector plane with this cell, whose exact site arrives with this step's load.
-    // A step therefore issues one round of loads (this cell's header and first entries) in the common case.
-    // It adds at most two segments (the pending one, and one more when the bounds leave several possible
-    // winners), see kSegsPerStep.
-    template <class SegFn>
-    __device__ static __forceinline__ bool step(const Args& a, const Shared&, Ray& r, SegFn seg) {
-        const VorEntry* B = a.vorSlots + r.cj;
-        const double2 h0 = *reinterpret_cast<const double2*>(B);
-        const double2 h1 = *reinterpret_cast<const double2*>(B + 1);
-        const int4 h2 = *reinterpret_cast<const int4*>(B + 2);
-        VorEntry e[kVorUnroll];
-#pragma unroll
-        for (int u = 0; u < kVorUnroll; u++) e[u] = B[kVorHead + u];
-        const double pwx = h0.x, pwy = h0.y, pwz = h1.x, rhow = h1.y;
-        const int idw = h2.x, cnt = h2.y;
+    // the operands of a step: the cell's header (exact site, density, id, neighbour count) and, for the
+    // bounds, the float offset D of the site from the ray's position and the direction in float
+    struct StepIn {
+        const VorEntry* B;
+        double pwx, pwy, pwz, rhow;
+        int idw, cnt;
+        float Dx, Dy, Dz, Dn, fkx, fky, fkz;
+    };
+    // U: the least upper bound of the certain exits; L1 <= L2: the two least lower bounds of the possible
+    // exits, w1: the first one's `next`
+    struct Best {
+        float U, L1, L2;
+        int w1;
+    };
 
+    // the bounds [lo, hi] of one neighbour's plane distance, in single precision on coordinates scaled by
+    // a.vorScale (the entries' offsets are stored scaled): each float operation adds a few 2^-24 of the sum
+    // of absolute terms, which kVorEpsF covers with margin; an approximate reciprocal (1 ulp) is covered by
+    // the |s| term. Walls are stored as the bisector plane with the site's mirror image (the same plane),
+    // so every entry takes the same branch-free arithmetic; lo = hi = FLT_MAX: certainly no exit.
+    __device__ static __forceinline__ void bounds(const StepIn& s, const VorEntry& en, bool valid, float& lo,
+                                                  float& hi) {
+        // the plane distance s = (n.D + |n|^2/2) / (n.k) with per-entry Cauchy-Schwarz error terms:
+        // |d(n.k)| <= eA = kVorEpsF |n|_1 and |d(n.D + |n|^2/2)| <= eA |D|_1 + kVorEpsF |n|^2, several
+        // times the float roundings of the offsets, D, k and the fused operations (round 2 summed the
+        // absolute terms of each product instead: 55 operations per entry against 38;
+        // tools/vor_compact_check.cpp, mode d, checks the resulting steps against the reference's)
+        const float nx = en.ox, ny = en.oy, nz = en.oz;
+        const float n2 = fmaf(nz, nz, fmaf(ny, ny, nx * nx));
+        const float den = fmaf(nz, s.fkz, fmaf(ny, s.fky, nx * s.fkx));
+        const float num = fmaf(n2, 0.5f, fmaf(nz, s.Dz, fmaf(ny, s.Dy, nx * s.Dx)));
+        const float eA = kVorEpsF * (fabsf(nx) + fabsf(ny) + fabsf(nz));
+        const float eB = fmaf(eA, s.Dn, kVorEpsF * n2);
+        const float inv = __builtin_amdgcn_rcpf(den);
+        const float sa = num * inv;
+        const float err = fmaf(2.0f * fmaf(fabsf(sa), eA, eB), inv, fabsf(sa) * kVorEpsF);
+        // den > 2 eA: the sign of n.k and the interval are certain; den <= -eA: moving away for
+        // certain; otherwise (or NaN offsets: a degenerate wall) the sign is uncertain
+        const bool sure = den > 2.0f * eA;
+        const bool none = !valid || den <= -eA || (sure && !(sa + err > 0.f));
+        lo = none ? FLT_MAX : sure ? sa - err : -FLT_MAX;
+        hi = (none || !sure) ? FLT_MAX : sa + err;
+    }
+
+    // one entry's bounds into the running Best, in list order
+    __device__ static __forceinline__ void take(Best& b, float lo, float hi, int next) {
+        b.U = fminf(b.U, lo > 0.f ? hi : FLT_MAX);
+        b.w1 = lo < b.L1 ? next : b.w1;
+        b.L2 = __builtin_amdgcn_fmed3f(b.L1, b.L2, lo);
+        b.L1 = fminf(b.L1, lo);
+    }
+
+    // The start of a step: the cell's header (with the first entries, loaded by the caller in the same
+    // round), the pending segment (r.ck = 1: the previous cell's segment, cell r.ci, density r.rho0, site
+    // r.bx0..bz0, ends on the bisector plane with this cell, whose exact site arrives with this load),
+    // and the bounds' operands. False: the ray ended.
+    template <class SegFn>
+    __device__ static __forceinline__ bool head(const Args& a, Ray& r, StepIn& s, SegFn seg) {
+        const double2 h0 = *reinterpret_cast<const double2*>(s.B);
+        const double2 h1 = *reinterpret_cast<const double2*>(s.B + 1);
+        const int4 h2 = *reinterpret_cast<const int4*>(s.B + 2);
+        s.pwx = h0.x; s.pwy = h0.y; s.pwz = h1.x; s.rhow = h1.y;
+        s.idw = h2.x; s.cnt = h2.y;
         if (r.ck) {
-            const double sq = planeDist(r, r.bx0, r.by0, r.bz0, pwx, pwy, pwz);
+            const double sq = planeDist(r, r.bx0, r.by0, r.bz0, s.pwx, s.pwy, s.pwz);
             if (!seg(r.ci, r.rho0, sq)) return false;
             r.x += (sq + a.eps) * r.dx; r.y += (sq + a.eps) * r.dy; r.z += (sq + a.eps) * r.dz;
             r.ck = 0;
         }
-        const double kx = r.dx, ky = r.dy, kz = r.dz;
-        // the bounds in single precision, on coordinates scaled by a.vorScale (the entries' offsets are
-        // stored scaled): each float operation adds a few 2^-24 of the sum of absolute terms, which
-        // kVorEpsF covers with margin; an approximate reciprocal (1 ulp) is covered by the |s| term
         const float sc = a.vorScale;
-        const float Dx = (float)((pwx - r.x) * sc), Dy = (float)((pwy - r.y) * sc), Dz = (float)((pwz - r.z) * sc);
-        const float Dn = fabsf(Dx) + fabsf(Dy) + fabsf(Dz);  // >= |D|
-        const float fkx = (float)kx, fky = (float)ky, fkz = (float)kz;
-        // bounds [lo, hi] of every neighbour's plane distance; U: the least upper bound of the certain
-        // exits; L1 <= L2: the two least lower bounds of the possible exits, w1: the first one's `next`.
-        // Walls are stored as the bisector plane with the site's mirror image (the same plane), so every
-        // entry takes the same branch-free arithmetic; lo = hi = FLT_MAX: certainly no exit.
-        float U = FLT_MAX, L1 = FLT_MAX, L2 = FLT_MAX;
-        int w1 = 0;
-        auto bounds = [&](const VorEntry& en, bool valid, float& lo, float& hi) {
-            // the plane distance s = (n.D + |n|^2/2) / (n.k) with per-entry Cauchy-Schwarz error terms:
-            // |d(n.k)| <= eA = kVorEpsF |n|_1 and |d(n.D + |n|^2/2)| <= eA |D|_1 + kVorEpsF |n|^2, several
-            // times the float roundings of the offsets, D, k and the fused operations (round 2 summed the
-            // absolute terms of each product instead: 55 operations per entry against 38;
-            // tools/vor_compact_check.cpp, mode d, checks the resulting steps against the reference's)
-            const float nx = en.ox, ny = en.oy, nz = en.oz;
-            const float n2 = fmaf(nz, nz, fmaf(ny, ny, nx * nx));
-            const float den = fmaf(nz, fkz, fmaf(ny, fky, nx * fkx));
-            const float num = fmaf(n2, 0.5f, fmaf(nz, Dz, fmaf(ny, Dy, nx * Dx)));
-            const float eA = kVorEpsF * (fabsf(nx) + fabsf(ny) + fabsf(nz));
-            const float eB = fmaf(eA, Dn, kVorEpsF * n2);
-            const float inv = __builtin_amdgcn_rcpf(den);
-            const float sa = num * inv;
-            const float err = fmaf(2.0f * fmaf(fabsf(sa), eA, eB), inv, fabsf(sa) * kVorEpsF);
-            // den > 2 eA: the sign of n.k and the interval are certain; den <= -eA: moving away for
-            // certain; otherwise (or NaN offsets: a degenerate wall) the sign is uncertain
-            const bool sure = den > 2.0f * eA;
-            const bool none = !valid || den <= -eA || (sure && !(sa + err > 0.f));
-            lo = none ? FLT_MAX : sure ? sa - err : -FLT_MAX;
-            hi = (none || !sure) ? FLT_MAX : sa + err;
-        };
-        auto entry = [&](const VorEntry& en, bool valid) {
-            float lo, hi;
-            bounds(en, valid, lo, hi);
-            U = fminf(U, lo > 0.f ? hi : FLT_MAX);
-            w1 = lo < L1 ? en.next : w1;
-            L2 = __builtin_amdgcn_fmed3f(L1, L2, lo);
-            L1 = fminf(L1, lo);
-        };
-        for (int q0 = 0; q0 < cnt; q0 += kVorUnroll) {
-            if (q0) {
-#pragma unroll
-                for (int u = 0; u < kVorUnroll; u++) e[u] = B[kVorHead + q0 + u];
-            }
-#pragma unroll
-            for (int u = 0; u < kVorUnroll; u++) entry(e[u], q0 + u < cnt);
-        }
-        if (L1 != FLT_MAX && L2 > U) {
-            if (w1 >= 0) {  // the exit: its exact distance when the next cell's header arrives
+        s.Dx = (float)((s.pwx - r.x) * sc); s.Dy = (float)((s.pwy - r.y) * sc); s.Dz = (float)((s.pwz - r.z) * sc);
+        s.Dn = fabsf(s.Dx) + fabsf(s.Dy) + fabsf(s.Dz);  // >= |D|
+        s.fkx = (float)r.dx; s.fky = (float)r.dy; s.fkz = (float)r.dz;
+        return true;
+    }
+
+    // The end of a step, from the bounds over all entries: a single certain exit is taken (its exact
+    // distance follows from the next cell's header, r.ck = 1); otherwise the reference's rule, exactly,
+    // over the possible winners.
+    template <class SegFn>
+    __device__ static __forceinline__ bool decide(const Args& a, Ray& r, const StepIn& s, const Best& b, SegFn seg) {
+        const VorEntry* B = s.B;
+        const int cnt = s.cnt;
+        if (b.L1 != FLT_MAX && b.L2 > b.U) {
+            if (b.w1 >= 0) {  // the exit: its exact distance when the next cell's header arrives
                 r.ck = 1;
-                r.ci = idw; r.rho0 = rhow;
-                r.bx0 = pwx; r.by0 = pwy; r.bz0 = pwz;
-                r.cj = w1;
+                r.ci = s.idw; r.rho0 = s.rhow;
+                r.bx0 = s.pwx; r.by0 = s.pwy; r.bz0 = s.pwz;
+                r.cj = b.w1;
                 return true;
             }
-            seg(idw, rhow, wallDist(a, r, w1));  // leaves the grid through a wall
+            seg(s.idw, s.rhow, wallDist(a, r, b.w1));  // leaves the grid through a wall
             return false;
         }
-        // no exit, or several possible exits: the reference's rule, exactly, over the possible winners.
-        // An entry whose lower bound exceeds U lies beyond a certain exit, so it can neither win nor tie;
-        // a second pass over the (cached) entries collects the others in list order (the first of equal
-        // distances wins) and their sites arrive in one round trip. More than kVorCand of them: the whole
-        // list, in groups.
+        // no exit, or several possible exits. An entry whose lower bound exceeds U lies beyond a certain
+        // exit, so it can neither win nor tie; a second pass over the (cached) entries collects the others
+        // in list order (the first of equal distances wins) and their sites arrive in one round trip. More
+        // than kVorCand of them: the whole list, in groups.
+        const double kx = r.dx, ky = r.dy, kz = r.dz;
         constexpr int NO_INDEX = (int)0x80000000u;
         double sq = kDblMax;
         int mq = NO_INDEX;
         auto consider = [&](int nxt, double pix, double piy, double piz) {
-            const double si = nxt < 0 ? wallDist(a, r, nxt) : planeDist(r, pwx, pwy, pwz, pix, piy, piz);
+            const double si = nxt < 0 ? wallDist(a, r, nxt) : planeDist(r, s.pwx, s.pwy, s.pwz, pix, piy, piz);
             if (si > 0 && si < sq) { sq = si; mq = nxt; }
         };
-        if (L1 != FLT_MAX) {
+        if (b.L1 != FLT_MAX) {
             int c0 = 0, c1 = 0, c2 = 0, c3 = 0, nc = 0;
+            VorEntry e[kVorUnroll];
             for (int q0 = 0; q0 < cnt; q0 += kVorUnroll) {
 #pragma unroll
                 for (int u = 0; u < kVorUnroll; u++) e[u] = B[kVorHead + q0 + u];
 #pragma unroll
                 for (int u = 0; u < kVorUnroll; u++) {
                     float lo, hi;
-                    bounds(e[u], q0 + u < cnt, lo, hi);
-                    if (lo < FLT_MAX && lo <= U) {
+                    bounds(s, e[u], q0 + u < cnt, lo, hi);
+                    if (lo < FLT_MAX && lo <= b.U) {
                         const int nx = e[u].next;
                         c0 = nc == 0 ? nx : c0; c1 = nc == 1 ? nx : c1; c2 = nc == 2 ? nx : c2; c3 = nc == 3 ? nx : c3;
                         nc++;
@@ -1222,10 +1239,100 @@ struct Grid<SKIRT_GRID_VORONOI> {
             r.cj = a.vorStart[m];
             return true;
         }
-        if (!seg(idw, rhow, sq)) return false;
+        if (!seg(s.idw, s.rhow, sq)) return false;
         r.x += (sq + a.eps) * kx; r.y += (sq + a.eps) * ky; r.z += (sq + a.eps) * kz;
         r.cj = mq;
         return mq >= 0;
+    }
+
+    // One step (VoronoiMesh::path, VoronoiMesh.cpp:749-844), lane-serial over the cell's entries. r.cj:
+    // the block of the cell the ray is in. A step issues one round of loads (this cell's header and first
+    // entries) in the common case. It adds at most two segments (the pending one, and one more when the
+    // bounds leave several possible winners), see kSegsPerStep.
+    template <class SegFn>
+    __device__ static __forceinline__ bool step(const Args& a, const Shared&, Ray& r, SegFn seg) {
+        StepIn s;
+        s.B = a.vorSlots + r.cj;
+        VorEntry e[kVorUnroll];
+#pragma unroll
+        for (int u = 0; u < kVorUnroll; u++) e[u] = s.B[kVorHead + u];
+        if (!head(a, r, s, seg)) return false;
+        Best b{FLT_MAX, FLT_MAX, FLT_MAX, 0};
+        for (int q0 = 0; q0 < s.cnt; q0 += kVorUnroll) {
+            if (q0) {
+#pragma unroll
+                for (int u = 0; u < kVorUnroll; u++) e[u] = s.B[kVorHead + q0 + u];
+            }
+#pragma unroll
+            for (int u = 0; u < kVorUnroll; u++) {
+                float lo, hi;
+                bounds(s, e[u], q0 + u < s.cnt, lo, hi);
+                take(b, lo, hi, e[u].next);
+            }
+        }
+        return decide(a, r, s, b, seg);
+    }
+
+    // The same step, neighbour-parallel, for a wave with at most kVorWideMax live rays (the drain of a
+    // launch, after the queue ran out; called by every lane of the wave, live = the lanes with a ray).
+    // The wave's groups of G lanes each take one live ray: a lane bounds the entries j, j + G, ... of that
+    // ray's cell and the group reduces the bounds (U, L1, L2 are order-free; w1 is used only when L1 is
+    // unique), so the ray's lane decides exactly as step() does. A lane-serial step runs its entries in
+    // rounds of kVorUnroll loads, each a round trip, which the drain waits on with few rays in flight.
+    template <class SegFn>
+    __device__ static __forceinline__ bool stepWide(const Args& a, Ray& r, unsigned long long live, SegFn seg) {
+        const int lane = threadIdx.x & 63;
+        const bool mine = (live >> lane) & 1ull;
+        const int k = __popcll(live);
+        const int lg = k <= 4 ? 4 : k <= 8 ? 3 : 2;  // log2 of the lanes per ray
+        const int G = 1 << lg;
+        const int g = lane >> lg, j = lane & (G - 1);
+        const bool grp = g < k;
+        int owner = 0;  // the lane of the g-th live ray
+        {
+            unsigned long long m = live;
+#pragma unroll
+            for (int t = 0; t < kVorWideMax; t++) {
+                owner = t == g ? __ffsll((long long)m) - 1 : owner;
+                m &= m - 1ull;
+            }
+        }
+        const int cj = __shfl(r.cj, owner);
+        const VorEntry* Bg = a.vorSlots + cj;
+        VorEntry e{0.f, 0.f, 0.f, -1};
+        if (grp) e = Bg[kVorHead + j];  // with the header, one round (the array is padded by kVorPad slots)
+        StepIn s{};
+        s.B = a.vorSlots + r.cj;
+        bool alive = false;
+        if (mine) alive = head(a, r, s, seg);
+        if (!alive) s.cnt = 0;  // the group of a ray that ended evaluates nothing (a count, not a shuffled bool:
+                                // the lane mask of a divergently assigned bool lost its upper 32 lanes there)
+        StepIn sg{};
+        sg.Dx = __shfl(s.Dx, owner); sg.Dy = __shfl(s.Dy, owner); sg.Dz = __shfl(s.Dz, owner);
+        sg.Dn = __shfl(s.Dn, owner);
+        sg.fkx = __shfl(s.fkx, owner); sg.fky = __shfl(s.fky, owner); sg.fkz = __shfl(s.fkz, owner);
+        const int cnt = __shfl(s.cnt, owner);
+        const bool act = grp && cnt > 0;
+        Best b{FLT_MAX, FLT_MAX, FLT_MAX, 0};
+        for (int q0 = 0; __ballot(act && q0 < cnt); q0 += G) {
+            const bool valid = act && q0 + j < cnt;
+            if (q0 && valid) e = Bg[kVorHead + q0 + j];
+            float lo, hi;
+            bounds(sg, e, valid, lo, hi);
+            take(b, lo, hi, e.next);
+        }
+        for (int o = 1; o < G; o <<= 1) {
+            const float U2 = __shfl_xor(b.U, o), L12 = __shfl_xor(b.L1, o), L22 = __shfl_xor(b.L2, o);
+            const int w2 = __shfl_xor(b.w1, o);
+            b.U = fminf(b.U, U2);
+            b.w1 = L12 < b.L1 ? w2 : b.w1;
+            b.L2 = fminf(fmaxf(b.L1, L12), fminf(b.L2, L22));  // the second least of the two pairs
+            b.L1 = fminf(b.L1, L12);
+        }
+        const int src = (mine ? __popcll(live & ((1ull << lane) - 1ull)) : 0) << lg;  // a lane of the ray's group
+        const Best mb{__shfl(b.U, src), __shfl(b.L1, src), __shfl(b.L2, src), __shfl(b.w1, src)};
+        if (!alive) return false;
+        return decide(a, r, s, mb, seg);
     }
 
     __device__ static __forceinline__ int whichcell(const Args& a, const Shared&, double x, double y, double z) {
@@ -1790,14 +1897,28 @@ __device__ __forceinline__ void traceBody(const Args& a) {
             if (!tlExhausted && __ballot(idle && id >= nrays)) tlExhausted = __builtin_amdgcn_s_memrealtime();
 #endif
         }
+        // the queue ran out for this wave: the Voronoi step goes neighbour-parallel when few rays remain
+        const bool draining = GRID == SKIRT_GRID_VORONOI && kVorWideMax > 0 && __ballot(done) != 0;
 #pragma unroll 1
         for (int it = 0; it < kStepsPerPull; it++) {
-            if (__ballot(r.mode != RAY_NONE) == 0) break;
+            const unsigned long long live = __ballot(r.mode != RAY_NONE);
+            if (live == 0) break;
 #ifndef SKIRT_EXPERIMENT_LINE_COUNT
             T.laneSlots += 64;
 #endif
+            auto seg = [&](int m, double rho0, double ds) { return T.segment(r, m, rho0, ds); };
+            if constexpr (GRID == SKIRT_GRID_VORONOI && kVorWideMax > 0) {
+                if (draining && __popcll(live) <= kVorWideMax) {
+                    if (!Grid<GRID>::stepWide(a, r, live, seg) && r.mode != RAY_NONE) {
+                        T.finish(r);
+                        r.mode = RAY_NONE;
+                    }
+                    if (__ballot(T.npend > kLabsBuf - kSegsPerStep<GRID>)) T.drain();
+                    continue;
+                }
+            }
             if (r.mode != RAY_NONE) {
-                if (!Grid<GRID>::step(a, sh, r, [&](int m, double rho0, double ds) { return T.segment(r, m, rho0, ds); })) {
+                if (!Grid<GRID>::step(a, sh, r, seg)) {
                     T.finish(r);
                     r.mode = RAY_NONE;
                 }
@@ -3345,7 +3466,7 @@ int skirt_mcrt_upload_grid(SkirtMcrt* c, const SkirtGridDesc* g) {
         for (int m = 0; m < N; m++) refOf[c->devCell[m]] = m;
         std::vector<double> site(3 * (size_t)N), bbox(6 * (size_t)N);
         // each device cell's block: kVorHead header slots + one slot per neighbour (see VorEntry); the
-        // array is padded by kVorUnroll slots, since a step loads whole groups of entries
+        // array is padded by kVorPad slots, since a step loads whole groups of entries
         std::vector<int> start(N + 1, 0);
         for (int d = 0; d < N; d++) {
             const int m = refOf[d];
@@ -3353,8 +3474,8 @@ int skirt_mcrt_upload_grid(SkirtMcrt* c, const SkirtGridDesc* g) {
             if (cnt < 1) return fail(c, SKIRT_ERR_ARG, "Voronoi cell without neighbours");
             start[d + 1] = start[d] + kVorHead + cnt;
         }
-        if ((size_t)start[N] + kVorUnroll >= (size_t)INT32_MAX) return fail(c, SKIRT_ERR_UNSUPPORTED, "Voronoi mesh too large");
-        std::vector<VorEntry> slots((size_t)start[N] + kVorUnroll, VorEntry{0.f, 0.f, 0.f, -1});
+        if ((size_t)start[N] + kVorPad >= (size_t)INT32_MAX) return fail(c, SKIRT_ERR_UNSUPPORTED, "Voronoi mesh too large");
+        std::vector<VorEntry> slots((size_t)start[N] + kVorPad, VorEntry{0.f, 0.f, 0.f, -1});
         // offsets in units of the domain's largest half-width: single-precision squares stay in range
         c->vorScale = 2.0 / std::max({c->gx1 - c->gx0, c->gy1 - c->gy0, c->gz1 - c->gz0});
         for (int d = 0; d < N; d++) {
