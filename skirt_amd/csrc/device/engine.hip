@@ -2535,16 +2535,27 @@ __global__ void __launch_bounds__(kBlock) SKIRT_EVENT_ATTR eventKernel(const Arg
     const unsigned int stride = gridDim.x * blockDim.x;
     // every lane of a wave runs the same number of rounds (wave-collective claims and appends below)
     const unsigned int rounds = (nwork + stride - 1) / stride;
+    // the active-list entry of the lane's next round is loaded a round ahead, so a round's first round trip
+    // is its slot's state (and the trace result, loaded with it)
+    const unsigned int w0 = blockIdx.x * blockDim.x + threadIdx.x;
+    int slotNext = (w0 < nwork) ? (a.init ? (int)w0 : actIn[w0]) : 0;
     for (unsigned int round = 0; round < rounds; round++) {
-        const unsigned int w = round * stride + blockIdx.x * blockDim.x + threadIdx.x;
+        const unsigned int w = round * stride + w0;
         const bool valid = w < nwork;
 #ifdef SKIRT_EXPERIMENT_TIMELINE
         unsigned long long ts0 = stamp();
 #endif
-        const int slot = valid ? (a.init ? (int)w : actIn[w]) : 0;
+        const int slot = slotNext;
+        const unsigned int wn = w + stride;
+        if (round + 1 < rounds) slotNext = (wn < nwork) ? (a.init ? (int)wn : actIn[wn]) : 0;
         Packet p;
         p.state = S_NEW;
-        if (valid && !a.init) E.load(slot, p);
+        double resA = 0.0, resB = 0.0;
+        if (valid && !a.init) {
+            E.load(slot, p);
+            resA = a.resA[slot];
+            if (!ONECOMP) resB = a.resB[slot];
+        }
         int peel = PEEL_NONE;
         unsigned mainMode = RAY_NONE;
         double mainParam = 0;
@@ -2552,13 +2563,13 @@ __global__ void __launch_bounds__(kBlock) SKIRT_EVENT_ATTR eventKernel(const Arg
         if (valid && !a.init) {
             if (p.state == S_FILL) {
                 // end of fillOpticalDepth + simulateescapeandabsorption; termination; simulatepropagation
-                const double taupath = a.resA[slot];
+                const double taupath = resA;
                 if (taupath < 0.0 || isnan(taupath) || isinf(taupath)) {
                     atomicOr(a.error, ERR_TAU);
                     p.state = S_NEW;
                 } else {
                     if (ONECOMP) p.L = p.L * sh.alb[p.ell] * (-expm1(-taupath));
-                    else p.L = a.resB[slot];
+                    else p.L = resB;
                     if (p.L <= 0 || (p.L <= p.Lth && p.nscatt >= a.minScatt)) {
                         p.state = S_NEW;
                     } else {
@@ -2566,13 +2577,13 @@ __global__ void __launch_bounds__(kBlock) SKIRT_EVENT_ATTR eventKernel(const Arg
                         double tauint = 0.0;  // taupath == 0: no propagation (MonteCarloSimulation.cpp:522)
                         if (taupath != 0.0) tauint = E.sampleTau(p, taupath);
                         if (tauint > 0) { mainMode = RAY_WALK; mainParam = tauint; }
-                        else a.resA[slot] = 0.0;
+                        else resA = 0.0;  // no walk: the interaction point is where the packet is
                     }
                 }
             }
             if (p.state == S_WALK && mainMode == RAY_NONE) {
                 // propagate to the interaction point; peel-off round; scatter; next FILL
-                const double s = a.resA[slot];
+                const double s = resA;
                 p.rx = p.rx + s * p.kx;
                 p.ry = p.ry + s * p.ky;
                 p.rz = p.rz + s * p.kz;

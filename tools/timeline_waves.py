@@ -57,6 +57,7 @@ def main(path):
         names = ("loads+FILL/WALK events", "claims+launches", "block reservations", "ray/state writes")
         tot = parts.sum()
         print("event kernel round parts: " + ", ".join("%s %.1f%%" % (nm, 100 * v / tot) for nm, v in zip(names, parts)))
+        print("event kernel round parts, wave-cycles x1e9: " + ", ".join("%s %.2f" % (nm, v / 1e9) for nm, v in zip(names, parts)))
     a = np.array([(r[1], r[2], r[3], r[4], r[6], r[7]) for r in rows])
     print("sum: event %.1f ms, gaps %.1f ms, trace %.1f ms (tail %.1f ms), detect %.1f ms" % (
         a[:, 0].sum() / 1e3, (a[:, 1].sum() + a[:, 4].sum()) / 1e3, a[:, 2].sum() / 1e3, a[:, 3].sum() / 1e3,
