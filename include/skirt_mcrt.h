@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define SKIRT_MCRT_ABI_VERSION 9
+#define SKIRT_MCRT_ABI_VERSION 10
 
 enum {
     SKIRT_OK = 0,
@@ -295,6 +295,11 @@ int skirt_mcrt_stats(SkirtMcrt* ctx, SkirtStats* out);
 int skirt_mcrt_set_crossed(SkirtMcrt* ctx, int bins);
 /* the histogram summed over the device copies: hist[b] for b < bins (waits for the engine's stream) */
 int skirt_mcrt_download_crossed(SkirtMcrt* ctx, uint64_t* hist, int bins);
+
+/* DustSystem::writeconvergence (DustSystem.cpp:195-250): the column density of the uploaded grid along n
+ * rays (rays[6 i .. 6 i + 5] = origin, direction), summed as DustGridPath::opticalDepth with the cell
+ * densities of all components, over the photon paths' walk; out[i] in kg/m2. Blocks until done. */
+int skirt_mcrt_column_densities(SkirtMcrt* ctx, const double* rays, int n, double* out);
 /* engine knobs (0 = default): packet slots in flight, trace-kernel workgroups, and the number of idle
  * lanes at which a trace wave pulls new rays (1..64) */
 int skirt_mcrt_configure(SkirtMcrt* ctx, int slots, int grid, int pull_threshold);

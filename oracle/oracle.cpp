@@ -1098,6 +1098,31 @@ OracleRun* oracle_run_shard(const char* ski, const char* datadir, int rngKind, i
             const std::vector<double>* dust = run->tal.labsDust.empty() ? nullptr : &run->tal.labsDust;
             writeOutputs(M, outprefix, run->tal.frames, run->tal.seds, totalLabs(M, run->tal.labs, dust));
             if (M.hasDust && M.writeCellsCrossed) writeCellsCrossed(M, outprefix, run->tal.crossed);
+            if (M.hasDust && M.writeConvergence) {
+                // DustSystem::writeconvergence (DustSystem.cpp:195-242): the paths from the origin along the
+                // six half axes, DustGridPath::opticalDepth of DustSystem::density (DustSystem.cpp:925-931)
+                const int Ncomp = (int)M.dust.size();
+                auto density = [&](int m) {
+                    double rho = 0;
+                    if (m >= 0)
+                        for (int h = 0; h < Ncomp; h++) rho += M.rho[(size_t)m * Ncomp + h];
+                    return rho;
+                };
+                double sigma[3];
+                Path p;
+                for (int ax = 0; ax < 3; ax++) {
+                    sigma[ax] = 0;
+                    for (int sgn = 1; sgn >= -1; sgn -= 2) {
+                        Vec3 k{0, 0, 0};
+                        (ax == 0 ? k.x : ax == 1 ? k.y : k.z) = sgn;
+                        sim.path(Vec3{0, 0, 0}, k, p);
+                        double tau = 0;
+                        for (auto& sg : p.v) tau += density(sg.m) * sg.ds;
+                        sigma[ax] += tau;
+                    }
+                }
+                writeConvergence(M, outprefix, sigma);
+            }
         }
         return run.release();
     } catch (std::exception& ex) {

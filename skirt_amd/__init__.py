@@ -68,7 +68,7 @@ ABI_SYMBOLS = [
     "skirt_sim_run_stellar_shard", "skirt_sim_run_dust_shard", "skirt_sim_set_photon_seed",
     "skirt_host_voronoi_build", "skirt_host_voronoi_describe", "skirt_host_voronoi_free",
     "skirt_sim_load_ex", "skirt_mcrt_sample_density", "skirt_sim_density",
-    "skirt_mcrt_set_crossed", "skirt_mcrt_download_crossed",
+    "skirt_mcrt_set_crossed", "skirt_mcrt_download_crossed", "skirt_mcrt_column_densities",
 ]
 
 _lib = None
@@ -131,6 +131,8 @@ def lib():
         L.skirt_mcrt_configure.argtypes = [vp, c_int, c_int, c_int]
         L.skirt_mcrt_set_crossed.argtypes = [vp, c_int]
         L.skirt_mcrt_download_crossed.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64), c_int]
+        L.skirt_mcrt_column_densities.argtypes = [vp, ctypes.POINTER(ctypes.c_double), c_int,
+                                                  ctypes.POINTER(ctypes.c_double)]
         _lib = L
     return _lib
 
@@ -262,6 +264,16 @@ class Simulation:
         self._check_engine(lib().skirt_mcrt_download_crossed(self.engine, h.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)),
                                                              int(bins)))
         return h
+
+    def column_densities(self, rays):
+        """Column densities (kg/m2) of the grid along rays (n x 6: origin, direction), over the photon
+        paths' walk (DustSystem::writeconvergence's DustGridPath::opticalDepth with the cell densities)."""
+        r = np.ascontiguousarray(rays, dtype=np.float64).reshape(-1, 6)
+        out = np.zeros(len(r))
+        dp = ctypes.POINTER(ctypes.c_double)
+        self._check_engine(lib().skirt_mcrt_column_densities(self.engine, r.ctypes.data_as(dp), len(r),
+                                                             out.ctypes.data_as(dp)))
+        return out
 
     def stats(self):
         s = SkirtStats()

@@ -1615,6 +1615,36 @@ __device__ __forceinline__ void detectPeel(const Args& a, const DevInstr& ins, u
     }
 }
 
+// DustSystem::writeconvergence (DustSystem.cpp:195-250): the column density of the grid along a ray, as
+// DustGridPath::opticalDepth (DustGridPath.hpp:97-108) sums it with DustSystem::density (the cell's
+// densities summed over the components, DustSystem.cpp:925-931), over the same walk as the photon paths.
+// One lane per ray; rays[6 i .. 6 i + 5] = origin, direction.
+template <int GRID>
+__global__ void __launch_bounds__(kBlock) columnKernel(const Args a, const double* rays, int n, double* out) {
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    Shared sh = stageTables(a, lds, gridParts<GRID>());
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    Ray r{};
+    r.x = rays[6 * i]; r.y = rays[6 * i + 1]; r.z = rays[6 * i + 2];
+    r.dx = rays[6 * i + 3]; r.dy = rays[6 * i + 4]; r.dz = rays[6 * i + 5];
+    r.ix = (fabs(r.dx) > 1e-15) ? 1.0 / r.dx : 0.0;
+    r.iy = (fabs(r.dy) > 1e-15) ? 1.0 / r.dy : 0.0;
+    r.iz = (fabs(r.dz) > 1e-15) ? 1.0 / r.dz : 0.0;
+    double tau = 0;
+    auto seg = [&](int m, double, double ds) {
+        if (ds > 0 && m >= 0) {  // (addSegment skips ds <= 0; a segment outside the grid adds 0 x ds)
+            double rho = 0;
+            for (int h = 0; h < a.ncomp; h++) rho += a.rho[(size_t)m * a.ncomp + h];
+            tau += rho * ds;
+        }
+        return true;
+    };
+    if (Grid<GRID>::begin(a, sh, r, seg))
+        while (Grid<GRID>::step(a, sh, r, seg)) {}
+    out[i] = tau;
+}
+
 // ================================================================== dust emission sources on the device
 // The grey-body emission spectrum of every cell and the per-wavelength cell distribution of the dust
 // phases (DustLib::calculate with AllCellsDustLib + GreyBodyDustEmissivity, DustLib.cpp:60-185,
@@ -3120,6 +3150,25 @@ int planLeafMap(SkirtMcrt* c, const SkirtGridDesc* g) {
     return SKIRT_OK;
 }
 
+// the grid and density fields of the kernel arguments (every kernel that walks the grid)
+void gridArgs(const SkirtMcrt* c, Args& a) {
+    a.ncells = c->ncells;
+    a.labsStride = c->labsStride;
+    a.nx = c->nx; a.ny = c->ny; a.nz = c->nz;
+    a.brick = c->brick ? 1 : 0;
+    a.mesh = c->dMesh;
+    a.gx0 = c->gx0; a.gx1 = c->gx1; a.gy0 = c->gy0; a.gy1 = c->gy1; a.gz0 = c->gz0; a.gz1 = c->gz1;
+    a.box = c->dBox; a.firstChild = c->dFirstChild; a.cellnumber = c->dCellnumber;
+    a.splitDir = c->binTree ? c->dSplitDir : nullptr;
+    a.father = c->dFather;
+    a.nbrOffset = c->dNbrOffset; a.nbrList = c->dNbrList; a.eps = c->eps; a.search = c->search;
+    a.site = c->dSite; a.vorStart = c->dVorStart; a.vorSlots = c->dVorSlots; a.vorScale = (float)c->vorScale; a.cellBbox = c->dCellBbox;
+    a.devCell = c->dDevCell;
+    a.vnb = c->vnb; a.blockOffset = c->dBlockOffset; a.blockList = c->dBlockList;
+    a.ncomp = std::max(1, c->ncomp); a.nlambda = c->nlambda;
+    a.rho = c->dRho;
+}
+
 int ensureLeafMap(SkirtMcrt* c) {
     if (c->mapL < 0 || c->mapReady) return SKIRT_OK;
     const size_t n = (size_t)leafMapSize(1 << c->mapL);
@@ -3989,19 +4038,7 @@ static int runPhase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, uint6
     for (int h = 0; h < kMaxHalves; h++) sT[h] = forked ? c->sT[h] : c->stream;
 
     Args a{};
-    a.ncells = c->ncells;
-    a.labsStride = c->labsStride;
-    a.nx = c->nx; a.ny = c->ny; a.nz = c->nz;
-    a.brick = c->brick ? 1 : 0;
-    a.mesh = c->dMesh;
-    a.gx0 = c->gx0; a.gx1 = c->gx1; a.gy0 = c->gy0; a.gy1 = c->gy1; a.gz0 = c->gz0; a.gz1 = c->gz1;
-    a.box = c->dBox; a.firstChild = c->dFirstChild; a.cellnumber = c->dCellnumber;
-    a.splitDir = c->binTree ? c->dSplitDir : nullptr;
-    a.father = c->dFather;
-    a.nbrOffset = c->dNbrOffset; a.nbrList = c->dNbrList; a.eps = c->eps; a.search = c->search;
-    a.site = c->dSite; a.vorStart = c->dVorStart; a.vorSlots = c->dVorSlots; a.vorScale = (float)c->vorScale; a.cellBbox = c->dCellBbox;
-    a.devCell = c->dDevCell;
-    a.vnb = c->vnb; a.blockOffset = c->dBlockOffset; a.blockList = c->dBlockList;
+    gridArgs(c, a);
     const bool bookkeeping = c->gridKind == SKIRT_GRID_OCTREE && c->search == SKIRT_TREE_BOOKKEEPING;
     const bool leafMap = c->gridKind == SKIRT_GRID_OCTREE && c->mapL >= 0 && p->has_dust && !bookkeeping;
     if (leafMap) {
@@ -4010,8 +4047,6 @@ static int runPhase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, uint6
         a.mapInvX = c->mapInv[0]; a.mapInvY = c->mapInv[1]; a.mapInvZ = c->mapInv[2];
         a.mapX0 = c->mapOrigin[0]; a.mapY0 = c->mapOrigin[1]; a.mapZ0 = c->mapOrigin[2];
     }
-    a.ncomp = std::max(1, c->ncomp); a.nlambda = c->nlambda;
-    a.rho = c->dRho;
     a.optics = c->dOptics;
     a.nstar = c->nstar; a.geomParam = c->dGeomParam; a.geomTable = c->dGeomTable; a.lum = c->dLum;
     a.lumtot = c->dLumtot; a.cdf = c->dCdf; a.emissionBias = c->emissionBias;
@@ -4367,6 +4402,40 @@ int skirt_mcrt_download_crossed(SkirtMcrt* c, uint64_t* hist, int bins) {
         hist[b] = v;
     }
     return SKIRT_OK;
+}
+
+int skirt_mcrt_column_densities(SkirtMcrt* c, const double* rays, int n, double* out) {
+    if (!c || n < 0 || (n > 0 && (!rays || !out))) return SKIRT_ERR_ARG;
+    if (n == 0) return SKIRT_OK;
+    if (!c->dRho) return fail(c, SKIRT_ERR_STATE, "no grid and media uploaded");
+    HIPCHECK(c, hipSetDevice(c->device));
+    Args a{};
+    gridArgs(c, a);
+    a.ldsMeshOff = a.ldsOptOff = a.ldsInstrOff = a.ldsSedOff = 0;
+    double* d = nullptr;
+    HIPCHECK(c, hipMalloc(&d, (size_t)n * 7 * sizeof(double)));
+    int rc = SKIRT_OK;
+    hipError_t e = hipMemcpyAsync(d, rays, (size_t)n * 6 * sizeof(double), hipMemcpyHostToDevice, c->stream);
+    const dim3 grid((n + kBlock - 1) / kBlock);
+    // the walks of the photon paths, through the node arrays for trees (equal to the leaf-map walk,
+    // tests/test_gpu_parity.py::test_leaf_map_walk_equals_node_walk)
+    if (e == hipSuccess) {
+        if (c->gridKind == SKIRT_GRID_CARTESIAN)
+            hipLaunchKernelGGL(columnKernel<SKIRT_GRID_CARTESIAN>, grid, dim3(kBlock),
+                               (size_t)(c->nx + c->ny + c->nz + 3) * sizeof(double), c->stream, a, d, n, d + 6 * (size_t)n);
+        else if (c->gridKind == SKIRT_GRID_VORONOI)
+            hipLaunchKernelGGL(columnKernel<SKIRT_GRID_VORONOI>, grid, dim3(kBlock), 0, c->stream, a, d, n, d + 6 * (size_t)n);
+        else if (c->search == SKIRT_TREE_BOOKKEEPING)
+            hipLaunchKernelGGL(columnKernel<kOctreeBookkeeping>, grid, dim3(kBlock), 0, c->stream, a, d, n, d + 6 * (size_t)n);
+        else
+            hipLaunchKernelGGL(columnKernel<kOctreeNodes>, grid, dim3(kBlock), 0, c->stream, a, d, n, d + 6 * (size_t)n);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipMemcpyAsync(out, d + 6 * (size_t)n, (size_t)n * sizeof(double), hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) rc = fail(c, SKIRT_ERR_HIP, hipGetErrorString(e));
+    (void)hipFree(d);
+    return rc;
 }
 
 int skirt_mcrt_stats(SkirtMcrt* c, SkirtStats* out) {

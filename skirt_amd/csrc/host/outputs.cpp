@@ -1,5 +1,6 @@
 #include "outputs.hpp"
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -316,6 +317,48 @@ void writeCellsCrossed(const Model& m, const std::string& prefix, const std::vec
     f.column("number of cells crossed", 'd');
     f.column("number of paths that crossed this number of cells", 'd');
     for (size_t i = 0; i < n; i++) f.row({(double)i, (double)hist[i]});
+}
+
+void writeConvergence(const Model& m, const std::string& prefix, const double sigma[3]) {
+    Units units(m.units_system);
+    const int Ncomp = (int)m.dust.size();
+    double M = 0.0;  // the grid's mass, in the reference's cell order
+    for (int c = 0; c < m.ncells(); c++) {
+        double rho = 0;
+        for (int h = 0; h < Ncomp; h++) rho += m.rho[(size_t)c * Ncomp + h];
+        M += rho * m.volume[c];
+    }
+    // CompDustDistribution: the sums over the components of nf times the geometry's value
+    // (DustComp.cpp:119-141; SpheGeometry.cpp:49-71 and AxGeometry.cpp:34-47 for the x and y axes)
+    int dim = 1;
+    double ref[3] = {0, 0, 0}, Mref = 0;
+    for (auto& d : m.dust) {
+        const bool ax = d.geom.kind == GeometryKind::ExpDisk;
+        dim = std::max(dim, ax ? 2 : 1);
+        const double sxy = ax ? 2.0 * d.geom.SigmaR() : 2.0 * d.geom.Sigmar();
+        ref[0] += d.nf * sxy;
+        ref[1] += d.nf * sxy;
+        ref[2] += d.nf * (ax ? d.geom.SigmaZ() : 2.0 * d.geom.Sigmar());
+        Mref += d.nf;
+    }
+    const std::string us = " " + units.unitFor("masssurfacedensity");
+    auto num = [&](double v) { return qtNumber(units.omasssurfacedensity(v), 'g', 6) + us; };
+    TextOut f(prefix + "_ds_convergence.dat");
+    f.line("Convergence check on the grid: ");
+    auto pair = [&](const std::string& what, double expected, double actual) {
+        f.line("   - " + what);
+        f.line("         expected value = " + num(expected));
+        f.line("         actual value =   " + num(actual));
+    };
+    if (dim == 1) {
+        pair("radial (r-axis) surface density", 0.5 * ref[0], 0.5 * sigma[0]);
+    } else {
+        pair("edge-on (R-axis) surface density", 0.5 * ref[0], 0.5 * sigma[0]);
+        pair("face-on (Z-axis) surface density", ref[2], sigma[2]);
+    }
+    f.line("   - total dust mass");
+    f.line("         expected value = " + qtNumber(units.omass(Mref), 'g', 6) + " " + units.unitFor("mass"));
+    f.line("         actual value =   " + qtNumber(units.omass(M), 'g', 6) + " " + units.unitFor("mass"));
 }
 
 }  // namespace skirt

@@ -27,6 +27,12 @@ void writeOutputs(const Model& m, const std::string& prefix, const std::vector<s
 // cells, written up to the last nonzero bin
 void writeCellsCrossed(const Model& m, const std::string& prefix, const std::vector<uint64_t>& hist);
 
+// DustSystem::writeconvergence (DustSystem.cpp:195-305): <prefix>_ds_convergence.dat, the grid's mass and
+// column densities through the origin (sigma: x, y and z axes, each the sum of its two half axes) beside
+// the dust distribution's analytic values. The geometries here are spherical (dimension 1) or axisymmetric
+// (ExpDisk, dimension 2); the dimension-3 branch of the reference has no geometry to reach it.
+void writeConvergence(const Model& m, const std::string& prefix, const double sigma[3]);
+
 // Qt-compatible number formatting: QString::number(v, 'e', prec) and QString::number(v, 'g', prec)
 std::string qtNumber(double v, char fmt, int prec);
 

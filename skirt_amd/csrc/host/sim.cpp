@@ -461,6 +461,21 @@ int skirt_sim_write(SkirtSim* s, const char* prefix) {
             if (rc) return rc;
             writeCellsCrossed(s->m, prefix, hist);
         }
+        if (s->m.hasDust && s->m.writeConvergence && s->eng) {
+            // the six half axes from the origin (DustSystem.cpp:213-242), walked by the engine
+            const double rays[36] = {0, 0, 0, 1, 0, 0, 0, 0, 0, -1, 0, 0, 0, 0, 0, 0, 1, 0,
+                                     0, 0, 0, 0, -1, 0, 0, 0, 0, 0, 0, 1, 0, 0, 0, 0, 0, -1};
+            double col[6];
+            int rc = check(s, skirt_mcrt_column_densities(s->eng, rays, 6, col));
+            if (rc) return rc;
+            double sigma[3];
+            for (int ax = 0; ax < 3; ax++) {
+                sigma[ax] = 0.0;
+                sigma[ax] += col[2 * ax];
+                sigma[ax] += col[2 * ax + 1];
+            }
+            writeConvergence(s->m, prefix, sigma);
+        }
     } catch (std::exception& e) {
         g_err = e.what();
         return SKIRT_ERR_ARG;

@@ -182,6 +182,14 @@ double Units::osurfacebrightness(double lambda, double flambda) const {
 
 double Units::olength(double x) const { return x / factor("length", unitFor("length")); }
 double Units::ovolume(double v) const { return v / factor("volume", unitFor("volume")); }
+double Units::omasssurfacedensity(double sigma) const {
+    return sigma / factor("masssurfacedensity", unitFor("masssurfacedensity"));
+}
+
+double Units::omass(double M) const {
+    return M / factor("mass", unitFor("mass"));
+}
+
 double Units::omassvolumedensity(double rho) const {
     return rho / factor("massvolumedensity", unitFor("massvolumedensity"));
 }

@@ -44,6 +44,8 @@ public:
     double olength(double x) const;
     double ovolume(double v) const;
     double omassvolumedensity(double rho) const;
+    double omasssurfacedensity(double sigma) const;
+    double omass(double M) const;
     double obolluminosity(double L) const;
 
     const std::string& system() const { return system_; }

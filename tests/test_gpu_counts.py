@@ -89,3 +89,27 @@ def test_ds_crossed_file_matches_oracle(tmp_path):
     assert gpu.startswith("# total number of cells in grid: ")
     assert "# column 2: number of paths that crossed this number of cells" in gpu
     assert gpu == orc
+
+
+@pytest.mark.parametrize("name,disk", [("pan_cart16", False), ("pan_oct", False), ("vor_pan", False),
+                                       ("oligo_2comp", False), ("pan_oct", True)],
+                         ids=["cart", "oct", "vor", "oligo_2comp", "oct_disk"])
+def test_ds_convergence_file_matches_oracle(tmp_path, name, disk):
+    """writeConvergence="true": the host driver writes <prefix>_ds_convergence.dat from the engine's walk of
+    the six half axes from the origin (skirt_mcrt_column_densities), identical to the oracle's file."""
+    from test_convergence import convergence_ski
+    path = convergence_ski(tmp_path, name, disk)
+    sim = S.Simulation(path, packages=10)
+    sim.attach(0)
+    sim.run_stellar()
+    sim.fetch()
+    sim.write(os.path.join(tmp_path, "gpu"))
+    O.run(path, rng=O.RNG_PHILOX, threads=4, packages=10, phases=O.PHASES_STELLAR, outprefix=os.path.join(tmp_path, "orc"))
+    gpu = open(os.path.join(tmp_path, "gpu_ds_convergence.dat")).read()
+    orc = open(os.path.join(tmp_path, "orc_ds_convergence.dat")).read()
+    assert gpu == orc
+    # the entry point itself, on the axes and off them (kg/m2)
+    rays = np.array([[0, 0, 0, 1, 0, 0], [0, 0, 0, -1, 0, 0], [0, 0, 0, 0, 1, 0], [0, 0, 0, 0, -1, 0],
+                     [0, 0, 0, 0, 0, 1], [0, 0, 0, 0, 0, -1], [10, -20, 5, 0.6, 0.0, 0.8]], dtype=np.float64)
+    col = sim.column_densities(rays)
+    assert np.all(col > 0)
