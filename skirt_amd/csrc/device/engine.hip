@@ -32,6 +32,7 @@
 #include <string>
 #include <vector>
 
+#include "vor_terms.hpp"
 #include "../../../include/skirt_mcrt.h"
 #include "philox.hpp"
 
@@ -168,8 +169,6 @@ struct alignas(16) VorEntry {
     int next;
 };
 constexpr int kVorHead = 3;  // header slots
-// bound factor of the approximate (single-precision) plane distances: 16 x 2^-24
-constexpr float kVorEpsF = 1.0f / (1 << 20);
 #ifndef SKIRT_VOR_UNROLL
 #define SKIRT_VOR_UNROLL 8  // at 2 waves/SIMD, no spills (C4 6.17e7 pkt/s; 4: 6.07e7, 2: 5.29e7)
 #endif
@@ -1085,7 +1084,8 @@ struct Grid<SKIRT_GRID_VORONOI> {
         const VorEntry* B;
         double pwx, pwy, pwz, rhow;
         int idw, cnt;
-        float Dx, Dy, Dz, Dn, fkx, fky, fkz;
+        float Dx, Dy, Dz, fkx, fky, fkz;
+        float eA, eA2, eB2;  // the cell's error terms: eA, 2 eA, 2 (eA |D|_1 + kVorEpsF max |n|^2)
     };
     // U: the least upper bound of the certain exits; L1 <= L2: the two least lower bounds of the possible
     // exits, w1: the first one's `next`
@@ -1101,24 +1101,23 @@ struct Grid<SKIRT_GRID_VORONOI> {
     // so every entry takes the same branch-free arithmetic; lo = hi = FLT_MAX: certainly no exit.
     __device__ static __forceinline__ void bounds(const StepIn& s, const VorEntry& en, bool valid, float& lo,
                                                   float& hi) {
-        // the plane distance s = (n.D + |n|^2/2) / (n.k) with per-entry Cauchy-Schwarz error terms:
-        // |d(n.k)| <= eA = kVorEpsF |n|_1 and |d(n.D + |n|^2/2)| <= eA |D|_1 + kVorEpsF |n|^2, several
-        // times the float roundings of the offsets, D, k and the fused operations (round 2 summed the
-        // absolute terms of each product instead: 55 operations per entry against 38;
-        // tools/vor_compact_check.cpp, mode d, checks the resulting steps against the reference's)
+        // the plane distance s = (n.D + |n|^2/2) / (n.k) with Cauchy-Schwarz error terms: |d(n.k)| <= eA
+        // and |d(n.D + |n|^2/2)| <= eB = eA |D|_1 + kVorEpsF |n|^2, at the cell's largest |n|_1 and |n|^2
+        // (vor_terms.hpp; several times the float roundings of the offsets, D, k and the fused
+        // operations). 33 operations per entry (per-entry terms: 38; round 2's sums of the absolute
+        // terms of each product: 55); tools/vor_compact_check.cpp, mode d, checks the resulting steps
+        // against the reference's.
         const float nx = en.ox, ny = en.oy, nz = en.oz;
         const float n2 = fmaf(nz, nz, fmaf(ny, ny, nx * nx));
         const float den = fmaf(nz, s.fkz, fmaf(ny, s.fky, nx * s.fkx));
         const float num = fmaf(n2, 0.5f, fmaf(nz, s.Dz, fmaf(ny, s.Dy, nx * s.Dx)));
-        const float eA = kVorEpsF * (fabsf(nx) + fabsf(ny) + fabsf(nz));
-        const float eB = fmaf(eA, s.Dn, kVorEpsF * n2);
         const float inv = __builtin_amdgcn_rcpf(den);
         const float sa = num * inv;
-        const float err = fmaf(2.0f * fmaf(fabsf(sa), eA, eB), inv, fabsf(sa) * kVorEpsF);
+        const float err = fmaf(fmaf(fabsf(sa), s.eA2, s.eB2), inv, fabsf(sa) * kVorEpsF);
         // den > 2 eA: the sign of n.k and the interval are certain; den <= -eA: moving away for
         // certain; otherwise (or NaN offsets: a degenerate wall) the sign is uncertain
-        const bool sure = den > 2.0f * eA;
-        const bool none = !valid || den <= -eA || (sure && !(sa + err > 0.f));
+        const bool sure = den > s.eA2;
+        const bool none = !valid || den <= -s.eA || (sure && !(sa + err > 0.f));
         lo = none ? FLT_MAX : sure ? sa - err : -FLT_MAX;
         hi = (none || !sure) ? FLT_MAX : sa + err;
     }
@@ -1142,6 +1141,7 @@ struct Grid<SKIRT_GRID_VORONOI> {
         const int4 h2 = *reinterpret_cast<const int4*>(s.B + 2);
         s.pwx = h0.x; s.pwy = h0.y; s.pwz = h1.x; s.rhow = h1.y;
         s.idw = h2.x; s.cnt = h2.y;
+        const float eA = __int_as_float(h2.z), eBn = __int_as_float(h2.w);  // the cell's terms (upload)
         if (r.ck) {
             const double sq = planeDist(r, r.bx0, r.by0, r.bz0, s.pwx, s.pwy, s.pwz);
             if (!seg(r.ci, r.rho0, sq)) return false;
@@ -1150,8 +1150,9 @@ struct Grid<SKIRT_GRID_VORONOI> {
         }
         const float sc = a.vorScale;
         s.Dx = (float)((s.pwx - r.x) * sc); s.Dy = (float)((s.pwy - r.y) * sc); s.Dz = (float)((s.pwz - r.z) * sc);
-        s.Dn = fabsf(s.Dx) + fabsf(s.Dy) + fabsf(s.Dz);  // >= |D|
+        const float Dn = fabsf(s.Dx) + fabsf(s.Dy) + fabsf(s.Dz);  // |D|_1
         s.fkx = (float)r.dx; s.fky = (float)r.dy; s.fkz = (float)r.dz;
+        s.eA = eA; s.eA2 = 2.0f * eA; s.eB2 = 2.0f * fmaf(eA, Dn, eBn);
         return true;
     }
 
@@ -1309,8 +1310,8 @@ struct Grid<SKIRT_GRID_VORONOI> {
                                 // the lane mask of a divergently assigned bool lost its upper 32 lanes there)
         StepIn sg{};
         sg.Dx = __shfl(s.Dx, owner); sg.Dy = __shfl(s.Dy, owner); sg.Dz = __shfl(s.Dz, owner);
-        sg.Dn = __shfl(s.Dn, owner);
         sg.fkx = __shfl(s.fkx, owner); sg.fky = __shfl(s.fky, owner); sg.fkz = __shfl(s.fkz, owner);
+        sg.eA = __shfl(s.eA, owner); sg.eA2 = __shfl(s.eA2, owner); sg.eB2 = __shfl(s.eB2, owner);
         const int cnt = __shfl(s.cnt, owner);
         const bool act = grp && cnt > 0;
         Best b{FLT_MAX, FLT_MAX, FLT_MAX, 0};
@@ -3547,8 +3548,6 @@ int skirt_mcrt_upload_grid(SkirtMcrt* c, const SkirtGridDesc* g) {
             const double head[4] = {sm[0], sm[1], sm[2], 0.0};  // rho of component 0: set by upload_media
             std::memcpy(blk, head, sizeof head);
             const int cnt = g->cell_nbr_offset[m + 1] - g->cell_nbr_offset[m];
-            const int ids[4] = {d, cnt, 0, 0};
-            std::memcpy(blk + 2, ids, sizeof ids);
             int o = kVorHead;
             for (int q = g->cell_nbr_offset[m]; q < g->cell_nbr_offset[m + 1]; q++, o++) {
                 const int id = g->cell_nbr_list[q];
@@ -3569,6 +3568,13 @@ int skirt_mcrt_upload_grid(SkirtMcrt* c, const SkirtGridDesc* g) {
                                  (float)((si[2] - sm[2]) * c->vorScale), start[c->devCell[id]]};
                 }
             }
+            // the header's last words: id, count and the cell's error terms of the bounds (vor_terms.hpp)
+            float eA, eB;
+            vorErrorTerms(&blk[kVorHead].ox, cnt, 4, &eA, &eB);
+            int ids[4] = {d, cnt, 0, 0};
+            std::memcpy(&ids[2], &eA, 4);
+            std::memcpy(&ids[3], &eB, 4);
+            std::memcpy(blk + 2, ids, sizeof ids);
         }
         c->vorSlotsHost = std::move(slots);
         std::vector<int> blocks(std::max(nbl, 1), 0);

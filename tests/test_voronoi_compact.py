@@ -23,9 +23,10 @@ def checker(tmp_path_factory):
     return exe
 
 
-# the checker's modes: n -- double bounds; f -- the round-2 float bounds; d -- the device's step (per-entry
-# Cauchy-Schwarz bounds, engine.hip Grid<SKIRT_GRID_VORONOI>::step)
-@pytest.mark.parametrize("mode", ["n", "f", "d"], ids=["f64", "f32_r2", "device"])
+# the checker's modes: n -- double bounds; f -- the round-2 float bounds; x -- per-entry Cauchy-Schwarz
+# terms; d -- the device's step (the cell's largest terms from its header, engine.hip
+# Grid<SKIRT_GRID_VORONOI>::bounds, computed by the engine's own vor_terms.hpp)
+@pytest.mark.parametrize("mode", ["n", "f", "x", "d"], ids=["f64", "f32_r2", "f32_entry", "device"])
 def test_compact_voronoi_step_is_exact(checker, mode):
     r = subprocess.run([checker, "20000", "3000", mode], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr

@@ -7,6 +7,7 @@
 //   g++ -O2 -std=c++17 -ffp-contract=off -I include tools/vor_compact_check.cpp -L skirt_amd -lskirt_amd \
 //       -Wl,-rpath,$PWD/skirt_amd -o /tmp/vor_compact_check && /tmp/vor_compact_check 100000 20000 d
 // (mode d: the device's round-3 bounds; f / e / c: round-2 float variants; none: double bounds)
+#include "../skirt_amd/csrc/device/vor_terms.hpp"
 #include <cfloat>
 #include <cmath>
 #include <cstdint>
@@ -24,6 +25,7 @@ struct Mesh {
     SkirtGridDesc g;
     std::vector<float> off;  // per list entry: float(site_nbr - site_own), 3 per entry
     std::vector<float> nmax;  // per cell: the longest scaled offset of its list
+    std::vector<float> eA, eB;  // per cell: the device's error terms (vor_terms.hpp)
 };
 
 double wallDist(const SkirtGridDesc& g, int mi, const double r[3], const double k[3]) {
@@ -66,6 +68,7 @@ int refStep(const SkirtGridDesc& g, int m, const double r[3], const double k[3],
 constexpr float kEpsF = 1.0f / (1 << 20);
 float gScale = 1.0f;
 bool gCell = false, gEntry = false;  // per-cell / per-entry-norm error bounds instead of the round-2 device's
+bool gPerEntry = false;  // mode x: the first round-3 device step (per-entry terms)
 bool gDevice = false;                // the round-3 device step: per-entry Cauchy-Schwarz error terms
 long gSignFallbacks = 0;  // re-evaluations with an entry whose n.k sign is uncertain
 long gWholeList = 0;      // re-evaluations over the whole list (more than 4 possible winners)
@@ -145,16 +148,18 @@ static int compactStepF(const Mesh& M, int m, const double r[3], const double k[
         const int mi = g.cell_nbr_list[q];
         const float nx = M.off[3 * (size_t)q], ny = M.off[3 * (size_t)q + 1], nz = M.off[3 * (size_t)q + 2];
         if (gDevice) {
-            // Grid<SKIRT_GRID_VORONOI>::step (engine.hip) operation for operation
+            // Grid<SKIRT_GRID_VORONOI>::bounds (engine.hip) operation for operation: the error terms from
+            // the cell's largest |n|_1 and |n|^2 (the header's eA, eB; mode x: per entry, as in round 3's
+            // first version)
             const float Dn = fabsf(Dx) + fabsf(Dy) + fabsf(Dz);
             const float n2 = fmaf(nz, nz, fmaf(ny, ny, nx * nx));
             const float den = fmaf(nz, kz, fmaf(ny, ky, nx * kx));
             const float num = fmaf(n2, 0.5f, fmaf(nz, Dz, fmaf(ny, Dy, nx * Dx)));
-            const float eA = kEpsF * (fabsf(nx) + fabsf(ny) + fabsf(nz));
-            const float eB = fmaf(eA, Dn, kEpsF * n2);
+            const float eA = gPerEntry ? kEpsF * (fabsf(nx) + fabsf(ny) + fabsf(nz)) : M.eA[m];
+            const float eB = gPerEntry ? fmaf(eA, Dn, kEpsF * n2) : fmaf(eA, Dn, M.eB[m]);
             const float inv = 1.0f / den;
             const float sa = num * inv;
-            const float err = fmaf(2.0f * fmaf(fabsf(sa), eA, eB), inv, fabsf(sa) * kEpsF);
+            const float err = fmaf(fmaf(fabsf(sa), 2.0f * eA, 2.0f * eB), inv, fabsf(sa) * kEpsF);
             const bool sure = den > 2.0f * eA;
             const bool none = den <= -eA || (sure && !(sa + err > 0.f));
             const float lo = none ? FLT_MAX : sure ? sa - err : -FLT_MAX;
@@ -227,8 +232,10 @@ int main(int argc, char** argv) {
     }
     const double ext[6] = {-L, -L, -L, L, L, L};
     gScale = (float)(1.0 / L);
-    const bool f32 = argc > 3 && (argv[3][0] == 'f' || argv[3][0] == 'c' || argv[3][0] == 'e' || argv[3][0] == 'd');
-    gDevice = argc > 3 && argv[3][0] == 'd';
+    const bool f32 = argc > 3 && (argv[3][0] == 'f' || argv[3][0] == 'c' || argv[3][0] == 'e' || argv[3][0] == 'd' ||
+                                  argv[3][0] == 'x');
+    gDevice = argc > 3 && (argv[3][0] == 'd' || argv[3][0] == 'x');
+    gPerEntry = argc > 3 && argv[3][0] == 'x';
     gCell = argc > 3 && argv[3][0] == 'c';
     gEntry = argc > 3 && argv[3][0] == 'e';
     if (gEntry) gCell = true;
@@ -263,6 +270,13 @@ int main(int argc, char** argv) {
             const float x = M.off[3 * (size_t)q], y = M.off[3 * (size_t)q + 1], z = M.off[3 * (size_t)q + 2];
             M.nmax[m] = fmaxf(M.nmax[m], sqrtf(x * x + y * y + z * z) * (1.0f + 4 * FLT_EPSILON));
         }
+    // the header's per-cell error terms as the engine's Voronoi upload computes them
+    M.eA.assign(N, 0.f);
+    M.eB.assign(N, 0.f);
+    for (int m = 0; m < N; m++) {
+        const int q0 = g.cell_nbr_offset[m], q1 = g.cell_nbr_offset[m + 1];
+        vorErrorTerms(M.off.data() + 3 * (size_t)q0, q1 - q0, 3, &M.eA[m], &M.eB[m]);
+    }
     long steps = 0, fallbacks = 0, mismatches = 0;
     for (int i = 0; i < R; i++) {
         // a random start site's cell and an isotropic direction (positions start at the site)
@@ -282,7 +296,8 @@ int main(int argc, char** argv) {
         }
     }
     printf("%s: sites %d, rays %d, steps %ld, exact re-evaluations %ld (%.3g per step), mismatches %ld\n",
-           gDevice ? "f32 device bounds (per-entry Cauchy-Schwarz, round 3)" : gEntry ? "f32 per-entry norm bounds" : gCell ? "f32 per-cell bounds" : f32 ? "f32 bounds" : "f64 bounds", N, R, steps,
+           gPerEntry ? "f32 per-entry Cauchy-Schwarz bounds (round 3, first)" :
+           gDevice ? "f32 device bounds (per-cell Cauchy-Schwarz terms)" : gEntry ? "f32 per-entry norm bounds" : gCell ? "f32 per-cell bounds" : f32 ? "f32 bounds" : "f64 bounds", N, R, steps,
            fallbacks, (double)fallbacks / steps, mismatches);
     if (f32) printf("  of which with an uncertain n.k sign: %ld; over the whole list: %ld\n", gSignFallbacks, gWholeList);
     skirt_host_voronoi_free(v);
