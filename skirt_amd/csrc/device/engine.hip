@@ -1100,7 +1100,7 @@ struct Grid<SKIRT_GRID_VORONOI> {
     // the |s| term. Walls are stored as the bisector plane with the site's mirror image (the same plane),
     // so every entry takes the same branch-free arithmetic; lo = hi = FLT_MAX: certainly no exit.
     __device__ static __forceinline__ void bounds(const StepIn& s, const VorEntry& en, bool valid, float& lo,
-                                                  float& hi) {
+                                                  float& ucand) {
         // the plane distance s = (n.D + |n|^2/2) / (n.k) with Cauchy-Schwarz error terms: |d(n.k)| <= eA
         // and |d(n.D + |n|^2/2)| <= eB = eA |D|_1 + kVorEpsF |n|^2, at the cell's largest |n|_1 and |n|^2
         // (vor_terms.hpp; several times the float roundings of the offsets, D, k and the fused
@@ -1114,17 +1114,21 @@ struct Grid<SKIRT_GRID_VORONOI> {
         const float inv = __builtin_amdgcn_rcpf(den);
         const float sa = num * inv;
         const float err = fmaf(fmaf(fabsf(sa), s.eA2, s.eB2), inv, fabsf(sa) * kVorEpsF);
-        // den > 2 eA: the sign of n.k and the interval are certain; den <= -eA: moving away for
-        // certain; otherwise (or NaN offsets: a degenerate wall) the sign is uncertain
-        const bool sure = den > s.eA2;
-        const bool none = !valid || den <= -s.eA || (sure && !(sa + err > 0.f));
-        lo = none ? FLT_MAX : sure ? sa - err : -FLT_MAX;
-        hi = (none || !sure) ? FLT_MAX : sa + err;
+        // den > 2 eA: the sign of n.k and the interval [sa - err, sa + err] are certain (an interval at or
+        // below 0: no exit); den <= -eA: moving away for certain; otherwise (or NaN offsets: a degenerate
+        // wall) the sign is uncertain: lo = -FLT_MAX. Entries past the count: no exit. ucand: the upper
+        // bound of a certain exit (lo > 0), else FLT_MAX. Selected as floats, no bool temporaries.
+        const float lov = sa - err, hiv = sa + err;
+        const bool sure = valid && den > s.eA2;
+        const bool maybe = valid && !(den <= -s.eA);
+        const float loSure = hiv > 0.f ? lov : FLT_MAX;
+        lo = sure ? loSure : (maybe ? -FLT_MAX : FLT_MAX);
+        ucand = (sure && lov > 0.f) ? hiv : FLT_MAX;
     }
 
     // one entry's bounds into the running Best, in list order
-    __device__ static __forceinline__ void take(Best& b, float lo, float hi, int next) {
-        b.U = fminf(b.U, lo > 0.f ? hi : FLT_MAX);
+    __device__ static __forceinline__ void take(Best& b, float lo, float ucand, int next) {
+        b.U = fminf(b.U, ucand);
         b.w1 = lo < b.L1 ? next : b.w1;
         b.L2 = __builtin_amdgcn_fmed3f(b.L1, b.L2, lo);
         b.L1 = fminf(b.L1, lo);
@@ -1194,8 +1198,8 @@ struct Grid<SKIRT_GRID_VORONOI> {
                 for (int u = 0; u < kVorUnroll; u++) e[u] = B[kVorHead + q0 + u];
 #pragma unroll
                 for (int u = 0; u < kVorUnroll; u++) {
-                    float lo, hi;
-                    bounds(s, e[u], q0 + u < cnt, lo, hi);
+                    float lo, uc;
+                    bounds(s, e[u], q0 + u < cnt, lo, uc);
                     if (lo < FLT_MAX && lo <= b.U) {
                         const int nx = e[u].next;
                         c0 = nc == 0 ? nx : c0; c1 = nc == 1 ? nx : c1; c2 = nc == 2 ? nx : c2; c3 = nc == 3 ? nx : c3;
@@ -1266,9 +1270,9 @@ struct Grid<SKIRT_GRID_VORONOI> {
             }
 #pragma unroll
             for (int u = 0; u < kVorUnroll; u++) {
-                float lo, hi;
-                bounds(s, e[u], q0 + u < s.cnt, lo, hi);
-                take(b, lo, hi, e[u].next);
+                float lo, uc;
+                bounds(s, e[u], q0 + u < s.cnt, lo, uc);
+                take(b, lo, uc, e[u].next);
             }
         }
         return decide(a, r, s, b, seg);
@@ -1318,9 +1322,9 @@ struct Grid<SKIRT_GRID_VORONOI> {
         for (int q0 = 0; __ballot(act && q0 < cnt); q0 += G) {
             const bool valid = act && q0 + j < cnt;
             if (q0 && valid) e = Bg[kVorHead + q0 + j];
-            float lo, hi;
-            bounds(sg, e, valid, lo, hi);
-            take(b, lo, hi, e.next);
+            float lo, uc;
+            bounds(sg, e, valid, lo, uc);
+            take(b, lo, uc, e.next);
         }
         for (int o = 1; o < G; o <<= 1) {
             const float U2 = __shfl_xor(b.U, o), L12 = __shfl_xor(b.L1, o), L22 = __shfl_xor(b.L2, o);

@@ -160,12 +160,14 @@ static int compactStepF(const Mesh& M, int m, const double r[3], const double k[
             const float inv = 1.0f / den;
             const float sa = num * inv;
             const float err = fmaf(fmaf(fabsf(sa), 2.0f * eA, 2.0f * eB), inv, fabsf(sa) * kEpsF);
+            const float lov = sa - err, hiv = sa + err;
             const bool sure = den > 2.0f * eA;
-            const bool none = den <= -eA || (sure && !(sa + err > 0.f));
-            const float lo = none ? FLT_MAX : sure ? sa - err : -FLT_MAX;
-            const float hi = (none || !sure) ? FLT_MAX : sa + err;
+            const bool maybe = !(den <= -eA);
+            const float loSure = hiv > 0.f ? lov : FLT_MAX;
+            const float lo = sure ? loSure : (maybe ? -FLT_MAX : FLT_MAX);
+            const float ucand = (sure && lov > 0.f) ? hiv : FLT_MAX;
             gLo[q - g.cell_nbr_offset[m]] = lo;
-            U = fminf(U, lo > 0.f ? hi : FLT_MAX);
+            U = fminf(U, ucand);
             w1 = lo < L1 ? mi : w1;
             L2 = fmaxf(fminf(L1, L2), fminf(fmaxf(L1, L2), lo));
             L1 = fminf(L1, lo);
