@@ -157,18 +157,40 @@ __device__ __forceinline__ int rayEll(unsigned f) { return (int)(f >> 18); }
 struct LeafEntry;
 
 // Voronoi cells on the device: per cell a block of 16-byte slots, contiguous, in device cell order: a
-// 48-byte header {exact site x, y | z, rho of component 0 | device cell number, neighbour count, 0, 0}
-// followed by one slot per neighbour, in the reference's list order: the neighbour's site relative to the
-// cell's site, scaled by Args::vorScale and rounded to float (an approximate bisector plane), and where the
-// neighbour's block starts
-// (walls: -1 xmin .. -6 zmax). A step bounds every plane distance from the float offsets, and evaluates
-// the reference's exact expression only for the winner (from the winner's header, which is the next
-// step's first load) or, when the bounds cannot single one out, for every possible winner.
+// 48-byte header {exact site x, y | z, rho of component 0 | device cell number, neighbour count, the
+// bounds' error terms eA, eB (vor_terms.hpp)} followed by one 16-byte slot per neighbour, in the reference's
+// list order: the neighbour's site relative to the cell's site, scaled by Args::vorScale and rounded to
+// float (an approximate bisector plane), and where the neighbour's block starts (walls: -1 xmin .. -6
+// zmax). The entries are stored in pairs, component-interleaved: slots {ox0, ox1, oy0, oy1} and {oz0, oz1,
+// next0, next1}, so that the two 16-byte loads of a pair hand the packed (v_pk_*) arithmetic its operand
+// pairs directly; a list of odd length ends in an unused half pair. A step bounds every plane distance from
+// the float offsets, and evaluates the reference's exact expression only for the winner (from the winner's
+// header, which is the next step's first load) or, when the bounds cannot single one out, for every
+// possible winner.
 struct alignas(16) VorEntry {
     float ox, oy, oz;
     int next;
 };
 constexpr int kVorHead = 3;  // header slots
+
+// entry q of the list of the cell whose block starts at B
+__device__ __forceinline__ VorEntry vorEntry(const VorEntry* B, int q) {
+    const float* P = reinterpret_cast<const float*>(B + kVorHead + (q & ~1));
+    const int h = q & 1;
+    return VorEntry{P[h], P[2 + h], P[4 + h], __float_as_int(P[6 + h])};
+}
+
+// entries q0 .. q0 + N - 1 (q0 even), two 16-byte loads per pair
+template <int N>
+__device__ __forceinline__ void vorEntries(const VorEntry* B, int q0, VorEntry (&e)[N]) {
+#pragma unroll
+    for (int p = 0; p < N / 2; p++) {
+        const float4 x = *reinterpret_cast<const float4*>(B + kVorHead + q0 + 2 * p);
+        const int4 y = *reinterpret_cast<const int4*>(B + kVorHead + q0 + 2 * p + 1);
+        e[2 * p] = VorEntry{x.x, x.z, __int_as_float(y.x), y.z};
+        e[2 * p + 1] = VorEntry{x.y, x.w, __int_as_float(y.y), y.w};
+    }
+}
 #ifndef SKIRT_VOR_UNROLL
 #define SKIRT_VOR_UNROLL 8  // at 2 waves/SIMD, no spills (C4 6.17e7 pkt/s; 4: 6.07e7, 2: 5.29e7)
 #endif
@@ -1194,8 +1216,7 @@ struct Grid<SKIRT_GRID_VORONOI> {
             int c0 = 0, c1 = 0, c2 = 0, c3 = 0, nc = 0;
             VorEntry e[kVorUnroll];
             for (int q0 = 0; q0 < cnt; q0 += kVorUnroll) {
-#pragma unroll
-                for (int u = 0; u < kVorUnroll; u++) e[u] = B[kVorHead + q0 + u];
+                vorEntries(B, q0, e);
 #pragma unroll
                 for (int u = 0; u < kVorUnroll; u++) {
                     float lo, uc;
@@ -1225,7 +1246,7 @@ struct Grid<SKIRT_GRID_VORONOI> {
                     double pix[G], piy[G], piz[G];
 #pragma unroll
                     for (int u = 0; u < G; u++) {
-                        nxt[u] = B[kVorHead + q0 + u].next;
+                        nxt[u] = vorEntry(B, q0 + u).next;
                         pix[u] = piy[u] = piz[u] = 0.0;
                         if (q0 + u < cnt && nxt[u] >= 0) siteAt(a, nxt[u], pix[u], piy[u], piz[u]);
                     }
@@ -1259,15 +1280,11 @@ struct Grid<SKIRT_GRID_VORONOI> {
         StepIn s;
         s.B = a.vorSlots + r.cj;
         VorEntry e[kVorUnroll];
-#pragma unroll
-        for (int u = 0; u < kVorUnroll; u++) e[u] = s.B[kVorHead + u];
+        vorEntries(s.B, 0, e);
         if (!head(a, r, s, seg)) return false;
         Best b{FLT_MAX, FLT_MAX, FLT_MAX, 0};
         for (int q0 = 0; q0 < s.cnt; q0 += kVorUnroll) {
-            if (q0) {
-#pragma unroll
-                for (int u = 0; u < kVorUnroll; u++) e[u] = s.B[kVorHead + q0 + u];
-            }
+            if (q0) vorEntries(s.B, q0, e);
 #pragma unroll
             for (int u = 0; u < kVorUnroll; u++) {
                 float lo, uc;
@@ -1305,7 +1322,7 @@ struct Grid<SKIRT_GRID_VORONOI> {
         const int cj = __shfl(r.cj, owner);
         const VorEntry* Bg = a.vorSlots + cj;
         VorEntry e{0.f, 0.f, 0.f, -1};
-        if (grp) e = Bg[kVorHead + j];  // with the header, one round (the array is padded by kVorPad slots)
+        if (grp) e = vorEntry(Bg, j);  // with the header, one round (the array is padded by kVorPad slots)
         StepIn s{};
         s.B = a.vorSlots + r.cj;
         bool alive = false;
@@ -1321,7 +1338,7 @@ struct Grid<SKIRT_GRID_VORONOI> {
         Best b{FLT_MAX, FLT_MAX, FLT_MAX, 0};
         for (int q0 = 0; __ballot(act && q0 < cnt); q0 += G) {
             const bool valid = act && q0 + j < cnt;
-            if (q0 && valid) e = Bg[kVorHead + q0 + j];
+            if (q0 && valid) e = vorEntry(Bg, q0 + j);
             float lo, uc;
             bounds(sg, e, valid, lo, uc);
             take(b, lo, uc, e.next);
@@ -1356,7 +1373,7 @@ struct Grid<SKIRT_GRID_VORONOI> {
         const double target = d2(sx, sy, sz);
         const int cnt = reinterpret_cast<const int4*>(a.vorSlots + start + 2)->y;
         for (int q = 0; q < cnt; q++) {
-            const int nxt = a.vorSlots[start + kVorHead + q].next;
+            const int nxt = vorEntry(a.vorSlots + start, q).next;
             if (nxt < 0) continue;
             siteAt(a, nxt, sx, sy, sz);
             if (d2(sx, sy, sz) < target) return false;
@@ -3530,14 +3547,14 @@ int skirt_mcrt_upload_grid(SkirtMcrt* c, const SkirtGridDesc* g) {
         std::vector<int> refOf(N);
         for (int m = 0; m < N; m++) refOf[c->devCell[m]] = m;
         std::vector<double> site(3 * (size_t)N), bbox(6 * (size_t)N);
-        // each device cell's block: kVorHead header slots + one slot per neighbour (see VorEntry); the
-        // array is padded by kVorPad slots, since a step loads whole groups of entries
+        // each device cell's block: kVorHead header slots + one slot per neighbour, in pairs (see VorEntry);
+        // the array is padded by kVorPad slots, since a step loads whole groups of entries
         std::vector<int> start(N + 1, 0);
         for (int d = 0; d < N; d++) {
             const int m = refOf[d];
             const int cnt = g->cell_nbr_offset[m + 1] - g->cell_nbr_offset[m];
             if (cnt < 1) return fail(c, SKIRT_ERR_ARG, "Voronoi cell without neighbours");
-            start[d + 1] = start[d] + kVorHead + cnt;
+            start[d + 1] = start[d] + kVorHead + ((cnt + 1) & ~1);  // pairs of entries
         }
         if ((size_t)start[N] + kVorPad >= (size_t)INT32_MAX) return fail(c, SKIRT_ERR_UNSUPPORTED, "Voronoi mesh too large");
         std::vector<VorEntry> slots((size_t)start[N] + kVorPad, VorEntry{0.f, 0.f, 0.f, -1});
@@ -3552,10 +3569,11 @@ int skirt_mcrt_upload_grid(SkirtMcrt* c, const SkirtGridDesc* g) {
             const double head[4] = {sm[0], sm[1], sm[2], 0.0};  // rho of component 0: set by upload_media
             std::memcpy(blk, head, sizeof head);
             const int cnt = g->cell_nbr_offset[m + 1] - g->cell_nbr_offset[m];
-            int o = kVorHead;
+            std::vector<float> off(3 * (size_t)cnt);
+            int o = 0;
             for (int q = g->cell_nbr_offset[m]; q < g->cell_nbr_offset[m + 1]; q++, o++) {
                 const int id = g->cell_nbr_list[q];
-                VorEntry& e = blk[o];
+                VorEntry e;
                 if (id < 0) {
                     // a wall (-1 xmin, -2 xmax, ... -6 zmax) is the bisector plane of the site and its mirror
                     // image: the offset to the mirror site along the wall's axis (NaN when the site lies on
@@ -3571,10 +3589,16 @@ int skirt_mcrt_upload_grid(SkirtMcrt* c, const SkirtGridDesc* g) {
                     e = VorEntry{(float)((si[0] - sm[0]) * c->vorScale), (float)((si[1] - sm[1]) * c->vorScale),
                                  (float)((si[2] - sm[2]) * c->vorScale), start[c->devCell[id]]};
                 }
+                // entry o in its pair (see VorEntry): {ox0, ox1, oy0, oy1} {oz0, oz1, next0, next1}
+                float* P = reinterpret_cast<float*>(blk + kVorHead + (o & ~1));
+                const int h = o & 1;
+                P[h] = e.ox; P[2 + h] = e.oy; P[4 + h] = e.oz;
+                std::memcpy(P + 6 + h, &e.next, 4);
+                off[3 * (size_t)o] = e.ox; off[3 * (size_t)o + 1] = e.oy; off[3 * (size_t)o + 2] = e.oz;
             }
             // the header's last words: id, count and the cell's error terms of the bounds (vor_terms.hpp)
             float eA, eB;
-            vorErrorTerms(&blk[kVorHead].ox, cnt, 4, &eA, &eB);
+            vorErrorTerms(off.data(), cnt, 3, &eA, &eB);
             int ids[4] = {d, cnt, 0, 0};
             std::memcpy(&ids[2], &eA, 4);
             std::memcpy(&ids[3], &eB, 4);
