@@ -192,9 +192,12 @@ __device__ __forceinline__ void vorEntries(const VorEntry* B, int q0, VorEntry (
     }
 }
 #ifndef SKIRT_VOR_UNROLL
-#define SKIRT_VOR_UNROLL 8  // at 2 waves/SIMD, no spills (C4 6.17e7 pkt/s; 4: 6.07e7, 2: 5.29e7)
+#define SKIRT_VOR_UNROLL 6  // entries per load group, even (pairs); two groups in flight: C4 7.44e7 pkt/s, 8: 7.03e7 (spills), 4: 7.36e7; one group of 8: 7.33e7 (profiles/r03_vor_pipe.txt)
 #endif
 constexpr int kVorUnroll = SKIRT_VOR_UNROLL;
+#ifndef SKIRT_VOR_PIPE
+#define SKIRT_VOR_PIPE 1  // two groups of entries in flight per step (see Grid<SKIRT_GRID_VORONOI>::step)
+#endif
 #ifndef SKIRT_VOR_FALLBACK_GROUP
 #define SKIRT_VOR_FALLBACK_GROUP 2  // neighbour sites loaded together by the exact re-evaluation (<= kVorUnroll)
 #endif
@@ -207,7 +210,7 @@ constexpr int kVorCand = 4;  // possible winners the exact re-evaluation collect
 constexpr int kVorWideMax = SKIRT_VOR_WIDE;
 // slots after the last cell's block: a step loads whole groups of entries (kVorUnroll lane-serial, 16
 // for the first round of a neighbour-parallel step)
-constexpr int kVorPad = kVorUnroll > 16 ? kVorUnroll : 16;
+constexpr int kVorPad = 2 * kVorUnroll > 16 ? 2 * kVorUnroll : 16;
 
 // grid kinds of the kernels: SKIRT_GRID_CARTESIAN, SKIRT_GRID_OCTREE (leaf-map walk), the k-d tree
 // through its leaf map, and any tree walked through the node arrays (trees deeper than the leaf maps
@@ -1279,10 +1282,37 @@ struct Grid<SKIRT_GRID_VORONOI> {
     __device__ static __forceinline__ bool step(const Args& a, const Shared&, Ray& r, SegFn seg) {
         StepIn s;
         s.B = a.vorSlots + r.cj;
+        Best b{FLT_MAX, FLT_MAX, FLT_MAX, 0};
+#if SKIRT_VOR_PIPE
+        // two groups of entries in flight: the first two load with the header, and each group's next load
+        // is issued as soon as the group is consumed, so a cell with more than kVorUnroll neighbours does
+        // not wait for a second round trip
+        VorEntry e[kVorUnroll], f[kVorUnroll];
+        vorEntries(s.B, 0, e);
+        vorEntries(s.B, kVorUnroll, f);
+        if (!head(a, r, s, seg)) return false;
+        for (int q0 = 0; q0 < s.cnt; q0 += 2 * kVorUnroll) {
+#pragma unroll
+            for (int u = 0; u < kVorUnroll; u++) {
+                float lo, uc;
+                bounds(s, e[u], q0 + u < s.cnt, lo, uc);
+                take(b, lo, uc, e[u].next);
+            }
+            if (q0 + 2 * kVorUnroll < s.cnt) vorEntries(s.B, q0 + 2 * kVorUnroll, e);
+            if (q0 + kVorUnroll < s.cnt) {
+#pragma unroll
+                for (int u = 0; u < kVorUnroll; u++) {
+                    float lo, uc;
+                    bounds(s, f[u], q0 + kVorUnroll + u < s.cnt, lo, uc);
+                    take(b, lo, uc, f[u].next);
+                }
+                if (q0 + 3 * kVorUnroll < s.cnt) vorEntries(s.B, q0 + 3 * kVorUnroll, f);
+            }
+        }
+#else
         VorEntry e[kVorUnroll];
         vorEntries(s.B, 0, e);
         if (!head(a, r, s, seg)) return false;
-        Best b{FLT_MAX, FLT_MAX, FLT_MAX, 0};
         for (int q0 = 0; q0 < s.cnt; q0 += kVorUnroll) {
             if (q0) vorEntries(s.B, q0, e);
 #pragma unroll
@@ -1292,6 +1322,7 @@ struct Grid<SKIRT_GRID_VORONOI> {
                 take(b, lo, uc, e[u].next);
             }
         }
+#endif
         return decide(a, r, s, b, seg);
     }
 
