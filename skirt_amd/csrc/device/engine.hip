@@ -549,6 +549,7 @@ struct Grid<SKIRT_GRID_CARTESIAN> {
         r.ci = locateClip(xv, a.nx + 1, x);
         r.cj = locateClip(yv, a.ny + 1, y);
         r.ck = locateClip(zv, a.nz + 1, z);
+        r.rho0 = a.rho[(size_t)dev(a, r.ci, r.cj, r.ck) * a.ncomp];
         return true;
     }
 
@@ -570,7 +571,7 @@ struct Grid<SKIRT_GRID_CARTESIAN> {
         const double* zv = yv + a.ny + 1;
         const int i = r.ci, j = r.cj, k = r.ck;
         const int m = dev(a, i, j, k);
-        const double rho0 = a.rho[(size_t)m * a.ncomp];
+        const double rho0 = r.rho0;  // loaded by the previous step (or begin), off this step's chain
         const double xE = (r.dx < 0.0) ? xv[i] : xv[i + 1];
         const double yE = (r.dy < 0.0) ? yv[j] : yv[j + 1];
         const double zE = (r.dz < 0.0) ? zv[k] : zv[k + 1];
@@ -590,6 +591,7 @@ struct Grid<SKIRT_GRID_CARTESIAN> {
         const int nk = k + (ez ? ((r.dz < 0.0) ? -1 : 1) : 0);
         if (ni >= a.nx || ni < 0 || nj >= a.ny || nj < 0 || nk >= a.nz || nk < 0) return false;
         r.ci = ni; r.cj = nj; r.ck = nk;
+        r.rho0 = a.rho[(size_t)dev(a, ni, nj, nk) * a.ncomp];  // the next step's density, requested now
         r.x = ex ? xE : r.x + r.dx * ds;
         r.y = ey ? yE : r.y + r.dy * ds;
         r.z = ez ? zE : r.z + r.dz * ds;
