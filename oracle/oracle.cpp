@@ -497,8 +497,29 @@ struct Tallies {
     // paths per number of segments (cells crossed, including those outside the grid), last bin = overflow
     std::atomic<uint64_t> segFill{0}, segPeel{0}, absorbs{0};
     std::vector<uint64_t> crossed = std::vector<uint64_t>(kCrossedBins, 0);
-    void cross(size_t n) { __atomic_fetch_add(&crossed[std::min(n, crossed.size() - 1)], 1, __ATOMIC_RELAXED); }
 };
+
+// The counts above, kept per thread while a phase runs and added to the Tallies when the thread ends: a
+// shared atomic per path or per absorbing segment would serialize the worker threads (the CPU baseline
+// of bench.py runs on this code).
+struct Counts {
+    uint64_t segments = 0, segFill = 0, segPeel = 0, absorbs = 0;
+    std::vector<uint64_t> crossed = std::vector<uint64_t>(kCrossedBins, 0);
+    void cross(size_t n) { crossed[std::min(n, crossed.size() - 1)]++; }
+    void mergeInto(Tallies& t) const {
+        t.segments.fetch_add(segments);
+        t.segFill.fetch_add(segFill);
+        t.segPeel.fetch_add(segPeel);
+        t.absorbs.fetch_add(absorbs);
+        for (size_t i = 0; i < crossed.size(); i++)
+            if (crossed[i]) __atomic_fetch_add(&t.crossed[i], crossed[i], __ATOMIC_RELAXED);
+    }
+};
+thread_local Counts* tCounts = nullptr;
+inline Counts& counts() {
+    static thread_local Counts spare;  // calls outside a phase (none on the hot path)
+    return tCounts ? *tCounts : spare;
+}
 
 class Sim {
 public:
@@ -544,9 +565,10 @@ public:
         if (M.hasDust) {
             Vec3 ko{ins.kobs[0], ins.kobs[1], ins.kobs[2]};
             path(pp.r, ko, tmp);
-            t.segments.fetch_add(tmp.v.size(), std::memory_order_relaxed);
-            t.segPeel.fetch_add(tmp.v.size(), std::memory_order_relaxed);
-            t.cross(tmp.v.size());
+            Counts& c = counts();
+            c.segments += tmp.v.size();
+            c.segPeel += tmp.v.size();
+            c.cross(tmp.v.size());
             for (auto& s : tmp.v) taupath += M.kapparho(s.m, ell) * s.ds;
         }
         double extf = exp(-taupath);
@@ -635,9 +657,10 @@ public:
         while (true) {
             // DustSystem::fillOpticalDepth
             path(pp.r, pp.k, p);
-            t.segments.fetch_add(p.v.size(), std::memory_order_relaxed);
-            t.segFill.fetch_add(p.v.size(), std::memory_order_relaxed);
-            t.cross(p.v.size());
+            Counts& c = counts();
+            c.segments += p.v.size();
+            c.segFill += p.v.size();
+            c.cross(p.v.size());
             double tau = 0;
             for (auto& s : p.v) {
                 double dtau = M.kapparho(s.m, pp.ell) * s.ds;
@@ -667,7 +690,7 @@ public:
                             att = att * (1.0 - expfactorm);
                             double Labsm = (1.0 - albedo) * Lintm;
                             t.add(*labs, (size_t)m * Nl + pp.ell, Labsm);
-                            t.absorbs.fetch_add(1, std::memory_order_relaxed);
+                            counts().absorbs++;
                         }
                     }
                 }
@@ -694,7 +717,7 @@ public:
                         Lsca += albedo * Lintm;
                         if (store) {
                             t.add(*labs, (size_t)m * Nl + pp.ell, (1.0 - albedo) * Lintm);
-                            t.absorbs.fetch_add(1, std::memory_order_relaxed);
+                            counts().absorbs++;
                         }
                     }
                 }
@@ -1004,7 +1027,11 @@ OracleRun* oracle_run_shard(const char* ski, const char* datadir, int rngKind, i
                 Path p, tmp;
                 p.v.reserve(1024);
                 tmp.v.reserve(1024);
+                Counts c;
+                tCounts = &c;
                 for (uint64_t pk = pb; pk < pe; pk++) shoot(ph, tl, mtr, pk, p, tmp, run->packets);
+                tCounts = nullptr;
+                c.mergeInto(tl);
                 return;
             }
             int T = std::max(1, nthreads);
@@ -1016,6 +1043,13 @@ OracleRun* oracle_run_shard(const char* ski, const char* datadir, int rngKind, i
             std::vector<uint64_t> cnt(T, 0);
             for (int w = 0; w < T; w++) {
                 th.emplace_back([&, w] {
+                    Counts c;
+                    tCounts = &c;
+                    struct Merge {  // on every exit of the worker
+                        Counts& c;
+                        Tallies& t;
+                        ~Merge() { tCounts = nullptr; c.mergeInto(t); }
+                    } merge{c, tl};
                     try {
                         PhiloxRng rng(theSeed, ph.tag);
                         Path p, tmp;
