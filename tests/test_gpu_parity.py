@@ -390,3 +390,38 @@ def test_benchmark_models_match_oracle_same_streams(config, packages):
     np.testing.assert_allclose(seds, orc.seds[0], rtol=rtol, atol=1e-300)
     np.testing.assert_allclose(frames.sum(axis=2), orc.frames[0].sum(axis=2), rtol=rtol, atol=1e-300)
     assert_parity(frames, orc.frames[0], rtol, DUST_OUTLIERS if dust else STELLAR_OUTLIERS, "frames")
+
+
+def test_continuous_scattering_with_several_instruments(tmp_path):
+    """Continuous scattering queues kPathCap peel-offs per instrument and slot, so the slot pool shrinks with
+    the instrument count. pan_oct_cs with a FullInstrument, an SEDInstrument and a
+    FrameInstrument whose field leaves part of the grid outside (its peel-offs from there are skipped):
+    all phases, every instrument against the oracle on the same streams."""
+    text = open(ski("pan_oct_cs")).read()
+    full = text.index("<FullInstrument")
+    end = text.index("/>", full) + 2
+    extra = ('\n            <SEDInstrument instrumentName="i0" distance="10 Mpc" inclination="0 deg" azimuth="0 deg"/>'
+             '\n            <FrameInstrument instrumentName="f60" distance="10 Mpc" inclination="60 deg" azimuth="-30 deg"'
+             ' positionAngle="0 deg" fieldOfViewX="400 pc" pixelsX="16" centerX="50 pc" fieldOfViewY="400 pc"'
+             ' pixelsY="16" centerY="0 pc"/>')
+    path = os.path.join(tmp_path, "pan_oct_cs3.ski")
+    with open(path, "w") as f:
+        f.write(text[:end] + extra + text[end:])
+    packages = 200
+    sim = S.Simulation(path, packages=packages)
+    assert sim.info.ninstruments == 3
+    sim.attach(0)
+    sim.run_stellar()
+    sim.run_dust()
+    sim.fetch()
+    orc = O.run(path, rng=O.RNG_PHILOX, threads=16, packages=packages, phases=O.PHASES_ALL)
+    assert_parity(sim.labs(), orc.labs, 1e-9, STELLAR_OUTLIERS, "labs")
+    for i in range(3):
+        frames, seds = sim.instrument(i)
+        assert (seds is None) == (orc.seds[i] is None) and (frames is None) == (orc.frames[i] is None)
+        if seds is not None:  # (a FrameInstrument has no SED)
+            assert seds.sum() > 0
+            np.testing.assert_allclose(seds, orc.seds[i], rtol=1e-8, atol=1e-300)
+        if frames is not None:  # (an SEDInstrument has no frame)
+            assert frames.sum() > 0
+            assert_parity(frames, orc.frames[i], 1e-8, DUST_OUTLIERS, "frames_%d" % i)
