@@ -474,7 +474,7 @@ inline void lockFreeAdd(double* p, double v) {
 
 constexpr size_t kCrossedBins = 1 << 16;
 
-// Test switch (oracle_set_engine_attenuation): exp(-tau_{n-1}) of the absorption sum as the GPU engine
+// Test switch (oracle_set_engine_attenuation): exp(-tau_{n-1}) of the absorption sum as the GPU engine did until round 3
 // carries it, the running product of 1 - (-expm1(-dtau)) over the path's dust segments, instead of the
 // reference's exp(-taustart) per segment (MonteCarloSimulation.cpp:458-462). The two part in the last digits
 // only behind optically thick segments, where 1 - (1 - exp(-dtau)) cancels; tests/test_gpu_parity.py uses

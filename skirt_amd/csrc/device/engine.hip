@@ -192,9 +192,16 @@ __device__ __forceinline__ void vorEntries(const VorEntry* B, int q0, VorEntry (
     }
 }
 #ifndef SKIRT_VOR_UNROLL
-#define SKIRT_VOR_UNROLL 6  // entries per load group, even (pairs); two groups in flight: C4 7.44e7 pkt/s, 8: 7.03e7 (spills), 4: 7.36e7; one group of 8: 7.33e7 (profiles/r03_vor_pipe.txt)
+#define SKIRT_VOR_UNROLL 4  // entries per load group, even (pairs), two groups in flight; with exp(-tau) per FILL segment 4 is best (C4 7.30e7; 6: 7.26e7 with 28 B/lane spilled; one group of 8: 7.25e7), without it 6 was (profiles/r03_vor_pipe.txt, r03_exact_attenuation.txt)
 #endif
 constexpr int kVorUnroll = SKIRT_VOR_UNROLL;
+#ifndef SKIRT_LABS_SMOOTH
+#define SKIRT_LABS_SMOOTH 1  // Labs adds leave one wave instruction per grid step (Tracer::drainStep)
+#endif
+constexpr bool kLabsSmooth = SKIRT_LABS_SMOOTH;
+#ifndef SKIRT_EXACT_ATTENUATION
+#define SKIRT_EXACT_ATTENUATION 1  // exp(-tau) per FILL segment, as the reference (0: the running product)
+#endif
 #ifndef SKIRT_VOR_PIPE
 #define SKIRT_VOR_PIPE 1  // two groups of entries in flight per step (see Grid<SKIRT_GRID_VORONOI>::step)
 #endif
@@ -1436,6 +1443,7 @@ struct Tracer {
     double* pendVal;    // LDS, [kLabsBuf][kBlock]
     unsigned* pendIdx;  // LDS, [kLabsBuf][kBlock]
     int npend = 0;
+    unsigned gstep = 0;  // grid steps of the wave (drainStep's round robin)
 
     __device__ __forceinline__ void drain() {
         static_assert(kLabsBuf >= 2 && kLabsBuf <= 64 && (kLabsBuf & (kLabsBuf - 1)) == 0, "kLabsBuf: power of 2");
@@ -1479,27 +1487,46 @@ struct Tracer {
         }
 #endif
 #pragma unroll
-        for (int i = 0; i < kLabsBuf; i++) {
-            const int src = G * i + lane / kLabsBuf;
-            const int n = __shfl(npend, src);
-            const int q = j * kBlock + wbase + src;
-            const unsigned idx = pendIdx[q];
-            // the requests of this instruction: a lane starts one unless the lane before it (the same
-            // ray's previous add) hit the same 64-byte line
-            const unsigned line = (unsigned)(reinterpret_cast<size_t>(a.labs + idx) >> 6);
-            const unsigned prev = __shfl(line, lane - 1);
-            const unsigned long long starts = __ballot(j < n && (j == 0 || prev != line));
-            absorbs += (unsigned)__popcll(__ballot(j < n));
+        for (int i = 0; i < kLabsBuf; i++) issue(i);
+        npend = 0;
+    }
+
+    // wave instruction i of a drain: the buffered adds of lanes G i .. G i + G - 1 (G = 64 / kLabsBuf),
+    // kLabsBuf consecutive adds of each, transposed onto the wave's lanes
+    __device__ __forceinline__ void issue(int i) {
+        constexpr int G = 64 / kLabsBuf;
+        const int lane = threadIdx.x & 63;
+        const int wbase = threadIdx.x - lane;
+        const int j = lane & (kLabsBuf - 1);
+        const int src = G * i + lane / kLabsBuf;
+        const int n = __shfl(npend, src);
+        const int q = j * kBlock + wbase + src;
+        const unsigned idx = pendIdx[q];
+        // the requests of this instruction: a lane starts one unless the lane before it (the same
+        // ray's previous add) hit the same 64-byte line
+        const unsigned line = (unsigned)(reinterpret_cast<size_t>(a.labs + idx) >> 6);
+        const unsigned prev = __shfl(line, lane - 1);
+        const unsigned long long starts = __ballot(j < n && (j == 0 || prev != line));
+        absorbs += (unsigned)__popcll(__ballot(j < n));
 #ifndef SKIRT_EXPERIMENT_LINE_COUNT
-            requests += (unsigned)__popcll(starts);
+        requests += (unsigned)__popcll(starts);
 #endif
 #ifdef SKIRT_EXPERIMENT_NO_LABS_ATOMICS  // tuning experiment only: the cost of the Labs atomics
-            if (j < n && pendVal[q] == -1.0) atomicAddF64(a.labs + idx, pendVal[q]);
+        if (j < n && pendVal[q] == -1.0) atomicAddF64(a.labs + idx, pendVal[q]);
 #else
-            if (j < n) atomicAddF64(a.labs + idx, pendVal[q]);
+        if (j < n) atomicAddF64(a.labs + idx, pendVal[q]);
 #endif
-        }
-        npend = 0;
+    }
+
+    // One drain instruction per grid step, round robin over the lane groups: every lane's buffer is
+    // emptied every kLabsBuf steps, which holds its at most kLabsBuf adds (one per step), and the adds
+    // leave as a steady stream instead of a burst of kLabsBuf instructions (which stalls the issuing
+    // wave behind its outstanding atomics and reaches the memory-side atomic units in clumps).
+    __device__ __forceinline__ void drainStep() {
+        constexpr int G = 64 / kLabsBuf;
+        const int i = (int)(gstep++ & (kLabsBuf - 1));
+        issue(i);
+        if (((threadIdx.x & 63) / G) == i) npend = 0;
     }
 
     __device__ __forceinline__ double rho(int m, int h) const { return a.rho[(size_t)m * a.ncomp + h]; }
@@ -1524,20 +1551,25 @@ struct Tracer {
                 atomicOr(a.error, ERR_PATH_CAP);
             }
         }
+        const double taustart = r.tau;
         r.s += ds;
         r.tau += dtau;
         nseg++;
         if (r.mode == RAY_FILL) {
             if (m >= 0 && (!ONECOMP || a.store)) {
-                // L_abs = (1-albedo) L exp(-tau_{n-1}) (1 - exp(-dtau_n)) (MonteCarloSimulation.cpp:458-462);
-                // exp(-tau_{n-1}) is carried in f1 as the running product of 1 - (1 - exp(-dtau)). Behind an
-                // optically thick segment that product is exact only to about 1e-16 / exp(-dtau) relative
-                // (dtau = 30: 1.7e-4), where the reference evaluates exp(-tau) afresh: the named cause of the
-                // deep-cell differences on the thick pan_oct_sa models (tests/parity.py). Evaluating exp
-                // here instead costs the octree walk ~80 B/lane of register spills.
+                // L_abs = (1-albedo) L exp(-tau_{n-1}) (1 - exp(-dtau_n)) (MonteCarloSimulation.cpp:458-462),
+                // in the reference's operation order. (Rounds 1-3 carried exp(-tau_{n-1}) as the running
+                // product of 1 - (1 - exp(-dtau)), exact only to about 1e-16 / exp(-dtau) relative behind an
+                // optically thick segment: the deep-cell differences of the thick pan_oct_sa models. With
+                // the Labs adds leaving one instruction per step, exp fits the octree walk's registers.)
                 const double ef = -expm1(-dtau);
+#if SKIRT_EXACT_ATTENUATION
+                const double Lintm = r.param * exp(-taustart) * ef;
+#else
+                (void)taustart;
                 const double Lintm = r.param * r.f1 * ef;
                 r.f1 = r.f1 * (1.0 - ef);
+#endif
                 double albedo;
                 if (ONECOMP) albedo = sh.alb[r.ell];
                 else {
@@ -2008,8 +2040,12 @@ __device__ __forceinline__ void traceBody(const Args& a) {
                     r.mode = RAY_NONE;
                 }
             }
-            // a buffer without room for another step's adds: issue the wave's adds
-            if (__ballot(T.npend > kLabsBuf - kSegsPerStep<GRID>)) T.drain();
+            if constexpr (kLabsSmooth && kSegsPerStep<GRID> == 1) {
+                T.drainStep();  // one drain instruction per step
+            } else {
+                // a buffer without room for another step's adds: issue the wave's adds
+                if (__ballot(T.npend > kLabsBuf - kSegsPerStep<GRID>)) T.drain();
+            }
         }
     }
     T.drain();

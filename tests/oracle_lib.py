@@ -99,8 +99,8 @@ class OracleResult:
 
 
 class engine_attenuation:
-    """Context: the oracle evaluates the absorption's exp(-tau_{n-1}) as the engine's running product (see
-    oracle_set_engine_attenuation), to separate that arithmetic from everything else in a comparison."""
+    """Context: the oracle evaluates the absorption's exp(-tau_{n-1}) as a running product (the engine's form
+    until round 3, see oracle_set_engine_attenuation), to separate that arithmetic from everything else."""
 
     def __enter__(self):
         lib().oracle_set_engine_attenuation(1)

@@ -12,8 +12,7 @@ its luminosity between a few cells, so a same-stream comparison is judged by
 * the mass of both: the summed |a - b| over them, relative to the table's total, held to `mass`.
 
 Elements below `floor` x the table's maximum are not compared: in optically thick models the deepest cells
-receive ~1e-220 of a packet's luminosity, where the engine's running exp(-tau) and the oracle's exp(-tau)
-per segment underflow at different depths. Each report is appended to $SKIRT_PARITY_LOG (JSON lines) when
+receive ~1e-220 of a packet's luminosity, where device and host exp underflow at slightly different depths. Each report is appended to $SKIRT_PARITY_LOG (JSON lines) when
 that variable is set, so a GPU run leaves the measured outlier counts behind.
 """
 import json
@@ -22,22 +21,18 @@ import os
 import numpy as np
 
 # Outlier budgets of the same-stream tests: elements per table allowed beyond 100 x rtol (stellar phases
-# at rtol 1e-9, dust phases at 1e-8). Measured on MI355X (profiles/r02_parity_outliers.jsonl): no element
-# beyond rtol in any table of any fixture model; on the full C3 octree 2 of 67,011 cells at 1.1e-9
-# (drift). The stellar Labs of the optically thick (3e6 Msun) octree self-absorption models (pan_oct_sa,
-# pan_oct_sac) differ in 32 of 39,082 cells beyond 1e-7 and 67 more beyond 1e-9, largest relative
-# difference 4.5e-4, together 1.4e-19 of the total. Named cause (round 3), not a changed packet history:
-# the engine carries a path's exp(-tau_{n-1}) as the running product of 1 - (-expm1(-dtau)), the reference
-# evaluates exp(-taustart) per segment (MonteCarloSimulation.cpp:458-462); behind a segment of dtau = 30
-# the product keeps only 1e-16 / exp(-30) = 1.7e-4 relative accuracy, so the cells behind the thick centre
-# part in those digits. Proof: with the oracle switched to the engine's form (oracle_set_engine_attenuation)
-# the same GPU run has 0 outliers and 0 drift on these models (test_dust_phases_match_oracle_same_streams,
-# label labs_engine_attenuation), and the oracle against itself in the two forms reproduces the differences
-# on the CPU (tests/test_attenuation.py). THICK_OUTLIERS bounds that cause; evaluating exp per segment in
-# the engine instead would cost the octree walk ~80 B/lane of register spills.
+# at rtol 1e-9, dust phases at 1e-8). Measured on MI355X (profiles/r02_parity_outliers.jsonl,
+# profiles/r03_gpu_tests_full.log): no element beyond rtol in any table of any fixture model; on the full C3
+# octree 2 of 67,011 cells at 1.1e-9 (drift). Until round 3 the stellar Labs of the optically thick (3e6
+# Msun) octree self-absorption models (pan_oct_sa, pan_oct_sac) differed in 32 of 39,082 cells beyond 1e-7
+# (largest 4.5e-4, together 1.4e-19 of the total), with a budget of 128. Named cause: the engine carried a
+# path's exp(-tau_{n-1}) as the running product of 1 - (-expm1(-dtau)) where the reference evaluates
+# exp(-taustart) per segment (MonteCarloSimulation.cpp:458-462); behind a segment of dtau = 30 the product
+# keeps only 1e-16 / exp(-30) = 1.7e-4 relative accuracy (tests/test_attenuation.py shows it on the CPU).
+# The engine now evaluates exp(-taustart) per segment as the reference does, and those models have no
+# element beyond 1e-9 either: one budget for all.
 STELLAR_OUTLIERS = 0
 DUST_OUTLIERS = 0
-THICK_OUTLIERS = 128
 
 
 def outliers(a, b, rtol, floor=1e-15, drift=100.0):

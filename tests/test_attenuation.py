@@ -1,14 +1,15 @@
-"""The named cause of the engine's deep-cell differences on optically thick models (tests/parity.py).
+"""The named cause of the deep-cell differences the engine had on optically thick models until round 3
+(tests/parity.py).
 
 The reference sums a packet's absorption along a path with exp(-taustart) per segment
-(MonteCarloSimulation.cpp:458-462). The engine carries exp(-tau) as the running product of
+(MonteCarloSimulation.cpp:458-462). The engine carried exp(-tau) as the running product of
 1 - (-expm1(-dtau)) over the path. Both agree to a few ulp per factor while dtau is small. Behind an
 optically thick segment, 1 - (1 - exp(-dtau)) cancels: the product keeps only about 1e-16 / exp(-dtau) relative
-accuracy (dtau = 30: 1.7e-4). These tests reproduce that on the CPU, with the oracle switched to the engine's
-form (oracle_set_engine_attenuation). The differences it makes there match the GPU's (test_gpu_parity.py):
-a few tens of deep cells on the 3e6 Msun pan_oct_sa models, with a mass below 1e-18 of the table. The
-thin models show none. With the switch on, the engine equals the oracle on the thick models too
-(test_dust_phases_match_oracle_same_streams)."""
+accuracy (dtau = 30: 1.7e-4). These tests reproduce that on the CPU, with the oracle switched to the product
+form (oracle_set_engine_attenuation): a few tens of deep cells on the 3e6 Msun pan_oct_sa models, with a
+mass below 1e-18 of the table, as the GPU showed; the thin models show none. The engine now evaluates
+exp(-taustart) per segment (SKIRT_EXACT_ATTENUATION), and its thick-model Labs equal the oracle's to 1e-9
+with no outlier (test_dust_phases_match_oracle_same_streams)."""
 import os
 
 import numpy as np
