@@ -31,8 +31,11 @@ CONFIGS = {
     # name: (ski, packets per wavelength per rank, segment geometry bytes, description)
     # C3 is 4e7 packets per wavelength (1e9 in all) over 8 GPUs: 5e6 per wavelength per rank
     "c3": ("benchmarks/c3_oct128.ski", 5000000, 56, "C3 octree 128^3 (levels 3-7, mass fraction 1e-6), 25 lambda, peel-off"),
-    "c2": ("benchmarks/c2_cart64.ski", 1000000, 0, "C2 Cartesian 64^3, 10 lambda, peel-off"),
-    "c4": ("benchmarks/c4_vor1e5.ski", 200000, 438,
+    # C2 is 1e8 packets over 10 wavelengths on one GPU: 1e7 per wavelength (rounds 1-3 ran 1e6)
+    "c2": ("benchmarks/c2_cart64.ski", 10000000, 0, "C2 Cartesian 64^3, 10 lambda, peel-off"),
+    # C4 is 1e9 packets over 25 wavelengths on 8 GPUs, like C3: 5e6 per wavelength per rank (rounds 1-3
+    # ran 2e5, whose phase tail -- the last few long-lived packets -- then weighed 25x more per packet)
+    "c4": ("benchmarks/c4_vor1e5.ski", 5000000, 438,
            "C4 Voronoi 1e5 sites (DustDensity), 25 lambda, peel-off"),
     # C5 at its per-GPU share of the 1e9-packet configuration, like C3 (round 2 ran 4e5 per wavelength)
     "c5": ("benchmarks/c5_oct128_sa.ski", 5000000, 56,
