@@ -130,6 +130,11 @@ constexpr int kContSlots = 1 << 15;  // packet slots in flight with continuous s
 enum ErrorBits : unsigned { ERR_TAU = 1u, ERR_PATH_CAP = 2u, ERR_QUEUE = 4u };
 template <int GRID>
 constexpr bool kEnterInEvent = GRID == SKIRT_GRID_VORONOI;
+#ifndef SKIRT_CELLINDEX_GROUP
+#define SKIRT_CELLINDEX_GROUP 4
+#endif
+constexpr int kCellIndexGroup = SKIRT_CELLINDEX_GROUP;  // Voronoi cellIndex: block-list candidates per load round
+constexpr int kNoCell = -2;  // a cached cell index not known yet (-1 is a located point without a cell)
 // a ray entered by the event kernel carries the number of its segments before the grid in the top bits
 // of its first cell (Voronoi device cells < 2^28)
 constexpr int kOutsideShift = 28;
@@ -302,6 +307,7 @@ struct Args {
     int nslots;
     double *srx, *sry, *srz, *skx, *sky, *skz, *sL, *sLth;
     int *sell, *snscatt, *sstellar, *sstate;
+    int* svcell;                 // Voronoi: the cell of the packet's position (cellIndex), kNoCell if not known
     uint32_t *splo, *sphi, *sblock, *sw2, *sw3, *shave;
     double *resA, *resB;         // per slot: FILL -> tau, Lsca | WALK -> distance
     RayRec* rays;
@@ -1060,20 +1066,53 @@ struct Grid<SKIRT_GRID_VORONOI> {
         const int b = i * nb * nb + j * nb + k;
         int m = -1;
         double best = kDblMax;
-        for (int q = a.blockOffset[b]; q < a.blockOffset[b + 1]; q++) {
-            const int c = a.blockList[q];
-            const double dx = x - a.site[3 * c], dy = y - a.site[3 * c + 1], dz = z - a.site[3 * c + 2];
-            const double d = dx * dx + dy * dy + dz * dz;
-            if (d < best) { best = d; m = c; }
+        // the list in groups of kCellIndexGroup: the group's list entries, then its sites, load together (one
+        // round trip each instead of two per candidate); the candidates are then taken in list order, so the
+        // first of equal distances wins as in the reference's loop
+        constexpr int G = kCellIndexGroup;
+        const int qe = a.blockOffset[b + 1];
+        for (int q0 = a.blockOffset[b]; q0 < qe; q0 += G) {
+            int c[G];
+            double sx[G], sy[G], sz[G];
+#pragma unroll
+            for (int u = 0; u < G; u++) c[u] = q0 + u < qe ? a.blockList[q0 + u] : -1;
+#pragma unroll
+            for (int u = 0; u < G; u++) {
+                sx[u] = sy[u] = sz[u] = 0.0;
+                if (c[u] >= 0) { sx[u] = a.site[3 * c[u]]; sy[u] = a.site[3 * c[u] + 1]; sz[u] = a.site[3 * c[u] + 2]; }
+            }
+#pragma unroll
+            for (int u = 0; u < G; u++) {
+                const double dx = x - sx[u], dy = y - sy[u], dz = z - sz[u];
+                const double d = dx * dx + dy * dy + dz * dz;
+                if (c[u] >= 0 && d < best) { best = d; m = c[u]; }
+            }
         }
         return m;
     }
 
     template <class SegFn>
     __device__ static __forceinline__ bool begin(const Args& a, const Shared&, Ray& r, SegFn seg) {
+        int none = kNoCell;
+        return beginAt(a, r, none, seg);
+    }
+
+    // begin() with the cell of the ray's origin cached in `cell` (kNoCell: not known yet). A point strictly
+    // inside the grid enters where it is, whatever the direction (enterGrid moves nothing), so its cellIndex
+    // serves every ray from that position: the peel-offs and the FILL ray of one event, and the WALK ray
+    // that retraces the FILL ray's path in the next one. A point on or outside the grid's faces enters
+    // where its direction takes it, so it is located per ray and not cached.
+    template <class SegFn>
+    __device__ static __forceinline__ bool beginAt(const Args& a, Ray& r, int& cell, SegFn seg) {
         double rx = r.x, ry = r.y, rz = r.z, d[3];
+        const bool strict = rx > a.gx0 && rx < a.gx1 && ry > a.gy0 && ry < a.gy1 && rz > a.gz0 && rz < a.gz1;
         if (!Grid<kOctreeNodes>::enterGrid(a, rx, ry, rz, r.dx, r.dy, r.dz, d)) return false;
-        const int m = cellIndex(a, rx, ry, rz);
+        int m;
+        if (strict && cell != kNoCell) m = cell;
+        else {
+            m = cellIndex(a, rx, ry, rz);
+            if (strict) cell = m;
+        }
         if (m < 0) return false;
         for (int q = 0; q < 3; q++)
             if (d[q] > 0) seg(-1, 0.0, d[q]);
@@ -2155,7 +2194,7 @@ struct Events {
     // cellIndex loops over a block's site list, which costs the trace kernel more than it costs here. A
     // path found empty here (no dust system, or a Voronoi ray missing the grid) is finished here.
     __device__ __forceinline__ void emitRay(unsigned pos, const Packet& p, double dx, double dy, double dz, double prm,
-                                            int idx, unsigned flags) {
+                                            int idx, unsigned flags, int& vcell) {
         Ray r;
         r.x = p.rx; r.y = p.ry; r.z = p.rz;
         r.dx = dx; r.dy = dy; r.dz = dz;
@@ -2168,8 +2207,8 @@ struct Events {
         int4* dst = reinterpret_cast<int4*>(a.rays + pos);
         bool entered = a.hasDust;
         unsigned nseg = 0;
-        if (kEnterInEvent<GRID> && entered) {
-            entered = Grid<GRID>::begin(a, sh, r, [&](int, double, double ds) {
+        if constexpr (kEnterInEvent<GRID>) {
+            if (entered) entered = Grid<GRID>::beginAt(a, r, vcell, [&](int, double, double ds) {
                 if (ds > 0) { r.s += ds; nseg++; }  // outside the grid: no optical depth
                 return true;
             });
@@ -2672,10 +2711,12 @@ __global__ void __launch_bounds__(kBlock) SKIRT_EVENT_ATTR eventKernel(const Arg
         Packet p;
         p.state = S_NEW;
         double resA = 0.0, resB = 0.0;
+        int vcell = kNoCell;  // Voronoi: the cell of the packet's position, while it stays there
         if (valid && !a.init) {
             E.load(slot, p);
             resA = a.resA[slot];
             if (!ONECOMP) resB = a.resB[slot];
+            if (kEnterInEvent<GRID>) vcell = a.svcell[slot];
         }
         int peel = PEEL_NONE;
         unsigned mainMode = RAY_NONE;
@@ -2705,6 +2746,7 @@ __global__ void __launch_bounds__(kBlock) SKIRT_EVENT_ATTR eventKernel(const Arg
             if (p.state == S_WALK && mainMode == RAY_NONE) {
                 // propagate to the interaction point; peel-off round; scatter; next FILL
                 const double s = resA;
+                vcell = kNoCell;  // the packet moves
                 p.rx = p.rx + s * p.kx;
                 p.ry = p.ry + s * p.ky;
                 p.rz = p.rz + s * p.kz;
@@ -2732,6 +2774,7 @@ __global__ void __launch_bounds__(kBlock) SKIRT_EVENT_ATTR eventKernel(const Arg
             if (need) {
                 if (idx >= total) need = false;  // exhausted: the slot retires
                 else if (E.launch(p, globalPacket(a, a.first + idx))) {
+                    vcell = kNoCell;  // a new position
                     if (!(p.L > 0) && !a.crossed) {
                         // a zero-weight dust packet (a cell without emission drawn uniformly): every
                         // tally it would touch receives 0, so it ends here -- unless the cells-crossed
@@ -2819,11 +2862,12 @@ __global__ void __launch_bounds__(kBlock) SKIRT_EVENT_ATTR eventKernel(const Arg
                 idx = slot;
                 flags = mainMode | ((unsigned)p.ell << 18);
             }
-            E.emitRay(pos++, p, dx, dy, dz, prm, idx, flags);
+            E.emitRay(pos++, p, dx, dy, dz, prm, idx, flags, vcell);
         }
         // the slot stays active while it has a FILL/WALK ray in flight
         if (active) actOut[apos] = slot;
         if (valid) E.store(slot, p);
+        if (kEnterInEvent<GRID> && valid) a.svcell[slot] = vcell;
 #ifdef SKIRT_EXPERIMENT_TIMELINE
         tlPart[3] += stamp() - ts3;
 #endif
@@ -2912,6 +2956,7 @@ __global__ void __launch_bounds__(kBlock) contKernel(const Args a) {
                 const double s = rec[n].s0 + rng.uniform() * rec[n].ds;
                 Packet q = p;
                 q.rx = p.rx + s * p.kx; q.ry = p.ry + s * p.ky; q.rz = p.rz + s * p.kz;
+                int qcell = kNoCell;  // the point's cell (Voronoi), located once for all instruments
                 for (int i = 0; i < a.ninstr; i++) {
                     const DevInstr& ins = sh.instr[i];
                     const int l = ins.kind == SKIRT_INSTR_SED ? -1 : E.pixel(ins, q);
@@ -2930,7 +2975,7 @@ __global__ void __launch_bounds__(kBlock) contKernel(const Args a) {
                     const unsigned level = (unsigned)min(p.nscatt + 1, 255);
                     const unsigned flags = RAY_PEEL | (cat << 2) | ((unsigned)i << 4) | (level << 10) | ((unsigned)p.ell << 18);
                     a.det[dpos] = DetRec{Lp, 0.0, l, flags};
-                    E.emitRay(pos++, q, ins.kobs[0], ins.kobs[1], ins.kobs[2], Lp, (int)dpos, flags);
+                    E.emitRay(pos++, q, ins.kobs[0], ins.kobs[1], ins.kobs[2], Lp, (int)dpos, flags, qcell);
                     dpos++;
                 }
             }
@@ -3083,7 +3128,7 @@ int ensurePool(SkirtMcrt* c, int nslots, bool continuous, int halves) {
     const int rayCap = (int)rays;
     const size_t path = continuous ? (size_t)nslots * (kPathCap * sizeof(PathRec) + sizeof(int)) : 0;
     const size_t half = (size_t)rayCap * sizeof(RayRec) + (size_t)(rayCap - nslots) * sizeof(DetRec) +
-                        (size_t)nslots * (10 * 8 + 4 * 4 + 6 * 4 + 2 * 4) + path + 4096;
+                        (size_t)nslots * (10 * 8 + 5 * 4 + 6 * 4 + 2 * 4) + path + 4096;
     if (c->dPool && c->nslots == nslots && c->rayCap == rayCap && c->poolPath == (path > 0) && c->poolHalves == halves)
         return SKIRT_OK;
     c->poolPath = path > 0;
@@ -3149,7 +3194,7 @@ void carvePool(SkirtMcrt* c, Args& a, int h) {
     p += (size_t)(c->rayCap - c->nslots) * sizeof(DetRec);
     takeD(a.srx); takeD(a.sry); takeD(a.srz); takeD(a.skx); takeD(a.sky); takeD(a.skz); takeD(a.sL); takeD(a.sLth);
     takeD(a.resA); takeD(a.resB);
-    takeI(a.sell); takeI(a.snscatt); takeI(a.sstellar); takeI(a.sstate);
+    takeI(a.sell); takeI(a.snscatt); takeI(a.sstellar); takeI(a.sstate); takeI(a.svcell);
     takeU(a.splo); takeU(a.sphi); takeU(a.sblock); takeU(a.sw2); takeU(a.sw3); takeU(a.shave);
     takeI(a.act[0]); takeI(a.act[1]);
     a.pathBuf = nullptr;
