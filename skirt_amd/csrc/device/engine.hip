@@ -1174,16 +1174,15 @@ struct Grid<SKIRT_GRID_VORONOI> {
     // so every entry takes the same branch-free arithmetic; lo = hi = FLT_MAX: certainly no exit.
     __device__ static __forceinline__ void bounds(const StepIn& s, const VorEntry& en, bool valid, float& lo,
                                                   float& ucand) {
-        // the plane distance s = (n.D + |n|^2/2) / (n.k) with Cauchy-Schwarz error terms: |d(n.k)| <= eA
-        // and |d(n.D + |n|^2/2)| <= eB = eA |D|_1 + kVorEpsF |n|^2, at the cell's largest |n|_1 and |n|^2
-        // (vor_terms.hpp; several times the float roundings of the offsets, D, k and the fused
-        // operations). 33 operations per entry (per-entry terms: 38; round 2's sums of the absolute
-        // terms of each product: 55); tools/vor_compact_check.cpp, mode d, checks the resulting steps
-        // against the reference's.
-        const float nx = en.ox, ny = en.oy, nz = en.oz;
-        const float n2 = fmaf(nz, nz, fmaf(ny, ny, nx * nx));
-        const float den = fmaf(nz, s.fkz, fmaf(ny, s.fky, nx * s.fkx));
-        const float num = fmaf(n2, 0.5f, fmaf(nz, s.Dz, fmaf(ny, s.Dy, nx * s.Dx)));
+        // the plane distance s = (n.D + |n|^2/2) / (n.k) = (m.D + 1/2) / (m.k) with m = n / |n|^2, the stored
+        // entry, and Cauchy-Schwarz error terms: |d(m.k)| <= eA and |d(m.D + 1/2)| <= eB = eA |D|_1 + kVorEpsF/2,
+        // at the cell's largest |m|_1 (vor_terms.hpp; several times the float roundings of the entries, D, k
+        // and the fused operations). 29 operations per entry (with n stored: 33; per-entry terms: 38; round
+        // 2's sums of the absolute terms of each product: 55); tools/vor_compact_check.cpp, mode r, checks
+        // the resulting steps against the reference's.
+        const float mx = en.ox, my = en.oy, mz = en.oz;  // m = n / |n|^2 (vor_terms.hpp)
+        const float den = fmaf(mz, s.fkz, fmaf(my, s.fky, mx * s.fkx));
+        const float num = fmaf(mz, s.Dz, fmaf(my, s.Dy, fmaf(mx, s.Dx, 0.5f)));
         const float inv = __builtin_amdgcn_rcpf(den);
         const float sa = num * inv;
         const float err = fmaf(fmaf(fabsf(sa), s.eA2, s.eB2), inv, fabsf(sa) * kVorEpsF);
@@ -3695,13 +3694,17 @@ int skirt_mcrt_upload_grid(SkirtMcrt* c, const SkirtGridDesc* g) {
                     const int axis = (-id - 1) / 2;
                     const double lim[6] = {c->gx0, c->gx1, c->gy0, c->gy1, c->gz0, c->gz1};
                     const double w = lim[-id - 1] - sm[axis];
-                    float o[3] = {0.f, 0.f, 0.f};
-                    o[axis] = w != 0.0 ? (float)(2.0 * w * c->vorScale) : NAN;
+                    double n[3] = {0.0, 0.0, 0.0};
+                    n[axis] = w != 0.0 ? 2.0 * w * c->vorScale : NAN;
+                    float o[3];
+                    vorRecipOffset(n[0], n[1], n[2], o);  // m = n / |n|^2 (vor_terms.hpp)
                     e = VorEntry{o[0], o[1], o[2], id};
                 } else {
                     const double* si = g->site + 3 * (size_t)id;
-                    e = VorEntry{(float)((si[0] - sm[0]) * c->vorScale), (float)((si[1] - sm[1]) * c->vorScale),
-                                 (float)((si[2] - sm[2]) * c->vorScale), start[c->devCell[id]]};
+                    float o[3];
+                    vorRecipOffset((si[0] - sm[0]) * c->vorScale, (si[1] - sm[1]) * c->vorScale,
+                                   (si[2] - sm[2]) * c->vorScale, o);
+                    e = VorEntry{o[0], o[1], o[2], start[c->devCell[id]]};
                 }
                 // entry o in its pair (see VorEntry): {ox0, ox1, oy0, oy1} {oz0, oz1, next0, next1}
                 float* P = reinterpret_cast<float*>(blk + kVorHead + (o & ~1));
@@ -3712,7 +3715,7 @@ int skirt_mcrt_upload_grid(SkirtMcrt* c, const SkirtGridDesc* g) {
             }
             // the header's last words: id, count and the cell's error terms of the bounds (vor_terms.hpp)
             float eA, eB;
-            vorErrorTerms(off.data(), cnt, 3, &eA, &eB);
+            vorRecipErrorTerms(off.data(), cnt, 3, &eA, &eB);
             int ids[4] = {d, cnt, 0, 0};
             std::memcpy(&ids[2], &eA, 4);
             std::memcpy(&ids[3], &eB, 4);

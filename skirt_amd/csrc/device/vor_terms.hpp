@@ -1,4 +1,4 @@
-// The per-cell error terms of the compact Voronoi step's single-precision bounds
+// The stored neighbour entries and per-cell error terms of the compact Voronoi step's single-precision bounds
 // (engine.hip, Grid<SKIRT_GRID_VORONOI>::bounds), shared by the engine's Voronoi upload and the host
 // exactness check (tools/vor_compact_check.cpp).
 //
@@ -26,4 +26,33 @@ inline void vorErrorTerms(const float* off, int n, int stride, float* eA, float*
     }
     *eA = std::nextafter((float)(kVorEpsF * a), INFINITY);
     *eB = std::nextafter((float)(kVorEpsF * b), INFINITY);
+}
+
+// Round 3 (final): the entries hold m = n / |n|^2 instead of n. The plane distance
+// s = (n.D + |n|^2/2) / (n.k), numerator and denominator divided by |n|^2, is s = (m.D + 1/2) / (m.k):
+// no |n|^2 to form per entry. Rounding m to float errs by 2^-24 |m_i| per component, as rounding n did, so
+// the same Cauchy-Schwarz terms hold with m in place of n and the constant 1/2 in place of |n|^2/2:
+// eA = kVorEpsF max |m|_1 and eB = kVorEpsF / 2 (the numerator's error <= eA |D|_1 + eB).
+// n: the scaled offset in double; out: m in float, NaN for a degenerate offset (the step then evaluates
+// the cell's list exactly).
+inline void vorRecipOffset(double nx, double ny, double nz, float out[3]) {
+    const double q = nx * nx + ny * ny + nz * nz;
+    if (!(q > 0.0) || !std::isfinite(q)) {
+        out[0] = out[1] = out[2] = NAN;
+        return;
+    }
+    out[0] = (float)(nx / q);
+    out[1] = (float)(ny / q);
+    out[2] = (float)(nz / q);
+}
+
+inline void vorRecipErrorTerms(const float* off, int n, int stride, float* eA, float* eB) {
+    double a = 0.0;
+    for (int q = 0; q < n; q++) {
+        const double x = off[(long)q * stride], y = off[(long)q * stride + 1], z = off[(long)q * stride + 2];
+        if (std::isnan(x) || std::isnan(y) || std::isnan(z)) continue;
+        a = std::fmax(a, std::fabs(x) + std::fabs(y) + std::fabs(z));
+    }
+    *eA = std::nextafter((float)(kVorEpsF * a), INFINITY);
+    *eB = std::nextafter((float)(kVorEpsF * 0.5), INFINITY);
 }

@@ -6,7 +6,8 @@
 // same cells and bitwise equal segment lengths. Reports how often the exact re-evaluation was needed.
 //   g++ -O2 -std=c++17 -ffp-contract=off -I include tools/vor_compact_check.cpp -L skirt_amd -lskirt_amd \
 //       -Wl,-rpath,$PWD/skirt_amd -o /tmp/vor_compact_check && /tmp/vor_compact_check 100000 20000 d
-// (mode d: the device's round-3 bounds; f / e / c: round-2 float variants; none: double bounds)
+// (mode r: the device's bounds on reciprocal entries m = n / |n|^2; d: round 3's bounds on the offsets n;
+// x: per-entry terms; f / e / c: round-2 float variants; none: double bounds)
 #include "../skirt_amd/csrc/device/vor_terms.hpp"
 #include <cfloat>
 #include <cmath>
@@ -70,6 +71,7 @@ float gScale = 1.0f;
 bool gCell = false, gEntry = false;  // per-cell / per-entry-norm error bounds instead of the round-2 device's
 bool gPerEntry = false;  // mode x: the first round-3 device step (per-entry terms)
 bool gDevice = false;                // the round-3 device step: per-entry Cauchy-Schwarz error terms
+bool gRecip = false;                 // mode r: the entries hold m = n / |n|^2 (the device's final step)
 long gSignFallbacks = 0;  // re-evaluations with an entry whose n.k sign is uncertain
 long gWholeList = 0;      // re-evaluations over the whole list (more than 4 possible winners)
 float gLo[4096];          // the step's lower bounds, per list entry
@@ -154,12 +156,15 @@ static int compactStepF(const Mesh& M, int m, const double r[3], const double k[
             const float Dn = fabsf(Dx) + fabsf(Dy) + fabsf(Dz);
             const float n2 = fmaf(nz, nz, fmaf(ny, ny, nx * nx));
             const float den = fmaf(nz, kz, fmaf(ny, ky, nx * kx));
-            const float num = fmaf(n2, 0.5f, fmaf(nz, Dz, fmaf(ny, Dy, nx * Dx)));
+            // mode r (engine.hip bounds()): (m.D + 1/2) / (m.k), the entries being m
+            const float num = gRecip ? fmaf(nz, Dz, fmaf(ny, Dy, fmaf(nx, Dx, 0.5f)))
+                                     : fmaf(n2, 0.5f, fmaf(nz, Dz, fmaf(ny, Dy, nx * Dx)));
             const float eA = gPerEntry ? kEpsF * (fabsf(nx) + fabsf(ny) + fabsf(nz)) : M.eA[m];
             const float eB = gPerEntry ? fmaf(eA, Dn, kEpsF * n2) : fmaf(eA, Dn, M.eB[m]);
             const float inv = 1.0f / den;
             const float sa = num * inv;
             const float err = fmaf(fmaf(fabsf(sa), 2.0f * eA, 2.0f * eB), inv, fabsf(sa) * kEpsF);
+            (void)n2;
             const float lov = sa - err, hiv = sa + err;
             const bool sure = den > 2.0f * eA;
             const bool maybe = !(den <= -eA);
@@ -235,8 +240,9 @@ int main(int argc, char** argv) {
     const double ext[6] = {-L, -L, -L, L, L, L};
     gScale = (float)(1.0 / L);
     const bool f32 = argc > 3 && (argv[3][0] == 'f' || argv[3][0] == 'c' || argv[3][0] == 'e' || argv[3][0] == 'd' ||
-                                  argv[3][0] == 'x');
-    gDevice = argc > 3 && (argv[3][0] == 'd' || argv[3][0] == 'x');
+                                  argv[3][0] == 'x' || argv[3][0] == 'r');
+    gDevice = argc > 3 && (argv[3][0] == 'd' || argv[3][0] == 'x' || argv[3][0] == 'r');
+    gRecip = argc > 3 && argv[3][0] == 'r';
     gPerEntry = argc > 3 && argv[3][0] == 'x';
     gCell = argc > 3 && argv[3][0] == 'c';
     gEntry = argc > 3 && argv[3][0] == 'e';
@@ -262,9 +268,17 @@ int main(int argc, char** argv) {
                 const double w = lim - sm[axis];
                 for (int d = 0; d < 3; d++) M.off[3 * (size_t)q + d] = 0.f;
                 M.off[3 * (size_t)q + axis] = w != 0.0 ? (float)(2.0 * w * gScale) : NAN;
+                if (gRecip) {  // as the engine's Voronoi upload: m = n / |n|^2 (vor_terms.hpp)
+                    double n[3] = {0.0, 0.0, 0.0};
+                    n[axis] = w != 0.0 ? 2.0 * w * gScale : NAN;
+                    vorRecipOffset(n[0], n[1], n[2], &M.off[3 * (size_t)q]);
+                }
                 continue;
             }
             for (int d = 0; d < 3; d++) M.off[3 * (size_t)q + d] = (float)((g.site[3 * (size_t)mi + d] - sm[d]) * gScale);
+            if (gRecip)
+                vorRecipOffset((g.site[3 * (size_t)mi] - sm[0]) * (double)gScale, (g.site[3 * (size_t)mi + 1] - sm[1]) * (double)gScale,
+                               (g.site[3 * (size_t)mi + 2] - sm[2]) * (double)gScale, &M.off[3 * (size_t)q]);
         }
     M.nmax.assign(N, 0.f);
     for (int m = 0; m < N; m++)
@@ -277,7 +291,8 @@ int main(int argc, char** argv) {
     M.eB.assign(N, 0.f);
     for (int m = 0; m < N; m++) {
         const int q0 = g.cell_nbr_offset[m], q1 = g.cell_nbr_offset[m + 1];
-        vorErrorTerms(M.off.data() + 3 * (size_t)q0, q1 - q0, 3, &M.eA[m], &M.eB[m]);
+        if (gRecip) vorRecipErrorTerms(M.off.data() + 3 * (size_t)q0, q1 - q0, 3, &M.eA[m], &M.eB[m]);
+        else vorErrorTerms(M.off.data() + 3 * (size_t)q0, q1 - q0, 3, &M.eA[m], &M.eB[m]);
     }
     long steps = 0, fallbacks = 0, mismatches = 0;
     for (int i = 0; i < R; i++) {
@@ -298,6 +313,7 @@ int main(int argc, char** argv) {
         }
     }
     printf("%s: sites %d, rays %d, steps %ld, exact re-evaluations %ld (%.3g per step), mismatches %ld\n",
+           gRecip ? "f32 device bounds on reciprocal entries m = n/|n|^2 (per-cell terms)" :
            gPerEntry ? "f32 per-entry Cauchy-Schwarz bounds (round 3, first)" :
            gDevice ? "f32 device bounds (per-cell Cauchy-Schwarz terms)" : gEntry ? "f32 per-entry norm bounds" : gCell ? "f32 per-cell bounds" : f32 ? "f32 bounds" : "f64 bounds", N, R, steps,
            fallbacks, (double)fallbacks / steps, mismatches);
