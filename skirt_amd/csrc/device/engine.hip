@@ -57,6 +57,7 @@ constexpr int kStepsPerPull = SKIRT_STEPS_PER_PULL;  // grid steps between two r
 // half's event and detect kernels run beside the other half's trace kernel, on CUs of their own (CU-masked
 // streams, see runPhase).
 constexpr int kMaxHalves = 2;
+constexpr int kCtrWords = 16;  // device counters per pipeline half (Args::ctr)
 constexpr int kSersicTable = 202;  // SersicFunction: 101 radii, then 101 cumulative masses
 constexpr int kDetectCopies = 8;   // most LDS copies of the SED sums in the detect kernel (one per 8 lanes)
 constexpr int kPollEvery = 1;      // iterations between two counter copies of a half
@@ -317,6 +318,7 @@ struct Args {
     unsigned int* ctr;           // [0,1] ray counts, [2,3] active counts, [4] trace pull counter,
                                  // [5,6] detection record counts
     int parity, init, threshold;
+    int walkBack;                // WALK rays queued from the top of the ray queue, so they are pulled last
     // continuous scattering: per slot the dust segments of its last FILL path and their number
     int continuous, rayCap;
     PathRec* pathBuf;            // [slot][kPathCap]
@@ -1989,8 +1991,13 @@ __device__ __forceinline__ void traceBody(const Args& a) {
         a.ctr[1 - a.parity] = 0;  // ray count of the next iteration
         a.ctr[5 + (1 - a.parity)] = 0;  // and its detection records (the last ones were detected already)
         a.ctr[2 + a.parity] = 0;  // active list just consumed by the event kernel
+        a.ctr[8 + (1 - a.parity)] = 0;  // the next iteration's WALK rays
     }
-    if (a.ctr[a.parity] == 0) return;  // an iteration after the end of the phase
+    // the iteration's rays: ctr[q] from the bottom of the queue, then the WALK rays ctr[8 + q] from its top
+    // (Args::walkBack), pulled last: the short WALK paths fill the lanes that the long FILL and peel-off
+    // paths free at the end of a launch, instead of idling until the launch's longest path ends
+    const unsigned int nfront = a.ctr[a.parity];
+    if (nfront + a.ctr[8 + a.parity] == 0) return;  // an iteration after the end of the phase
 #ifdef SKIRT_EXPERIMENT_TIMELINE
     const unsigned long long tlStart = __builtin_amdgcn_s_memrealtime();
     unsigned long long tlExhausted = 0, tlRays = 0;
@@ -2004,7 +2011,7 @@ __device__ __forceinline__ void traceBody(const Args& a) {
     if (threadIdx.x < 3 * (kBlock / 64)) T.waveSegs[threadIdx.x] = 0;
     __syncthreads();
     const int lane = threadIdx.x & 63;
-    const unsigned int nrays = a.ctr[a.parity];
+    const unsigned int nrays = nfront + a.ctr[8 + a.parity];
     Ray r;
     r.mode = RAY_NONE;
     bool done = false;
@@ -2045,7 +2052,7 @@ __device__ __forceinline__ void traceBody(const Args& a) {
 #endif
             if (idle) {
                 if (id >= nrays) done = true;
-                else T.load(r, id);  // a RAY_NONE record (empty path) leaves the lane idle
+                else T.load(r, id < nfront ? id : (unsigned)a.rayCap - 1u - (id - nfront));  // a RAY_NONE record (empty path) leaves the lane idle
             }
 #ifdef SKIRT_EXPERIMENT_TIMELINE
             tlRays += (unsigned long long)__popcll(__ballot(idle && id < nrays));
@@ -2655,6 +2662,48 @@ __device__ __forceinline__ void blockReserve3(unsigned* ctr0, unsigned c0, unsig
     __syncthreads();  // the scratch words are reused by the next call
 }
 
+// four counters at once (scratch: 4 * (kBlock / 64) + 4 words)
+__device__ __forceinline__ void blockReserve4(unsigned* const (&ctr)[4], const unsigned (&c)[4], unsigned (&r)[4],
+                                              unsigned long long* scratch) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    constexpr int W = kBlock / 64;
+    unsigned in[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) in[q] = c[q];
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        unsigned v[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) v[q] = __shfl_up(in[q], off);
+        if (lane >= off) {
+#pragma unroll
+            for (int q = 0; q < 4; q++) in[q] += v[q];
+        }
+    }
+    if (lane == 63) {
+#pragma unroll
+        for (int q = 0; q < 4; q++) scratch[q * W + wave] = in[q];
+    }
+    __syncthreads();
+    unsigned w[4] = {0, 0, 0, 0}, t[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int ww = 0; ww < W; ww++) {
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const unsigned sv = (unsigned)scratch[q * W + ww];
+            if (ww < wave) w[q] += sv;
+            t[q] += sv;
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; q++)
+        if (threadIdx.x == 64 * q) scratch[4 * W + q] = t[q] ? atomicAdd(ctr[q], t[q]) : 0u;
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 4; q++) r[q] = (unsigned)scratch[4 * W + q] + w[q] + in[q] - c[q];
+    __syncthreads();  // the scratch words are reused by the next call
+}
+
 // Global packet index of the j-th packet of this call. A sharded call (IdenticalAssigner,
 // IdenticalAssigner.cpp:37-58: every process runs its block of chunks at every wavelength) shoots
 // packets [sliceLo, sliceLo + sliceCnt) of each wavelength; the Philox stream is keyed on the global
@@ -2667,7 +2716,7 @@ __device__ __forceinline__ unsigned long long globalPacket(const Args& a, unsign
 
 template <int GRID, bool ONECOMP>
 __global__ void __launch_bounds__(kBlock) SKIRT_EVENT_ATTR eventKernel(const Args a) {
-    __shared__ unsigned long long resv[3 * (kBlock / 64) + 3];
+    __shared__ unsigned long long resv[4 * (kBlock / 64) + 4];
     extern __shared__ __attribute__((aligned(16))) double lds[];
     if (blockIdx.x == 0 && threadIdx.x == 0) a.ctr[4] = 0;  // the trace kernel's pull counter
     if (!a.init && a.ctr[2 + a.parity] == 0) return;  // an iteration after the end of the phase
@@ -2815,9 +2864,16 @@ __global__ void __launch_bounds__(kBlock) SKIRT_EVENT_ATTR eventKernel(const Arg
         // the peel-offs: one atomic each per block
         const bool active = mainMode != RAY_NONE;
         const int npeel = nray - (mainMode != RAY_NONE ? 1 : 0);
-        unsigned int pos = 0, apos = 0, dpos = 0;
-        blockReserve3(a.ctr + a.parity, (unsigned)nray, pos, a.ctr + 2 + (1 - a.parity), active ? 1u : 0u, apos,
-                      a.ctr + 5 + a.parity, (unsigned)npeel, dpos, resv);
+        // a WALK ray goes to the top of the queue (Args::walkBack)
+        const bool back = a.walkBack && mainMode == RAY_WALK;
+        unsigned int pos, apos, dpos, wpos;
+        {
+            unsigned* const ctrs[4] = {a.ctr + a.parity, a.ctr + 2 + (1 - a.parity), a.ctr + 5 + a.parity, a.ctr + 8 + a.parity};
+            const unsigned cnt[4] = {(unsigned)nray - (back ? 1u : 0u), active ? 1u : 0u, (unsigned)npeel, back ? 1u : 0u};
+            unsigned res[4];
+            blockReserve4(ctrs, cnt, res, resv);
+            pos = res[0]; apos = res[1]; dpos = res[2]; wpos = res[3];
+        }
 #ifdef SKIRT_EXPERIMENT_TIMELINE
         unsigned long long ts3 = stamp();
         tlPart[2] += ts3 - ts2;
@@ -2860,6 +2916,10 @@ __global__ void __launch_bounds__(kBlock) SKIRT_EVENT_ATTR eventKernel(const Arg
                 prm = mainParam;
                 idx = slot;
                 flags = mainMode | ((unsigned)p.ell << 18);
+                if (back) {
+                    E.emitRay((unsigned)a.rayCap - 1u - wpos, p, dx, dy, dz, prm, idx, flags, vcell);
+                    continue;
+                }
             }
             E.emitRay(pos++, p, dx, dy, dz, prm, idx, flags, vcell);
         }
@@ -3077,6 +3137,11 @@ struct SkirtMcrt {
     size_t poolBytes = 0;
     // config
     int traceGrid = 0, threshold = 8, slotsWanted = 0;
+    // WALK rays at the end of the pull order: SKIRT_AMD_WALK_BACK=1 / 0, default (-1) on Voronoi grids only.
+    // It shortens every grid's launch tail, but on the tree and Cartesian grids the launch's main part then
+    // runs without the atomic-free WALK paths between the absorbing FILL paths: C3 2.16e8 -> 2.08e8, C2
+    // 2.9e8 -> 2.8e8; C4 9.30e7 -> 9.38e7 (profiles/r03_walk_back_ab.txt)
+    int walkBack = getenv("SKIRT_AMD_WALK_BACK") ? atoi(getenv("SKIRT_AMD_WALK_BACK")) : -1;
     int traceBlocksPerCU = 0;  // the occupancy the last trace launch was sized for
     int lastDetCopies = 0;  // SED copies of the last run's detect kernel
     double lastMs = 0;
@@ -3206,7 +3271,7 @@ void carvePool(SkirtMcrt* c, Args& a, int h) {
     }
     a.nslots = c->nslots;
     a.rayCap = c->rayCap;
-    a.ctr = c->dCtr + 8 * h;
+    a.ctr = c->dCtr + kCtrWords * h;
 }
 
 // Decides whether the octree can be walked through a leaf map (Grid<SKIRT_GRID_OCTREE>): every node
@@ -3430,8 +3495,8 @@ int skirt_mcrt_create(int device, SkirtMcrt** out) {
         hipMalloc(&c->dClaim, sizeof(unsigned long long)) != hipSuccess ||
         hipMalloc(&c->dStats, 8 * kStatCopies * sizeof(unsigned long long)) != hipSuccess ||
         hipMalloc(&c->dError, sizeof(unsigned int)) != hipSuccess ||
-        hipMalloc(&c->dCtr, kMaxHalves * 8 * sizeof(unsigned int)) != hipSuccess ||
-        hipHostMalloc(&c->hCtr, kMaxHalves * kPollRing * 8 * sizeof(unsigned int)) != hipSuccess ||
+        hipMalloc(&c->dCtr, kMaxHalves * kCtrWords * sizeof(unsigned int)) != hipSuccess ||
+        hipHostMalloc(&c->hCtr, kMaxHalves * kPollRing * kCtrWords * sizeof(unsigned int)) != hipSuccess ||
         hipEventCreateWithFlags(&c->evFork, hipEventDisableTiming) != hipSuccess) {
         delete c;
         return SKIRT_ERR_HIP;
@@ -4223,6 +4288,7 @@ static int runPhase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, uint6
     a.crossed = c->dCrossed; a.crossedBins = c->crossedBins;
     a.claim = c->dClaim;
     a.threshold = c->threshold;
+    a.walkBack = c->walkBack >= 0 ? c->walkBack : (c->gridKind == SKIRT_GRID_VORONOI ? 1 : 0);
     // LDS layout (doubles): mesh | optics | instruments | SED sums
     int off = 0;
     a.ldsMeshOff = off;
@@ -4297,7 +4363,7 @@ static int runPhase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, uint6
     const int dgrid = std::max(1, std::max(1, c->nCusE) * 4);
 
     HIPCHECK(c, hipMemsetAsync(c->dClaim, 0, sizeof(unsigned long long), c->stream));
-    HIPCHECK(c, hipMemsetAsync(c->dCtr, 0, kMaxHalves * 8 * sizeof(unsigned int), c->stream));
+    HIPCHECK(c, hipMemsetAsync(c->dCtr, 0, kMaxHalves * kCtrWords * sizeof(unsigned int), c->stream));
     HIPCHECK(c, hipEventRecord(c->ev0, c->stream));
     if (forked) {  // the pipeline streams start after the caller's stream
         HIPCHECK(c, hipEventRecord(c->evFork, c->stream));
@@ -4388,7 +4454,7 @@ static int runPhase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, uint6
             if (pendingDet[h] && (rc = detect(h))) return rc;
             if (its[h] > 0 && its[h] % kPollEvery == 0) {
                 const int slot = polls[h] % kPollRing;
-                unsigned int* hc = c->hCtr + (h * kPollRing + slot) * 8;
+                unsigned int* hc = c->hCtr + (h * kPollRing + slot) * kCtrWords;
                 hipEvent_t pe = c->pollEv[h * kPollRing + slot];
                 if (polls[h] >= kPollRing) {
                     // the copy made kPollRing polls ago: is the half finished?
