@@ -59,6 +59,14 @@ def pmc_traffic(config):
     return {"bytes_per_launch": d["traffic_bytes_per_launch"], "source": d["source"]}
 
 
+def bound_of(hbm_frac, atomic_frac):
+    """The trace kernel's limiter from the fractions of HBM bandwidth and of the f64 atomic request rate it
+    uses: the larger one if it is at least half its peak, else instruction issue / latency."""
+    if max(hbm_frac, atomic_frac) < 0.5:
+        return "issue"
+    return "hbm" if hbm_frac >= atomic_frac else "atomic"
+
+
 def algorithmic_bytes(stats, geom_bytes, ncomp):
     """SURVEY.md section 8(d): per segment the cell geometry (octree: 48 B box + 8 B index/neighbour;
     Voronoi: 4 + 28 k B for k ~ 15.5 neighbours; Cartesian: 0, the mesh lives in LDS) plus 8*Ncomp B of density; 16 B read-modify-write per absorbed
@@ -244,9 +252,13 @@ def main():
                            ("segments_fill", "segments_walk", "segments_peel", "absorb_adds", "detects")},
         },
         "roofline": {
-            # the limiter is whichever resource the trace kernel uses the largest fraction of: HBM bytes
-            # (SURVEY 8(d) algorithmic bytes) or the chip's f64 atomic request rate (the Labs adds)
-            "bound": "hbm" if hbm_frac >= atomic_frac else "atomic",
+            # the limiter: whichever of HBM bytes and the chip's f64 atomic request rate (the Labs adds) the
+            # trace kernel uses the larger fraction of -- HBM as measured (PMC traffic) when the passes exist,
+            # since a cached working set (the C4 Voronoi mesh, 30 MB, in the MALL) makes the SURVEY bytes exceed
+            # what HBM delivers -- or "issue" when neither is above half its peak (instruction issue and
+            # latency)
+            "bound": bound_of(hbm_frac if traffic is None else traffic["bytes_per_launch"] / launch_s / 1e9 / HBM_PEAK_GBS,
+                              atomic_frac),
             "achieved": achieved,
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
@@ -262,6 +274,7 @@ def main():
             "engine_frac": engine_bytes / launch_s / 1e9 / HBM_PEAK_GBS,
             "traffic_source": traffic["source"] if traffic else None,
             "traffic_gbs": traffic["bytes_per_launch"] / launch_s / 1e9 if traffic else None,
+            "traffic_frac": traffic["bytes_per_launch"] / launch_s / 1e9 / HBM_PEAK_GBS if traffic else None,
             # Labs adds are scattered f64 atomics, executed memory-side in 64-byte requests at a fixed
             # chip-wide request rate (tools/atomic_bench.hip, profiles/r01_atomic_bench.txt); adds of one
             # wave instruction that fall in one line share a request
