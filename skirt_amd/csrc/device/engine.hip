@@ -173,6 +173,14 @@ struct LeafEntry;
 // the float offsets, and evaluates the reference's exact expression only for the winner (from the winner's
 // header, which is the next step's first load) or, when the bounds cannot single one out, for every
 // possible winner.
+// one entry of a Voronoi block list (Box::cellindices): the device cell and its exact site, so that cellIndex
+// reads a candidate in one round trip (two 16-byte loads) instead of the list entry, then the site
+struct alignas(16) BlockSite {
+    double x, y, z;
+    int id, pad;
+};
+static_assert(sizeof(BlockSite) == 32, "block site layout");
+
 struct alignas(16) VorEntry {
     float ox, oy, oz;
     int next;
@@ -256,7 +264,7 @@ struct Args {
     const int* devCell;          // reference cell -> device cell (Voronoi launches)
     int vnb;                     // Voronoi block grid: blocks per axis
     const int* blockOffset;
-    const int* blockList;
+    const struct BlockSite* blockSites;  // Voronoi: the block lists, each entry with its cell's exact site
     const LeafEntry* leafMap;       // octree leaf map: Morton-ordered finest-level cells -> leaf
     const double* treeT;         // octree split coordinates per axis, 3 x (mapN + 1) (staged in LDS)
     int mapL, mapN;              // leaf map depth and 2^depth
@@ -277,6 +285,7 @@ struct Args {
     // dust-phase cell sources (PanMonteCarloSimulation.cpp:193-205, 273-294), reference cell order
     const double* cellLv;        // [nlambda][ncells]
     const double* cellCdf;       // [nlambda][ncells + 1]
+    const int* cellGuide;        // [nlambda][ncells + 1]: the CDF index at k / ncells (cellGuideKernel)
     const double* cellLtot;      // [nlambda]
     double cellBias;             // PanDustSystem::emissionBias (dust emission phase)
     const int* cellNode;         // octree: the leaf node of every reference cell
@@ -1068,20 +1077,24 @@ struct Grid<SKIRT_GRID_VORONOI> {
         const int b = i * nb * nb + j * nb + k;
         int m = -1;
         double best = kDblMax;
-        // the list in groups of kCellIndexGroup: the group's list entries, then its sites, load together (one
-        // round trip each instead of two per candidate); the candidates are then taken in list order, so the
-        // first of equal distances wins as in the reference's loop
+        // the list in groups of kCellIndexGroup candidates, each {site, cell} in one 32-byte record, a group's
+        // records loaded together (one round trip per group); the candidates are then taken in list order, so
+        // the first of equal distances wins as in the reference's loop
         constexpr int G = kCellIndexGroup;
         const int qe = a.blockOffset[b + 1];
         for (int q0 = a.blockOffset[b]; q0 < qe; q0 += G) {
             int c[G];
             double sx[G], sy[G], sz[G];
 #pragma unroll
-            for (int u = 0; u < G; u++) c[u] = q0 + u < qe ? a.blockList[q0 + u] : -1;
-#pragma unroll
             for (int u = 0; u < G; u++) {
+                c[u] = -1;
                 sx[u] = sy[u] = sz[u] = 0.0;
-                if (c[u] >= 0) { sx[u] = a.site[3 * c[u]]; sy[u] = a.site[3 * c[u] + 1]; sz[u] = a.site[3 * c[u] + 2]; }
+                if (q0 + u < qe) {
+                    const double2* rec = reinterpret_cast<const double2*>(a.blockSites + q0 + u);
+                    const double2 r0 = rec[0], r1 = rec[1];
+                    sx[u] = r0.x; sy[u] = r0.y; sz[u] = r1.x;
+                    c[u] = (int)(unsigned)__double_as_longlong(r1.y);  // the id, in the low word
+                }
             }
 #pragma unroll
             for (int u = 0; u < G; u++) {
@@ -1929,6 +1942,45 @@ __global__ void __launch_bounds__(kBlock) cellCdfKernel(const EmisArgs e) {
     if (m == 0) X[0] = 0.0;
 }
 
+// NR::locate_clip over a table in global memory (n entries): the largest j <= n - 2 with v[j] <= q, 0 below v[0]
+__device__ __forceinline__ int locateClipTable(const double* v, int n, double q) {
+    if (q < v[0]) return 0;
+    int jl = -1, ju = n - 1;
+    while (ju - jl > 1) {
+        const int jm = (ju + jl) >> 1;
+        if (q < v[jm]) ju = jm;
+        else jl = jm;
+    }
+    return jl;
+}
+
+// A guide table over a CDF of N + 1 entries: G[k] = locate_clip(v, k / N), k = 0 .. N. A draw q then only
+// bisects [G[k], G[k + 1]] with k = floor(q N) -- two or three dependent loads instead of log2(N) ~ 20 (the
+// dust-phase launch draws a cell from 622,490 per packet in C5).
+__global__ void __launch_bounds__(kBlock) cellGuideKernel(const double* cdf, int* guide, int N) {
+    const int ell = blockIdx.y, k = blockIdx.x * kBlock + threadIdx.x;
+    if (k > N) return;
+    const double* v = cdf + (size_t)ell * (N + 1);
+    guide[(size_t)ell * (N + 1) + k] = locateClipTable(v, N + 1, (double)k / (double)N);
+}
+
+// locate_clip(v, N + 1, q) through the guide table: the bracket [G[k], G[k + 1] + 1) holds the answer when
+// v[G[k]] <= q and q < v[G[k + 1] + 1] (or the bracket ends at the table's last index) -- checked, since
+// floor(q N) may round across a bucket edge; otherwise the whole table is bisected. Within a valid bracket
+// the bisection finds the same largest j with v[j] <= q as the full one.
+__device__ __forceinline__ int locateGuided(const double* v, const int* G, int N, double q) {
+    const int k = max(0, min(N - 1, static_cast<int>(q * (double)N)));
+    const int lo = G[k], hi = G[k + 1] + 1;
+    if (!(v[lo] <= q) || (hi < N && !(q < v[hi]))) return locateClipTable(v, N + 1, q);
+    int jl = lo, ju = hi;
+    while (ju - jl > 1) {
+        const int jm = (ju + jl) >> 1;
+        if (q < v[jm]) ju = jm;
+        else jl = jm;
+    }
+    return jl;
+}
+
 // fills the leaf map: one thread per finest-level cell descends the (checked) tree by its index bits
 // (a k-d tree by the bit of its split axis at that axis' depth)
 __global__ void __launch_bounds__(kBlock) buildLeafMapKernel(LeafEntry* map, const int* firstChild, const signed char* splitDir,
@@ -2434,18 +2486,19 @@ struct Events {
         p.ell = ell;
         const int N = a.ncells;
         const double* cdf = a.cellCdf + (size_t)ell * (N + 1);
+        const int* guide = a.cellGuide + (size_t)ell * (N + 1);
         const double X = p.rng.uniform();
         int m;
         double L = L0;
         if (a.phase == SKIRT_PHASE_DUST_EMISSION) {
             const double xi = a.cellBias;
             if (X < xi) m = max(0, min(N - 1, static_cast<int>(N * X / xi)));
-            else m = locateClipGlobal(cdf, N + 1, (X - xi) / (1 - xi));
+            else m = locateGuided(cdf, guide, N, (X - xi) / (1 - xi));
             const double Lmean = Ltot / N;
             const double weight = 1.0 / (1 - xi + xi * Lmean / a.cellLv[(size_t)ell * N + m]);
             L = L0 * weight;
         } else {
-            m = locateClipGlobal(cdf, N + 1, X);
+            m = locateGuided(cdf, guide, N, X);
         }
         if (GRID == SKIRT_GRID_VORONOI) m = a.devCell[m];  // the Voronoi arrays are in device order
         double b[6];
@@ -3073,7 +3126,8 @@ struct SkirtMcrt {
     // Voronoi grid
     double *dSite = nullptr, *dCellBbox = nullptr;
     VorEntry* dVorSlots = nullptr;
-    int *dVorStart = nullptr, *dBlockOffset = nullptr, *dBlockList = nullptr;
+    int *dVorStart = nullptr, *dBlockOffset = nullptr;
+    BlockSite* dBlockSites = nullptr;
     std::vector<VorEntry> vorSlotsHost;  // host copy: upload_media writes the densities into the headers
     std::vector<int> vorStartHost;
     double vorScale = 1.0;
@@ -3100,6 +3154,8 @@ struct SkirtMcrt {
     double emissionBias = 0.5;
     // dust-phase cell sources and the dust Labs tally
     double *dCellLv = nullptr, *dCellCdf = nullptr, *dCellLtot = nullptr;
+    int* dCellGuide = nullptr;  // guide tables of the cell CDFs (cellGuideKernel)
+    size_t cellGuideCount = 0;
     double cellBias = 0.5;
     int* dCellNode = nullptr;
     double* dLabsDust = nullptr;
@@ -3364,7 +3420,7 @@ void gridArgs(const SkirtMcrt* c, Args& a) {
     a.nbrOffset = c->dNbrOffset; a.nbrList = c->dNbrList; a.eps = c->eps; a.search = c->search;
     a.site = c->dSite; a.vorStart = c->dVorStart; a.vorSlots = c->dVorSlots; a.vorScale = (float)c->vorScale; a.cellBbox = c->dCellBbox;
     a.devCell = c->dDevCell;
-    a.vnb = c->vnb; a.blockOffset = c->dBlockOffset; a.blockList = c->dBlockList;
+    a.vnb = c->vnb; a.blockOffset = c->dBlockOffset; a.blockSites = c->dBlockSites;
     a.ncomp = std::max(1, c->ncomp); a.nlambda = c->nlambda;
     a.rho = c->dRho;
 }
@@ -3787,8 +3843,11 @@ int skirt_mcrt_upload_grid(SkirtMcrt* c, const SkirtGridDesc* g) {
             std::memcpy(blk + 2, ids, sizeof ids);
         }
         c->vorSlotsHost = std::move(slots);
-        std::vector<int> blocks(std::max(nbl, 1), 0);
-        for (int q = 0; q < nbl; q++) blocks[q] = c->devCell[g->block_list[q]];
+        std::vector<BlockSite> blocks(std::max(nbl, 1), BlockSite{0.0, 0.0, 0.0, -1, 0});
+        for (int q = 0; q < nbl; q++) {
+            const int m = g->block_list[q];
+            blocks[q] = BlockSite{g->site[3 * (size_t)m], g->site[3 * (size_t)m + 1], g->site[3 * (size_t)m + 2], c->devCell[m], 0};
+        }
         int rc;
         if ((rc = upload(c, c->dSite, site.data(), site.size()))) return rc;
         if ((rc = upload(c, c->dCellBbox, bbox.data(), bbox.size()))) return rc;
@@ -3796,7 +3855,7 @@ int skirt_mcrt_upload_grid(SkirtMcrt* c, const SkirtGridDesc* g) {
         if ((rc = upload(c, c->dVorSlots, c->vorSlotsHost.data(), c->vorSlotsHost.size()))) return rc;
         c->vorStartHost = std::move(start);
         if ((rc = upload(c, c->dBlockOffset, g->block_offset, nb3 + 1))) return rc;
-        if ((rc = upload(c, c->dBlockList, blocks.data(), blocks.size()))) return rc;
+        if ((rc = upload(c, c->dBlockSites, blocks.data(), blocks.size()))) return rc;
         if ((rc = upload(c, c->dDevCell, c->devCell.data(), c->devCell.size()))) return rc;
     } else {
         return fail(c, SKIRT_ERR_UNSUPPORTED, "unsupported grid kind");
@@ -3982,6 +4041,19 @@ int skirt_mcrt_run_stellar(SkirtMcrt* c, uint64_t npp, uint64_t first, uint64_t 
     return skirt_mcrt_run_phase(c, SKIRT_PHASE_STELLAR, 0, npp, first, count, seed, p);
 }
 
+// the guide tables of the cell CDFs (dCellCdf must hold them), on the engine's stream
+static int buildCellGuide(SkirtMcrt* c) {
+    const int N = c->ncells, Nl = c->nlambda;
+    const size_t n = (size_t)Nl * (N + 1);
+    if (c->dCellGuide && c->cellGuideCount != n) { (void)hipFree(c->dCellGuide); c->dCellGuide = nullptr; }
+    if (!c->dCellGuide) HIPCHECK(c, hipMalloc(&c->dCellGuide, n * sizeof(int)));
+    c->cellGuideCount = n;
+    hipLaunchKernelGGL(cellGuideKernel, dim3((N + 1 + kBlock - 1) / kBlock, Nl), dim3(kBlock), 0, c->stream,
+                       (const double*)c->dCellCdf, c->dCellGuide, N);
+    HIPCHECK(c, hipGetLastError());
+    return SKIRT_OK;
+}
+
 int skirt_mcrt_upload_cell_sources(SkirtMcrt* c, const SkirtCellSourceDesc* src) {
     if (!c || !src) return SKIRT_ERR_ARG;
     if (c->gridKind < 0) return fail(c, SKIRT_ERR_STATE, "upload the grid before cell sources");
@@ -3995,7 +4067,7 @@ int skirt_mcrt_upload_cell_sources(SkirtMcrt* c, const SkirtCellSourceDesc* src)
     if ((rc = upload(c, c->dCellCdf, src->cdf, nl * (nc + 1)))) return rc;
     if ((rc = upload(c, c->dCellLtot, src->ltot, nl))) return rc;
     c->cellBias = src->emission_bias;
-    return SKIRT_OK;
+    return buildCellGuide(c);
 }
 
 static int ensureDustLabs(SkirtMcrt* c);
@@ -4063,7 +4135,7 @@ int skirt_mcrt_compute_cell_sources(SkirtMcrt* c, int include_dust) {
     hipLaunchKernelGGL(cellScanBlocksKernel, dim3(Nl), dim3(kBlock), 0, c->stream, e);
     hipLaunchKernelGGL(cellCdfKernel, dim3(nblocks, Nl), dim3(kBlock), 0, c->stream, e);
     HIPCHECK(c, hipGetLastError());
-    return SKIRT_OK;
+    return buildCellGuide(c);
 }
 
 int skirt_mcrt_dust_labs_total(SkirtMcrt* c, double* total) {
@@ -4273,7 +4345,7 @@ static int runPhase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, uint6
     a.phase = phase;
     a.peel = phase != SKIRT_PHASE_DUST_SELFABS;
     a.continuous = continuous ? 1 : 0;
-    a.cellLv = c->dCellLv; a.cellCdf = c->dCellCdf; a.cellLtot = c->dCellLtot; a.cellBias = c->cellBias;
+    a.cellLv = c->dCellLv; a.cellCdf = c->dCellCdf; a.cellGuide = c->dCellGuide; a.cellLtot = c->dCellLtot; a.cellBias = c->cellBias;
     a.cellNode = c->dCellNode;
     a.minWeightReduction = p->min_weight_reduction; a.minScatt = p->min_scatt_events; a.xi = p->scatt_bias;
     // absorption: the stellar phase as its parameters say (into Labs), self-absorption always (into the
@@ -4690,10 +4762,10 @@ void skirt_mcrt_destroy(SkirtMcrt* c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     void* bufs[] = {c->dMesh, c->dBox, c->dFirstChild, c->dSplitDir, c->dFather, c->dCellnumber, c->dNbrOffset, c->dNbrList, c->dTreeT,
-                    c->dLeafMap, c->dCellLv, c->dCellCdf, c->dCellLtot, c->dCellNode, c->dEmisVolume, c->dEmisKabs,
+                    c->dLeafMap, c->dCellLv, c->dCellCdf, c->dCellGuide, c->dCellLtot, c->dCellNode, c->dEmisVolume, c->dEmisKabs,
                     c->dEmisSigma, c->dEmisMu, c->dEmisTv, c->dEmisPlanck, c->dEmisLambda, c->dEmisDlambda,
                     c->dEmisScratch, c->dDevCell, c->dSite, c->dCellBbox, c->dVorStart, c->dVorSlots,
-                    c->dBlockOffset, c->dBlockList, c->dRho,
+                    c->dBlockOffset, c->dBlockSites, c->dRho,
                     c->dOptics, c->dGeomParam, c->dGeomTable, c->dLum, c->dLumtot, c->dCdf, c->dInstr,
                     c->dClaim, c->dStats, c->dError, c->dCtr, c->dPool, c->dCrossed};
     for (void* b : bufs)
