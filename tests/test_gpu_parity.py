@@ -86,6 +86,34 @@ def test_leaf_map_walk_equals_node_walk(path, packages, monkeypatch):
     np.testing.assert_allclose(fa, fb, rtol=1e-10, atol=1e-300)
 
 
+@pytest.mark.parametrize("name,packages,dust", [("pan_cart16", 2000, False), ("pan_oct", 2000, False),
+                                                ("vor_pan", 1000, False), ("pan_oct_sa", 500, True),
+                                                ("vor_pan_cs", 150, False)])
+def test_walk_ray_queue_order_does_not_change_results(name, packages, dust, monkeypatch):
+    """WALK rays queued from the top of the ray queue and pulled last (SKIRT_AMD_WALK_BACK=1, the Voronoi
+    default) or in event order (0, the tree and Cartesian default): the same packets take the same paths,
+    so the counts are equal and the tallies agree up to the order of the f64 atomic additions."""
+    runs = []
+    for back in ("1", "0"):
+        monkeypatch.setenv("SKIRT_AMD_WALK_BACK", back)
+        runs.append(run_gpu(name, packages=packages, dust=dust))
+    a, b = runs
+    sa, sb = a.stats(), b.stats()
+    for k in ("packets", "segments_fill", "segments_walk", "segments_peel", "detects", "absorb_adds"):
+        assert sa[k] == sb[k], (k, sa[k], sb[k])
+    for la, lb in ((a.labs(), b.labs()), (a.labs_dust(), b.labs_dust())):
+        assert (la is None) == (lb is None)
+        if la is not None:
+            np.testing.assert_allclose(la, lb, rtol=1e-10, atol=1e-300)
+    for i in range(a.info.ninstruments):
+        fa, da = a.instrument(i)
+        fb, db = b.instrument(i)
+        if da is not None:
+            np.testing.assert_allclose(da, db, rtol=1e-10, atol=1e-300)
+        if fa is not None:
+            np.testing.assert_allclose(fa, fb, rtol=1e-10, atol=1e-300)
+
+
 @pytest.mark.parametrize("name,packages", [("pan_cart16", 2000), ("pan_oct", 2000), ("pan_cart16_sa", 1000),
                                            ("pan_oct_sa", 1000), ("pan_oct_sac", 1000), ("vor_pan", 1000),
                                            ("pan_cart16_cs", 300), ("pan_oct_cs", 300), ("vor_pan_cs", 200)])
