@@ -201,7 +201,9 @@ int skirt_mcrt_upload_sources(SkirtMcrt* ctx, const SkirtSourceDesc* src);
 int skirt_mcrt_set_instruments(SkirtMcrt* ctx, const SkirtInstrDesc* instr, int n);
 /* device tally buffers: Labs (stored wavelength-major [nlambda][row] on the device, rows of device cells
  * padded to a 64-byte line; n_labs >= ncells*nlambda) and the concatenated instrument tallies. Optionally bind caller-owned device memory of the
- * sizes returned by skirt_mcrt_tally_sizes (e.g. torch tensors, so they can be all-reduced in place). */
+ * sizes returned by skirt_mcrt_tally_sizes (e.g. torch tensors, so they can be all-reduced in place).
+ * Any 8-byte alignment is correct; 64-byte aligned buffers (hipMalloc, torch) let the adds of one line
+ * share an atomic request (sibling cells of Labs, the slots of one frame pixel). */
 int skirt_mcrt_tally_sizes(SkirtMcrt* ctx, size_t* n_labs, size_t* n_instr);
 int skirt_mcrt_bind_tallies(SkirtMcrt* ctx, double* d_labs, double* d_instr);
 int skirt_mcrt_zero_tallies(SkirtMcrt* ctx);

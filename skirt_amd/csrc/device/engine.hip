@@ -3964,6 +3964,10 @@ int skirt_mcrt_set_instruments(SkirtMcrt* c, const SkirtInstrDesc* in, int n) {
         d.sinpa = in[i].sinpa; d.cospa = in[i].cospa;
         d.xpmin = in[i].xpmin; d.xpsiz = in[i].xpsiz; d.ypmin = in[i].ypmin; d.ypsiz = in[i].ypsiz;
         d.slotStride = d.nslots == 1 ? 1 : (d.nslots + 7) / 8 * 8;
+        // every frame starts on a 64-byte line (the tally itself is at least 256-byte aligned), so that a
+        // detection's slots (slotStride 8) share one line and one atomic request also after another
+        // instrument's SEDs
+        off = (off + 7) & ~7LL;
         d.frameBase = off;
         const long long nframes = (d.kind == SKIRT_INSTR_SED) ? 0 : (long long)d.slotStride * c->nlambda * d.nx * d.ny;
         off += nframes;
