@@ -2715,7 +2715,8 @@ __device__ __forceinline__ void blockReserve3(unsigned* ctr0, unsigned c0, unsig
     __syncthreads();  // the scratch words are reused by the next call
 }
 
-// four counters at once (scratch: 4 * (kBlock / 64) + 4 words)
+// four counters at once (scratch: 4 * (kBlock / 64) + 4 words); the first lane of wave q issues counter q's atomic
+static_assert(kBlock >= 256, "blockReserve4 needs four waves per block");
 __device__ __forceinline__ void blockReserve4(unsigned* const (&ctr)[4], const unsigned (&c)[4], unsigned (&r)[4],
                                               unsigned long long* scratch) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
