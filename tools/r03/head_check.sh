@@ -1,0 +1,9 @@
+# round 3: last check at the head -- smoke, the whole GPU suite, the default bench (C3 + CPU baseline)
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+run() { local name=$1 t=$2; shift 2; echo "== $name"; timeout -k 10 $t "$@" > gpurun_out/$name.log 2>&1; local rc=$?; echo "rc=$rc"; tail -${TAILN:-1} gpurun_out/$name.log | cut -c1-300; return $rc; }
+run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" &&
+TAILN=3 run pytest_gpu 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread &&
+run bench_default 600 python bench.py
