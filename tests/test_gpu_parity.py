@@ -26,7 +26,12 @@ GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 
 def ski(name):
-    return os.path.join(GOLD, "ski", name + ".ski")
+    path = os.path.join(GOLD, "ski", name + ".ski")
+    if not os.path.exists(path):  # a variant of tests/tree_models.py (grid, geometry, mix, outputs)
+        import tempfile
+        import tree_models
+        path = tree_models.write_any(name, tempfile.mkdtemp(prefix="skirt_variant_"))
+    return path
 
 
 def run_gpu(name, packages=0.0, seed=0, first=0, count=0, dust=False):
@@ -238,26 +243,30 @@ def _engine_seed_runs(tmp_path, name, seeds=SEEDS):
     return np.array(J), np.array(seds)
 
 
-def _reference_outputs(tmp_path, name):
-    """(ds_isrf path, SED path) of `skirt -t 1` for `name`: the committed reference fixture, or -- for the
-    models without one (pan_oct_sa: parity against the reference unpinned) -- the oracle in MT mode, which
-    reproduces `skirt -t 1` bit for bit on every committed fixture (tests/test_oracle_golden.py)."""
+def _reference_outputs(name):
+    """(ds_isrf path, SED path) of `skirt -t 1` for `name`: the committed reference fixture (written by the
+    reference rebuilt from its sources, tests/golden/make_fixtures.sh; regenerated by
+    tests/test_reference_rebuild.py)."""
     ref = os.path.join(GOLD, "ref", name + "_s4357")
-    if os.path.exists(ref + "_ds_isrf.dat"):
-        return ref + "_ds_isrf.dat", ref + "_i30_sed.dat"
-    prefix = str(tmp_path / (name + "_oracle_mt"))
-    O.run(ski(name), rng=O.RNG_MT, threads=1, phases=O.PHASES_ALL, outprefix=prefix)
-    return prefix + "_ds_isrf.dat", prefix + "_i30_sed.dat"
+    assert os.path.exists(ref + "_ds_isrf.dat") and os.path.exists(ref + "_i30_sed.dat"), name
+    return ref + "_ds_isrf.dat", ref + "_i30_sed.dat"
 
 
-@pytest.mark.parametrize("name", ["pan_cart16", "pan_oct", "pan_cart16_sa", "vor_pan", "pan_oct_sa"])
+# every fixture model with dust emission (an ISRF): the originals, the C5 shape (octree + self-absorption,
+# fixed and convergence-driven cycles), continuous scattering, and the grid / geometry / mix variants
+STATISTICAL_MODELS = ["pan_cart16", "pan_oct", "pan_cart16_sa", "vor_pan", "pan_oct_sa", "pan_oct_sac",
+                      "pan_cart16_cs", "pan_oct_cs", "vor_pan_cs", "bin_pan", "oct_bary", "oct_pan_bk",
+                      "disk_oct", "bulge_oct", "sersic_cart", "cart_pow", "zubko_cart", "draineli_cart"]
+
+
+@pytest.mark.parametrize("name", STATISTICAL_MODELS)
 def test_engine_matches_reference_statistically(tmp_path, name):
     """All phases (stellar, self-absorption, dust emission) against `skirt -t 1`: per-wavelength ISRF sums
     and every SED column -- total, direct and scattered stellar, dust emission, dust scattered,
     transparent -- as z-scores against the spread of 8 independently seeded engine runs."""
     J, seds = _engine_seed_runs(tmp_path, name)
     Jsum = J.sum(axis=1)
-    ref_isrf, ref_sed_path = _reference_outputs(tmp_path, name)
+    ref_isrf, ref_sed_path = _reference_outputs(name)
     ref_J = _isrf_sums(ref_isrf)
     ref_sed = F.read_text_table(ref_sed_path)
     infl = np.sqrt(1 + 1.0 / len(SEEDS))
@@ -295,7 +304,7 @@ def _pools(J, max_rel_sd):
     return pools
 
 
-@pytest.mark.parametrize("name", ["pan_cart16", "pan_oct", "vor_pan", "pan_cart16_sa"])
+@pytest.mark.parametrize("name", ["pan_cart16", "pan_oct", "vor_pan", "pan_cart16_sa", "pan_oct_sa"])
 def test_per_cell_mean_intensity_matches_reference(tmp_path, name):
     """north_star's per-cell criterion: every cell's J_lambda (ds_isrf, i.e. its absorbed luminosity
     divided by the cell constant of DustSystem::meanintensityv, DustSystem.cpp:935-957) within the Monte

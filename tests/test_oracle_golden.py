@@ -15,10 +15,18 @@ import pytest
 
 import oracle_lib as O
 import skirt_files as F
+import tree_models
 
 RUNS = [("c1_oligo16", 4357), ("c1_oligo16", 777), ("oligo_2comp", 1234), ("pan_cart16", 4357),
         ("pan_oct", 4357), ("pan_oct", 99), ("pan_cart16_sa", 4357), ("pan_cart16_sac", 4357),
         ("vor_oligo", 4357), ("vor_pan", 4357)]
+# fixtures written by the rebuilt reference (oracle/ref.mk) in round 4: the C5 shape, continuous scattering,
+# the tree, mesh, geometry and mix variants of tests/tree_models.py, and the diagnostic outputs
+VARIANT_RUNS = [(name, 4357) for name in (
+    "pan_oct_sa", "pan_oct_sac", "pan_cart16_cs", "pan_oct_cs", "vor_pan_cs",
+    "bin_pan", "bin_bary", "bin_full_td", "oct_bary", "oct_pan_td", "oct_pan_bk", "oct_bary_bk",
+    "cart_odd", "cart_pow", "disk_oct", "disk_cart", "bulge_oct", "sersic_cart", "point_oct",
+    "zubko_cart", "draineli_cart", "pan_oct_out", "pan_cart16_out", "vor_pan_out")]
 LSUN = 3.839e26  # W (Units.cpp)
 
 
@@ -43,10 +51,15 @@ def _compare_outputs(golden_dir, tag, outdir, pan):
     return checked
 
 
-@pytest.mark.parametrize("ski,seed", RUNS)
+def _ski_path(golden_dir, tmp_path, name):
+    path = os.path.join(golden_dir, "ski", name + ".ski")
+    return path if os.path.exists(path) else tree_models.write_any(name, str(tmp_path))
+
+
+@pytest.mark.parametrize("ski,seed", RUNS + VARIANT_RUNS)
 def test_oracle_matches_reference_bit_for_bit(golden_dir, tmp_path, ski, seed):
     tag = "%s_s%d" % (ski, seed)
-    O.run(os.path.join(golden_dir, "ski", ski + ".ski"), rng=O.RNG_MT, seed=seed,
+    O.run(_ski_path(golden_dir, tmp_path, ski), rng=O.RNG_MT, seed=seed,
           outprefix=str(tmp_path / tag), phases=O.PHASES_ALL)
     n = _compare_outputs(golden_dir, tag, str(tmp_path), pan=ski.startswith("pan"))
     assert n >= 2

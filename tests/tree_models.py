@@ -119,3 +119,28 @@ def write(name, directory):
     with open(path, "w") as f:
         f.write(text)
     return path
+
+
+# the reference's diagnostic outputs switched on: ds_convergence (DustSystem.cpp:195-420), ds_crossed
+# (DustSystem.cpp:1004-1024) and ds_cellprops (DustSystem.cpp:636-660)
+OUTPUTS = {"pan_oct_out": "pan_oct", "pan_cart16_out": "pan_cart16", "vor_pan_out": "vor_pan"}
+
+
+def write_outputs(name, directory):
+    """Writes output variant `name` into `directory` and returns its path."""
+    text = open(os.path.join(GOLD, OUTPUTS[name] + ".ski")).read()
+    for attr in ("writeConvergence", "writeCellsCrossed", "writeCellProperties"):
+        text, n = re.subn(attr + '="false"', attr + '="true"', text)
+        assert n <= 1, (name, attr)
+    path = os.path.join(directory, name + ".ski")
+    with open(path, "w") as f:
+        f.write(text)
+    return path
+
+
+def write_any(name, directory):
+    """Writes the variant `name` of any kind (grid, geometry, mix, outputs) and returns its path."""
+    for table, writer in ((GRIDS, write), (GEOMETRIES, write_geometry), (MIXES, write_mix), (OUTPUTS, write_outputs)):
+        if name in table:
+            return writer(name, directory)
+    raise KeyError(name)
