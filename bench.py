@@ -11,6 +11,10 @@ phase ends with the reference's reductions (Labs all-reduce, instrument all-redu
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2|c4|c5]
        (N > 1: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...)
+       --dist-backend gloo runs the same sharded path over gloo (ranks may then share one GPU: rank r uses
+       device LOCAL_RANK mod the visible device count), to rehearse N > 1 on a one-GPU box;
+       --digest adds the summed tallies (Labs per wavelength, instrument totals) to the line, so that an
+       N-rank run can be checked against one rank shooting the same global packets.
 """
 import argparse
 import json
@@ -48,15 +52,23 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip-level parameters (spec)
 ATOMIC_PEAK_REQUESTS = 2.36e10
 
 
+# VALU issue peak of the chip in wave-instructions per second: a wave issues one VALU instruction over 2
+# cycles (MI355X_MICROARCH.md, "32 lanes/cycle x 2"), so 0.5 per SIMD per cycle, 4 SIMDs x 256 CUs, at the
+# 2.4 GHz maximum clock (the clock under load is lower; f64 arithmetic takes more cycles per instruction)
+VALU_ISSUE_PEAK = 256 * 4 * 0.5 * 2.4e9
+
+
 def pmc_traffic(config):
-    """HBM bytes per trace-kernel launch from the committed rocprofv3 PMC passes of this same bench
-    command (tools/pmc_traffic.py writes profiles/pmc_<config>.json); None when absent."""
+    """Per trace-kernel launch, from the committed rocprofv3 PMC passes of this same bench command
+    (tools/pmc_traffic.py writes profiles/pmc_<config>.json): HBM bytes (FETCH_SIZE + WRITE_SIZE) and, where
+    their passes ran, VALU wave-instructions; None when absent."""
     path = os.path.join(REPO, "profiles", "pmc_%s.json" % config)
     if not os.path.exists(path):
         return None
     with open(path) as f:
         d = json.load(f)
-    return {"bytes_per_launch": d["traffic_bytes_per_launch"], "source": d["source"]}
+    return {"bytes_per_launch": d["traffic_bytes_per_launch"], "source": d["source"],
+            "valu_per_launch": d.get("valu_insts_per_launch")}
 
 
 def bound_of(hbm_frac, atomic_frac):
@@ -105,6 +117,9 @@ def main():
     ap.add_argument("--threshold", type=int, default=0, help="idle lanes before a wave pulls rays (0 = engine default)")
     ap.add_argument("--slots", type=int, default=0, help="packet slots in flight (0 = engine default)")
     ap.add_argument("--trace-grid", type=int, default=0, help="trace kernel workgroups (0 = occupancy-derived)")
+    ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
+                    help="torch.distributed backend for N > 1 (nccl = RCCL over xGMI)")
+    ap.add_argument("--digest", action="store_true", help="report the reduced tallies' sums")
     args = ap.parse_args()
 
     import torch
@@ -113,9 +128,15 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    device = local
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    torch.cuda.set_device(local)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            # gloo: ranks may share a device (rehearsal of the N > 1 path on a one-GPU box)
+            device = local % max(1, torch.cuda.device_count())
+            dist.init_process_group("gloo")
+    torch.cuda.set_device(device)
 
     import skirt_amd
     from skirt_amd.sharding import TallyReducer, shard_slice
@@ -130,7 +151,7 @@ def main():
     # weak scaling: the phase has ppl packets per wavelength per rank; rank r shoots its slice of every
     # wavelength (the reference's IdenticalAssigner, skirt_mcrt_run_phase_shard)
     share = shard_slice(ppl * world, rank, world)[1] * info.nlambda
-    sim.attach(local)
+    sim.attach(device)
     if args.threshold or args.slots or args.trace_grid:
         sim.configure(slots=args.slots, grid=args.trace_grid, threshold=args.threshold)
     stream = torch.cuda.current_stream()
@@ -212,6 +233,10 @@ def main():
     achieved = bytes_per_launch / launch_s / 1e9
     traffic = pmc_traffic(args.config)
     hbm_frac = achieved / HBM_PEAK_GBS
+    traffic_frac = traffic["bytes_per_launch"] / launch_s / 1e9 / HBM_PEAK_GBS if traffic else None
+    # instruction issue: VALU wave-instructions per second (PMC) over the chip's issue peak
+    issue_frac = (traffic["valu_per_launch"] / launch_s / VALU_ISSUE_PEAK
+                  if traffic and traffic.get("valu_per_launch") else None)
     # the same launch priced at the bytes this engine's layouts read (ENGINE_SEGMENT_BYTES)
     engine_bytes = (segs * ENGINE_SEGMENT_BYTES[info.grid_kind] + delta["absorb_adds"] * 16) / max(1, trace_launches)
     requests_per_s = delta["labs_requests"] / max(1e-9, trace_ms / 1e3)
@@ -257,13 +282,19 @@ def main():
             # since a cached working set (the C4 Voronoi mesh, 30 MB, in the MALL) makes the SURVEY bytes exceed
             # what HBM delivers -- or "issue" when neither is above half its peak (instruction issue and
             # latency)
-            "bound": bound_of(hbm_frac if traffic is None else traffic["bytes_per_launch"] / launch_s / 1e9 / HBM_PEAK_GBS,
-                              atomic_frac),
+            "bound": bound_of(hbm_frac if traffic is None else traffic_frac, atomic_frac),
+            # SURVEY 8(d)'s bytes over the launch time; where they exceed the HBM peak (a cache-resident
+            # working set: the C4 mesh lives in the MALL) they are no roofline, and frac is the measured
+            # HBM traffic's fraction instead
             "achieved": achieved,
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
-            "frac": hbm_frac,
+            "frac": hbm_frac if (hbm_frac <= 1.0 or traffic_frac is None) else traffic_frac,
+            "frac_basis": "algorithmic bytes (SURVEY 8(d))" if (hbm_frac <= 1.0 or traffic_frac is None) else
+                          "measured HBM traffic (the SURVEY bytes model a cache-resident working set: %.2f of peak)" % hbm_frac,
             "atomic_frac": atomic_frac,
+            "issue_frac": issue_frac,
+            "valu_issue_peak": VALU_ISSUE_PEAK,
             "traffic": traffic["bytes_per_launch"] if traffic else None,
             "kernel": {0: "traceKernel<cartesian>", 1: "traceKernel<octree leaf map>", 2: "traceKernel<voronoi>"}[info.grid_kind],
             "launch_ms_avg": launch_s * 1e3,
@@ -274,7 +305,7 @@ def main():
             "engine_frac": engine_bytes / launch_s / 1e9 / HBM_PEAK_GBS,
             "traffic_source": traffic["source"] if traffic else None,
             "traffic_gbs": traffic["bytes_per_launch"] / launch_s / 1e9 if traffic else None,
-            "traffic_frac": traffic["bytes_per_launch"] / launch_s / 1e9 / HBM_PEAK_GBS if traffic else None,
+            "traffic_frac": traffic_frac,
             # Labs adds are scattered f64 atomics, executed memory-side in 64-byte requests at a fixed
             # chip-wide request rate (tools/atomic_bench.hip, profiles/r01_atomic_bench.txt); adds of one
             # wave instruction that fall in one line share a request
@@ -285,6 +316,26 @@ def main():
         },
         "phase_ms_avg": avg_kernel_s * 1e3,
     }
+    if world > 1:
+        # every rank's share of the work (its slice of every wavelength): segments and packets per rank
+        mine = torch.tensor([float(delta["packets"]), float(segs), elapsed], dtype=torch.float64, device="cuda")
+        every = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(every, mine)
+        result["per_rank"] = [{"rank": r, "packets": int(e[0].item()), "segments": int(e[1].item()),
+                               "elapsed_s": float(e[2].item())} for r, e in enumerate(every)]
+        result["config"]["dist_backend"] = args.dist_backend
+        if args.dist_backend != "nccl":
+            result["config"]["note"] = "gloo rehearsal: ranks share %d device(s); not a hardware scaling number" % (
+                torch.cuda.device_count())
+    if args.digest:
+        # the last step's tallies, already summed over the ranks by the engine's reducer
+        sim.fetch()
+        labs_l = sim.labs().sum(axis=0)
+        frames, seds = sim.instrument(0)
+        result["tally_digest"] = {"labs_per_lambda": [float(x) for x in labs_l],
+                                  "labs_total": float(labs_l.sum()),
+                                  "sed_total": float(seds.sum()) if seds is not None else None,
+                                  "frame_total": float(frames.sum()) if frames is not None else None}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         v, cores, sample = cpu_baseline(ski)
         result["cpu_baseline"] = {"value": v, "unit": "photon packets/s", "cores": cores, "kind": "port",

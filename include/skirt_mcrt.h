@@ -295,7 +295,11 @@ int skirt_mcrt_stats(SkirtMcrt* ctx, SkirtStats* out);
  * every peel-off path of the following phases counts one in bin min(segments, bins - 1), its number of
  * segments including those before the grid; zeroed by skirt_mcrt_zero_tallies; bins = 0 turns it off. */
 int skirt_mcrt_set_crossed(SkirtMcrt* ctx, int bins);
-/* the histogram summed over the device copies: hist[b] for b < bins (waits for the engine's stream) */
+/* the histogram summed over the device copies: hist[b] for b < bins (waits for the engine's stream).
+ * Per process, as in the reference: DustSystem::write (DustSystem.cpp:1004-1024) writes the root process's
+ * own _crossed through TextOutFile (root only, TextOutFile.cpp:24-25) and no sumResults covers it, so in a
+ * sharded run each rank's histogram counts the paths of its own slice (the ranks' histograms sum to the
+ * unsharded run's). */
 int skirt_mcrt_download_crossed(SkirtMcrt* ctx, uint64_t* hist, int bins);
 
 /* DustSystem::writeconvergence (DustSystem.cpp:195-250): the column density of the uploaded grid along n

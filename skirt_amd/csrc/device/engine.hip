@@ -231,7 +231,7 @@ constexpr int kVorCand = 4;  // possible winners the exact re-evaluation collect
 constexpr int kVorWideMax = SKIRT_VOR_WIDE;
 // slots after the last cell's block: a step loads whole groups of entries (kVorUnroll lane-serial, 16
 // for the first round of a neighbour-parallel step)
-constexpr int kVorPad = 2 * kVorUnroll > 16 ? 2 * kVorUnroll : 16;
+constexpr int kVorPad = 4 * kVorUnroll > 16 ? 4 * kVorUnroll : 16;  // a step loads up to 4 groups past its list
 
 // grid kinds of the kernels: SKIRT_GRID_CARTESIAN, SKIRT_GRID_OCTREE (leaf-map walk), the k-d tree
 // through its leaf map, and any tree walked through the node arrays (trees deeper than the leaf maps
@@ -1353,6 +1353,10 @@ struct Grid<SKIRT_GRID_VORONOI> {
         vorEntries(s.B, 0, e);
         vorEntries(s.B, kVorUnroll, f);
         if (!head(a, r, s, seg)) return false;
+        // The next groups are loaded unconditionally (a conditional load makes the compiler merge old and new
+        // values of the group's registers with moves at the join, and a move waits for its load: the loads
+        // then stalled right after issue instead of staying in flight). Past the list they read the next
+        // block, or the kVorPad slots after the last one; those entries are masked as invalid.
         for (int q0 = 0; q0 < s.cnt; q0 += 2 * kVorUnroll) {
 #pragma unroll
             for (int u = 0; u < kVorUnroll; u++) {
@@ -1360,7 +1364,7 @@ struct Grid<SKIRT_GRID_VORONOI> {
                 bounds(s, e[u], q0 + u < s.cnt, lo, uc);
                 take(b, lo, uc, e[u].next);
             }
-            if (q0 + 2 * kVorUnroll < s.cnt) vorEntries(s.B, q0 + 2 * kVorUnroll, e);
+            vorEntries(s.B, q0 + 2 * kVorUnroll, e);
             if (q0 + kVorUnroll < s.cnt) {
 #pragma unroll
                 for (int u = 0; u < kVorUnroll; u++) {
@@ -1368,8 +1372,8 @@ struct Grid<SKIRT_GRID_VORONOI> {
                     bounds(s, f[u], q0 + kVorUnroll + u < s.cnt, lo, uc);
                     take(b, lo, uc, f[u].next);
                 }
-                if (q0 + 3 * kVorUnroll < s.cnt) vorEntries(s.B, q0 + 3 * kVorUnroll, f);
             }
+            vorEntries(s.B, q0 + 3 * kVorUnroll, f);
         }
 #else
         VorEntry e[kVorUnroll];
@@ -2050,6 +2054,13 @@ __device__ __forceinline__ void traceBody(const Args& a) {
     // paths free at the end of a launch, instead of idling until the launch's longest path ends
     const unsigned int nfront = a.ctr[a.parity];
     if (nfront + a.ctr[8 + a.parity] == 0) return;  // an iteration after the end of the phase
+    // the front rays (growing up from 0) and the WALK rays (growing down from rayCap - 1) must not meet:
+    // the event and continuous peel-off kernels reserved them independently, so this is the first point
+    // where both totals are final; an overflow fails the phase instead of tracing overwritten records
+    if ((unsigned long long)nfront + a.ctr[8 + a.parity] > (unsigned long long)a.rayCap) {
+        if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(a.error, ERR_QUEUE);
+        return;
+    }
 #ifdef SKIRT_EXPERIMENT_TIMELINE
     const unsigned long long tlStart = __builtin_amdgcn_s_memrealtime();
     unsigned long long tlExhausted = 0, tlRays = 0;
@@ -2932,6 +2943,15 @@ __global__ void __launch_bounds__(kBlock) SKIRT_EVENT_ATTR eventKernel(const Arg
         unsigned long long ts3 = stamp();
         tlPart[2] += ts3 - ts2;
 #endif
+        // the queue holds rayCap records (ensurePool sizes it for the slots' most rays per iteration): a
+        // lane whose records would fall outside it writes none and fails the phase (ERR_QUEUE); the trace
+        // kernel checks that the front and the WALK region do not meet
+        if ((unsigned long long)pos + (unsigned)(nray - (back ? 1 : 0)) > (unsigned long long)a.rayCap ||
+            (back && wpos >= (unsigned)a.rayCap) ||
+            (unsigned long long)dpos + (unsigned)npeel > (unsigned long long)a.rayCap) {
+            atomicOr(a.error, ERR_QUEUE);
+            nray = 0;
+        }
         int inext = 0;  // next instrument to consider for a peel-off
         for (int k = 0; k < nray; k++) {
             double dx, dy, dz, prm;
@@ -3055,6 +3075,8 @@ __global__ void __launch_bounds__(kBlock) contKernel(const Args a) {
         }
         unsigned int pos = 0, dpos = 0, unused = 0;
         blockReserve3(a.ctr + a.parity, nray, pos, a.ctr + 7, 0u, unused, a.ctr + 5 + a.parity, nray, dpos, resv);
+        // (the WALK rays of the event kernel that follows are reserved from the queue's top later: the trace
+        // kernel checks that the two regions do not meet)
         if (nray && (pos + nray > (unsigned)a.rayCap || dpos + nray > (unsigned)(a.rayCap - a.nslots))) {
             atomicOr(a.error, ERR_QUEUE);  // cannot happen with the pool sized for kPathCap (ensurePool)
             nray = 0;

@@ -459,6 +459,13 @@ int skirt_sim_write(SkirtSim* s, const char* prefix) {
             std::vector<uint64_t> hist(kCrossedBins);
             int rc = check(s, skirt_mcrt_download_crossed(s->eng, hist.data(), kCrossedBins));
             if (rc) return rc;
+            // the last bin counts every longer path: the reference's _crossed grows without limit
+            // (DustSystem.cpp:969), so a path that reached it cannot be written as an exact count
+            if (hist[kCrossedBins - 1]) {
+                g_err = "ds_crossed: " + std::to_string(hist[kCrossedBins - 1]) + " paths crossed " +
+                         std::to_string(kCrossedBins - 1) + " or more cells, beyond the histogram's bins";
+                return SKIRT_ERR_UNSUPPORTED;
+            }
             writeCellsCrossed(s->m, prefix, hist);
         }
         if (s->m.hasDust && s->m.writeConvergence && s->eng) {

@@ -276,7 +276,10 @@ def test_engine_matches_reference_statistically(tmp_path, name):
     assert np.all(np.abs(z) < 5), z
     for col in (1, 2, 3, 4, 5, 6):  # total, direct, scattered, dust, dust scattered, transparent
         m, s = seds[:, :, col].mean(axis=0), seds[:, :, col].std(axis=0, ddof=1)
-        good = s > 0
+        # values below 1e-12 of the column's peak are the Wien tail of the dust emission (e.g. 1.8e-135 W/m2 at
+        # 0.77 micron against a 1.3e-15 peak): set by the few hottest cells, heavy-tailed from run to run (the
+        # reference's own pan_oct and pan_oct_cs runs differ there by a factor 340), so no z-score applies
+        good = (s > 0) & (m > 1e-12 * m.max())
         zz = (ref_sed[good, col] - m[good]) / (s[good] * infl)
         assert np.all(np.abs(zz) < 5), (col, zz)
 

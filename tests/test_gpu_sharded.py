@@ -83,3 +83,24 @@ def test_two_ranks_equal_one_run(tmp_path, via_host):
     frames, seds = full.instrument(0)
     np.testing.assert_allclose(load("seds"), seds, rtol=1e-9, atol=1e-300)
     np.testing.assert_allclose(load("frames").sum(axis=2), frames.sum(axis=2), rtol=1e-9, atol=1e-300)
+
+
+def test_crossed_histograms_of_the_shards_sum_to_the_whole():
+    """ds_crossed is per process, as in the reference (DustSystem::write writes the root process's own
+    _crossed, DustSystem.cpp:1004-1024; TextOutFile writes on the root only): each shard's histogram counts
+    the paths of its own slice, and the shards' histograms add up to the unsharded run's, bin for bin."""
+    ski = os.path.join(GOLD, "ski", "pan_oct.ski")
+    full = S.Simulation(ski, packages=600)
+    full.attach(0)
+    full.set_crossed()
+    full.run_stellar()
+    whole = full.crossed()
+    parts = []
+    for r in range(3):
+        sim = S.Simulation(ski, packages=600)
+        sim.attach(0)
+        sim.set_crossed()
+        sim.run_stellar_shard(r, 3)
+        parts.append(sim.crossed())
+        assert 0 < parts[-1].sum() < whole.sum()
+    assert np.array_equal(sum(parts), whole)

@@ -26,8 +26,11 @@ def checker(tmp_path_factory):
 # the checker's modes: n -- double bounds; f -- the round-2 float bounds; x -- per-entry Cauchy-Schwarz
 # terms; d -- the cell's largest terms from its header on the offsets n (round 3); r -- the device's step
 # (engine.hip Grid<SKIRT_GRID_VORONOI>::bounds: entries m = n / |n|^2 and the cell's terms, both computed by
-# the engine's own vor_terms.hpp)
-@pytest.mark.parametrize("mode", ["n", "f", "x", "d", "r"], ids=["f64", "f32_r2", "f32_entry", "f32_cell_terms", "device"])
+# the engine's own vor_terms.hpp); r+ / r- / r~ -- the device's step with its approximate reciprocal
+# (v_rcp_f32, 1 ulp) emulated: every reciprocal one ulp up, down, or each by a random -1 / 0 / +1 ulp
+@pytest.mark.parametrize("mode", ["n", "f", "x", "d", "r", "r+", "r-", "r~"],
+                         ids=["f64", "f32_r2", "f32_entry", "f32_cell_terms", "device", "device_rcp_up",
+                              "device_rcp_down", "device_rcp_random"])
 def test_compact_voronoi_step_is_exact(checker, mode):
     r = subprocess.run([checker, "20000", "3000", mode], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr

@@ -2,7 +2,8 @@
 
   profiles/<round>_rocprof_<cfg>_kernel_stats.csv   the --kernel-trace --stats summary, as written
   profiles/<round>_rocprof_<cfg>.txt                per-kernel averages of every PMC counter collected
-  profiles/pmc_<cfg>.json                           HBM bytes per traceKernel launch (read by bench.py)
+  profiles/pmc_<cfg>.json                           per traceKernel launch: HBM bytes, VALU/SALU wave-instructions,
+                                                    f64 atomic requests, GRBM_GUI_ACTIVE (read by bench.py)
 
 HBM bytes follow MI355X_MICROARCH.md (HBM section): FETCH_SIZE and WRITE_SIZE come from separate passes
 (they cannot share one on gfx950), in KiB; WRITE_SIZE is exact for 16-byte stores and for the f64
@@ -81,6 +82,13 @@ def main():
         d = {"kernel": "traceKernel", "fetch_size_kib": f, "write_size_kib": w,
              "traffic_bytes_per_launch": f * 1024 + w * 1024,
              "source": "profiles/%s_rocprof_%s.txt: FETCH_SIZE + WRITE_SIZE per traceKernel dispatch" % (rnd, cfg)}
+        # the issue and atomic counters of the same dispatches, where their passes ran
+        for key, cn in (("valu_insts_per_launch", "SQ_INSTS_VALU"), ("salu_insts_per_launch", "SQ_INSTS_SALU"),
+                        ("atomic_requests_per_launch", "TCC_EA0_ATOMIC_sum"), ("grbm_gui_active_per_launch", "GRBM_GUI_ACTIVE"),
+                        ("sq_waves_per_launch", "SQ_WAVES")):
+            v = avg.get(("traceKernel", cn))
+            if v is not None:
+                d[key] = v
         json.dump(d, open(os.path.join(prof, "pmc_%s.json" % cfg), "w"), indent=1)
         print(json.dumps(d))
     print("\n".join(lines))

@@ -7,7 +7,10 @@
 //   g++ -O2 -std=c++17 -ffp-contract=off -I include tools/vor_compact_check.cpp -L skirt_amd -lskirt_amd \
 //       -Wl,-rpath,$PWD/skirt_amd -o /tmp/vor_compact_check && /tmp/vor_compact_check 100000 20000 d
 // (mode r: the device's bounds on reciprocal entries m = n / |n|^2; d: round 3's bounds on the offsets n;
-// x: per-entry terms; f / e / c: round-2 float variants; none: double bounds)
+// x: per-entry terms; f / e / c: round-2 float variants; none: double bounds). The device takes 1/(m.k)
+// from v_rcp_f32 (__builtin_amdgcn_rcpf), accurate to 1 ulp: mode r+ / r- nudges every reciprocal one ulp
+// up / down, mode r~ each one by a pseudo-random -1, 0 or +1 ulp, so that the margin the device relies on
+// is what the walk checks.
 #include "../skirt_amd/csrc/device/vor_terms.hpp"
 #include <cfloat>
 #include <cmath>
@@ -72,6 +75,8 @@ bool gCell = false, gEntry = false;  // per-cell / per-entry-norm error bounds i
 bool gPerEntry = false;  // mode x: the first round-3 device step (per-entry terms)
 bool gDevice = false;                // the round-3 device step: per-entry Cauchy-Schwarz error terms
 bool gRecip = false;                 // mode r: the entries hold m = n / |n|^2 (the device's final step)
+int gRcpUlp = 0;                     // mode r+ / r- / r~: the approximate reciprocal's error (+1, -1, 2 = random)
+uint32_t gRcpState = 12345u;
 long gSignFallbacks = 0;  // re-evaluations with an entry whose n.k sign is uncertain
 long gWholeList = 0;      // re-evaluations over the whole list (more than 4 possible winners)
 float gLo[4096];          // the step's lower bounds, per list entry
@@ -161,7 +166,13 @@ static int compactStepF(const Mesh& M, int m, const double r[3], const double k[
                                      : fmaf(n2, 0.5f, fmaf(nz, Dz, fmaf(ny, Dy, nx * Dx)));
             const float eA = gPerEntry ? kEpsF * (fabsf(nx) + fabsf(ny) + fabsf(nz)) : M.eA[m];
             const float eB = gPerEntry ? fmaf(eA, Dn, kEpsF * n2) : fmaf(eA, Dn, M.eB[m]);
-            const float inv = 1.0f / den;
+            float inv = 1.0f / den;
+            if (gRcpUlp) {  // the device's v_rcp_f32 errs by up to 1 ulp
+                int u = gRcpUlp;
+                if (u == 2) { gRcpState = gRcpState * 1664525u + 1013904223u; u = (int)(gRcpState >> 30) % 3 - 1; }
+                if (u > 0) inv = nextafterf(inv, INFINITY);
+                if (u < 0) inv = nextafterf(inv, -INFINITY);
+            }
             const float sa = num * inv;
             const float err = fmaf(fmaf(fabsf(sa), 2.0f * eA, 2.0f * eB), inv, fabsf(sa) * kEpsF);
             (void)n2;
@@ -243,6 +254,7 @@ int main(int argc, char** argv) {
                                   argv[3][0] == 'x' || argv[3][0] == 'r');
     gDevice = argc > 3 && (argv[3][0] == 'd' || argv[3][0] == 'x' || argv[3][0] == 'r');
     gRecip = argc > 3 && argv[3][0] == 'r';
+    if (gRecip && argv[3][1]) gRcpUlp = argv[3][1] == '+' ? 1 : argv[3][1] == '-' ? -1 : 2;
     gPerEntry = argc > 3 && argv[3][0] == 'x';
     gCell = argc > 3 && argv[3][0] == 'c';
     gEntry = argc > 3 && argv[3][0] == 'e';
@@ -312,6 +324,7 @@ int main(int argc, char** argv) {
             m = a;
         }
     }
+    if (gRcpUlp) printf("reciprocals nudged: %s\n", gRcpUlp == 1 ? "+1 ulp" : gRcpUlp == -1 ? "-1 ulp" : "random -1/0/+1 ulp");
     printf("%s: sites %d, rays %d, steps %ld, exact re-evaluations %ld (%.3g per step), mismatches %ld\n",
            gRecip ? "f32 device bounds on reciprocal entries m = n/|n|^2 (per-cell terms)" :
            gPerEntry ? "f32 per-entry Cauchy-Schwarz bounds (round 3, first)" :
