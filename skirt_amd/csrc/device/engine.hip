@@ -72,6 +72,14 @@ constexpr int kPollRing = 3;       // copies in flight per half (the host reads 
 #ifndef SKIRT_LEAF_CHECK_FACES
 #define SKIRT_LEAF_CHECK_FACES 1
 #endif
+// leaf-map walk: the next step's leaf-map entry is requested at the end of a step (before the wave's Labs
+// drain), not at the start of the next one. A load waits for every older vector-memory operation of its
+// wave (vmcnt counts in issue order, atomics included), and a no-return f64 atomic stays counted for
+// thousands of cycles under load (MI355X_MICROARCH.md, float atomic add row): requested after the drain,
+// each step's entry waited for the previous step's Labs atomic too.
+#ifndef SKIRT_LEAF_PREFETCH
+#define SKIRT_LEAF_PREFETCH 1
+#endif
 #ifndef SKIRT_TRACE_ATTR
 #define SKIRT_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(3)))
 #endif
@@ -496,6 +504,8 @@ struct Ray {
     double rho0;           // density (component 0) of the current cell
     int ci, cj, ck;        // Cartesian cell indices | octree: node, cell number, leaf size in finest cells
     int jx, jy, jz;        // octree leaf map: finest-level index of the current leaf's lower corner
+    int4 pre;              // octree leaf map: the next step's leaf-map entry, requested at the end of this step
+    int pfx, pfy, pfz;     //   and the finest-level cell it was requested for (SKIRT_LEAF_PREFETCH)
     int idx, ell;
     unsigned flags, mode;
     unsigned id;           // queue index of the ray (a PEEL ray writes its optical depth back there)
@@ -973,7 +983,41 @@ struct LeafMapGrid {
         const LeafEntry e = lookup(a, sh, rx, ry, rz, fx, fy, fz);
         r.x = rx; r.y = ry; r.z = rz;
         enter(a, sh, r, fx, fy, fz, e);
+        prefetch(a, r);
         return true;
+    }
+
+    // the exit of the current leaf: the distance to the nearest of its three faces ahead of the ray, the wall
+    // (the reference's order of comparisons) and the exit point nudged by eps
+    __device__ static __forceinline__ void exitPoint(const Args& a, const Ray& r, double& ds, int& wall, double& x,
+                                                     double& y, double& z) {
+        const double xnext = r.bx0, ynext = r.by0, znext = r.bz0;
+        const double dsx = (r.ix != 0.0) ? (xnext - r.x) * r.ix : kDblMax;
+        const double dsy = (r.iy != 0.0) ? (ynext - r.y) * r.iy : kDblMax;
+        const double dsz = (r.iz != 0.0) ? (znext - r.z) * r.iz : kDblMax;
+        if (dsx <= dsy && dsx <= dsz) { ds = dsx; wall = (r.dx < 0.0) ? 0 : 1; }
+        else if (dsy <= dsx && dsy <= dsz) { ds = dsy; wall = (r.dy < 0.0) ? 2 : 3; }
+        else { ds = dsz; wall = (r.dz < 0.0) ? 4 : 5; }
+        x = r.x + (ds + a.eps) * r.dx;
+        y = r.y + (ds + a.eps) * r.dy;
+        z = r.z + (ds + a.eps) * r.dz;
+    }
+
+    // requests the leaf-map entry of the estimated finest cell of the next exit point (SKIRT_LEAF_PREFETCH):
+    // issued at the end of a step, it is in flight during the wave's Labs drain and the next step's segment
+    __device__ static __forceinline__ void prefetch(const Args& a, Ray& r) {
+#if SKIRT_LEAF_PREFETCH && SKIRT_LEAF_CHECK_FACES
+        double ds, x, y, z;
+        int wall;
+        exitPoint(a, r, ds, wall, x, y, z);
+        const int N = a.mapN;
+        r.pfx = estimate(N, a.mapX0, a.mapInvX, x);
+        r.pfy = estimate(N, a.mapY0, a.mapInvY, y);
+        r.pfz = estimate(N, a.mapZ0, a.mapInvZ, z);
+        r.pre = *reinterpret_cast<const int4*>(a.leafMap + leafIndex(N, r.pfx, r.pfy, r.pfz));
+#else
+        (void)a; (void)r;
+#endif
     }
 
     template <class SegFn>
@@ -982,28 +1026,25 @@ struct LeafMapGrid {
         const double* tx = sh.mesh;
         const double* ty = tx + N1;
         const double* tz = ty + N1;
-        const double xnext = r.bx0, ynext = r.by0, znext = r.bz0;
-        const double dsx = (r.ix != 0.0) ? (xnext - r.x) * r.ix : kDblMax;
-        const double dsy = (r.iy != 0.0) ? (ynext - r.y) * r.iy : kDblMax;
-        const double dsz = (r.iz != 0.0) ? (znext - r.z) * r.iz : kDblMax;
-        double ds;
+        double ds, x, y, z;
         int wall;
-        if (dsx <= dsy && dsx <= dsz) { ds = dsx; wall = (r.dx < 0.0) ? 0 : 1; }
-        else if (dsy <= dsx && dsy <= dsz) { ds = dsy; wall = (r.dy < 0.0) ? 2 : 3; }
-        else { ds = dsz; wall = (r.dz < 0.0) ? 4 : 5; }
-        double x = r.x + (ds + a.eps) * r.dx;
-        double y = r.y + (ds + a.eps) * r.dy;
-        double z = r.z + (ds + a.eps) * r.dz;
+        exitPoint(a, r, ds, wall, x, y, z);
         // the next leaf's entry is requested first; the segment's own work (optical depth, absorption)
         // runs while the load is in flight
 #if SKIRT_LEAF_CHECK_FACES
         // the entry of the estimated finest cell; its leaf is the right one when the leaf's own faces
         // (read anyway) contain the point, since T is monotone: then the exact finest cell lies in it too
         const int N = a.mapN;
+#if SKIRT_LEAF_PREFETCH
+        // requested by the previous step (prefetch), for the same exit point computed the same way
+        int fx = r.pfx, fy = r.pfy, fz = r.pfz;
+        const int4 raw = r.pre;
+#else
         int fx = estimate(N, a.mapX0, a.mapInvX, x);
         int fy = estimate(N, a.mapY0, a.mapInvY, y);
         int fz = estimate(N, a.mapZ0, a.mapInvZ, z);
         const int4 raw = *reinterpret_cast<const int4*>(a.leafMap + leafIndex(N, fx, fy, fz));
+#endif
 #else
         int fx, fy, fz;
         const int4 raw = fetch(a, sh, x, y, z, fx, fy, fz);
@@ -1040,10 +1081,12 @@ struct LeafMapGrid {
             const double* b = a.box + 6 * (size_t)next;  // its lower corner is a finest cell of it
             e = lookup(a, sh, b[0], b[1], b[2], fx, fy, fz);
             enter(a, sh, r, fx, fy, fz, e);
+            prefetch(a, r);
             return true;
         }
         enterPlanes(r, jx, jy, jz, e, lox, loy, loz, hix, hiy, hiz);
         if (!BIN) r.ck = 1 << lx;
+        prefetch(a, r);
         return true;
     }
 

@@ -221,7 +221,14 @@ def _isrf_cells(path, ncells):
     return J
 
 
-SEEDS = [101, 202, 303, 404, 505, 606, 707, 808]
+# the engine runs behind each reference comparison: the reference value is then a t variate with 15 degrees of
+# freedom in z = (ref - mean) / (sd * sqrt(1 + 1/K)); over the ~1,000 compared elements of the statistical
+# test, P(|t_15| > 7) = 4.6e-6 each (8 runs and a bound of 5 left ~1.6 chance exceedances per suite run).
+# Elements whose runs spread by more than half their mean are a few packets' events (the UV direct flux through
+# an optically thick disk, the Wien tail of the dust emission): heavy-tailed, so no z applies to them; the
+# same-stream tests against the oracle (which equals the reference bit for bit on these fixtures) cover them.
+SEEDS = [101 * (k + 1) for k in range(16)]
+Z_BOUND = 7.0
 
 
 def _engine_seed_runs(tmp_path, name, seeds=SEEDS):
@@ -263,7 +270,7 @@ STATISTICAL_MODELS = ["pan_cart16", "pan_oct", "pan_cart16_sa", "vor_pan", "pan_
 def test_engine_matches_reference_statistically(tmp_path, name):
     """All phases (stellar, self-absorption, dust emission) against `skirt -t 1`: per-wavelength ISRF sums
     and every SED column -- total, direct and scattered stellar, dust emission, dust scattered,
-    transparent -- as z-scores against the spread of 8 independently seeded engine runs."""
+    transparent -- as z-scores against the spread of 16 independently seeded engine runs."""
     J, seds = _engine_seed_runs(tmp_path, name)
     Jsum = J.sum(axis=1)
     ref_isrf, ref_sed_path = _reference_outputs(name)
@@ -271,17 +278,17 @@ def test_engine_matches_reference_statistically(tmp_path, name):
     ref_sed = F.read_text_table(ref_sed_path)
     infl = np.sqrt(1 + 1.0 / len(SEEDS))
     m, s = Jsum.mean(axis=0), Jsum.std(axis=0, ddof=1)
-    good = s > 0
+    good = (s > 0) & (s <= 0.5 * m)
     z = (ref_J[good] - m[good]) / (s[good] * infl)
-    assert np.all(np.abs(z) < 5), z
+    assert np.all(np.abs(z) < Z_BOUND), z
     for col in (1, 2, 3, 4, 5, 6):  # total, direct, scattered, dust, dust scattered, transparent
         m, s = seds[:, :, col].mean(axis=0), seds[:, :, col].std(axis=0, ddof=1)
         # values below 1e-12 of the column's peak are the Wien tail of the dust emission (e.g. 1.8e-135 W/m2 at
         # 0.77 micron against a 1.3e-15 peak): set by the few hottest cells, heavy-tailed from run to run (the
         # reference's own pan_oct and pan_oct_cs runs differ there by a factor 340), so no z-score applies
-        good = (s > 0) & (m > 1e-12 * m.max())
+        good = (s > 0) & (m > 1e-12 * m.max()) & (s <= 0.5 * m)
         zz = (ref_sed[good, col] - m[good]) / (s[good] * infl)
-        assert np.all(np.abs(zz) < 5), (col, zz)
+        assert np.all(np.abs(zz) < Z_BOUND), (col, zz)
 
 
 def _pools(J, max_rel_sd):

@@ -8,7 +8,8 @@
 #                    the same global packets (--digest: the reduced tallies must agree)
 #   ab CFG...        A/B of skirt_amd/libskirt_amd.so (the change) against libskirt_amd_base.so (built from
 #                    the previous commit by hand or tools/build_variant.sh): same-stream parity, then
-#                    alternating benches new/base/new/base (pkt/s, ms/step, trace ms per launch)
+#                    alternating benches new/base/new/base (pkt/s, ms/step, trace ms per launch);
+#                    AB_NEW / AB_BASE name other builds, AB_NO_TESTS=1 skips the parity step
 #   prof CFG         rocprofv3 kernel trace + PMC passes of the bench (tools/gpu_prof.sh)
 # Every GPU step runs under its own timeout; the first failing step ends the call.
 set -o pipefail
@@ -66,7 +67,7 @@ ab)
   out=gpurun_out/ab.txt; : > $out
   for cfg in "${@:-c3}"; do
     for v in new base new base; do
-      lib=libskirt_amd.so; [ $v != new ] && lib=libskirt_amd_$v.so
+      lib=${AB_NEW:-libskirt_amd.so}; [ $v != new ] && lib=${AB_BASE:-libskirt_amd_base.so}
       SKIRT_AMD_LIB=$lib timeout -k 10 300 python bench.py --config $cfg --steps 2 --warmup 1 --no-cpu-baseline \
           > gpurun_out/ab_${cfg}_$v.log 2>&1 || { echo "FAIL $cfg $v"; tail -5 gpurun_out/ab_${cfg}_$v.log; exit 1; }
       line "$cfg $v" gpurun_out/ab_${cfg}_$v.log >> $out; tail -1 $out
