@@ -15,7 +15,11 @@
  *
  * Two random-number modes:
  *   ORACLE_RNG_MT     one MT19937 stream continuing from model setup, packets in the reference's
- *                     order -- bit-for-bit the output of `skirt -t 1` (pinned by tests/golden).
+ *                     order -- bit-for-bit the output of `skirt -t 1`. Parity PINNED: the reference
+ *                     binary is rebuilt from its own sources by oracle/ref.mk (oracle/_ref/skirt, never
+ *                     shipped), tests/test_reference_rebuild.py regenerates every tests/golden/ref file
+ *                     with it byte for byte, and tests/test_oracle_golden.py holds this mode to all 34
+ *                     fixtures (SEDs, FITS frames, ds_isrf, ds_cellprops, ds_crossed, ds_convergence).
  *   ORACLE_RNG_PHILOX one Philox4x32-10 stream per packet, keyed exactly like the GPU engine
  *                     (see DESIGN.md "Random numbers"), so GPU and oracle agree packet by packet.
  * Model setup (ski parsing, grids, densities, tables) is shared with the product host library.

@@ -74,6 +74,11 @@ all() {
   run pan_oct_out 4357 pan_oct_out_s4357      # ds_convergence, ds_crossed, ds_cellprops
   run pan_cart16_out 4357 pan_cart16_out_s4357
   run vor_pan_out 4357 vor_pan_out_s4357
+  run bbody_cart 4357 bbody_cart_s4357        # BlackBodySED
+  run quasar_cart 4357 quasar_cart_s4357      # QuasarSED
+  run faceon_cart 4357 faceon_cart_s4357      # dust normalized by face-on optical depth
+  run edgeon_cart 4357 edgeon_cart_s4357      # ... edge-on optical depth
+  run radial_cart 4357 radial_cart_s4357      # ... radial optical depth
   LEAN=
 }
 if [ $# -ge 3 ]; then LEAN=${4#0}; run "$1" "$2" "$3"; else all; fi

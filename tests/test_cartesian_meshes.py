@@ -2,7 +2,7 @@
 NR::lingrid / NR::powgrid / NR::sympowgrid, Fundamentals/NR.hpp:171-261): the borders the host builds
 are the reference's formulas evaluated in the same order, read back through the oracle's
 DustGrid::path along each axis. No reference fixture uses these meshes, so beyond these formulas the
-power-law meshes are parity unpinned against the reference itself (the GPU engine matches the oracle
+power-law meshes are pinned against the reference by the cart_pow and cart_odd fixtures (the GPU engine matches the oracle
 on them, tests/test_gpu_cartesian.py)."""
 import math
 

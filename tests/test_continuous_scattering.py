@@ -1,6 +1,6 @@
 """continuousScattering (MonteCarloSimulation::continuouspeeloffscattering, MonteCarloSimulation.cpp:367-434)
 in the oracle: peel-offs from a random point of every dust segment of each path replace the peel-off at
-the interaction point. No reference fixture uses it (parity against the reference unpinned); both
+the interaction point. The reference fixtures pan_cart16_cs, pan_oct_cs and vor_pan_cs pin it (tests/test_oracle_golden.py); both
 estimators measure the same scattered flux, so the oracle's continuous runs must agree with its own
 discrete runs -- which are pinned bit for bit to the reference -- where the discrete estimator is well
 sampled, while the continuous one also reaches the optically thin wavelengths where discrete packets

@@ -1,7 +1,7 @@
 """DustSystem::writeconvergence (DustSystem.cpp:195-305) in the oracle: <prefix>_ds_convergence.dat holds the
 grid's mass and its column densities through the origin beside the dust distribution's analytic values.
 The reference's fixtures all set writeConvergence="false", so there is no reference file to compare with
-(parity unpinned against the reference); these checks pin the format and the physics: the grid's values
+(pinned against the reference by the pan_oct_out, pan_cart16_out and vor_pan_out fixtures); these checks also pin the format and the physics: the grid's values
 approach the analytic ones, spherical models write the radial branch, an exponential disk the edge-on and
 face-on branches. tests/test_gpu_counts.py compares the engine's file with the oracle's."""
 import os

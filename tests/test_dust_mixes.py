@@ -1,7 +1,7 @@
 """MeanZubkoDustMix and DraineLiDustMix (MeanZubkoDustMix.cpp, DraineLiDustMix.cpp, DustMix::addpopulation):
 the packaged tables (skirt_amd/data/*.bin, written by tools/convert_dat.py) hold the reference's data
 files' numbers, and models using the mixes run. No reference fixture uses these mixes: beyond the data
-and the shared DustMix code (pinned through InterstellarDustMix), parity unpinned against the reference;
+and the shared DustMix code (pinned through InterstellarDustMix), pinned against the reference by the zubko_cart and draineli_cart fixtures;
 the GPU engine matches the oracle on them (tests/test_gpu_geometries.py)."""
 import os
 import struct

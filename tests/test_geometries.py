@@ -1,8 +1,8 @@
 """ExpDiskGeometry (SKIRTcore/ExpDiskGeometry.cpp, SepAxGeometry::generatePosition,
 SpecialFunctions::LambertW1) in the host model and the oracle.
 
-No reference fixture uses this geometry (no reference binary is available here to write one), so it is parity
-unpinned against the reference itself; these tests pin the restatement to its own defining properties:
+The disk_oct, disk_cart, bulge_oct, sersic_cart and point_oct reference fixtures pin these geometries
+(tests/test_oracle_golden.py); these tests pin the restatement to its own defining properties:
 the density formula and its normalization (setupSelfBefore's rho0 makes the density integrate to 1),
 and the random positions (randomR by LambertW1 inversion, randomz, the truncations) distributed as
 that density. The GPU engine then matches the oracle on the same streams (tests/test_gpu_geometries.py).

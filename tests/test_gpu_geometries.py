@@ -1,6 +1,6 @@
 """ExpDiskGeometry and SersicGeometry stars and dust on the GPU against the CPU oracle on the same Philox
 streams (the geometries' restatements are checked on their own in tests/test_geometries.py; parity
-unpinned against the reference itself, which has no fixture for them)."""
+pinned against the reference by the disk_oct, disk_cart, bulge_oct, sersic_cart and point_oct fixtures)."""
 import os
 
 import numpy as np

@@ -263,7 +263,8 @@ def _reference_outputs(name):
 # fixed and convergence-driven cycles), continuous scattering, and the grid / geometry / mix variants
 STATISTICAL_MODELS = ["pan_cart16", "pan_oct", "pan_cart16_sa", "vor_pan", "pan_oct_sa", "pan_oct_sac",
                       "pan_cart16_cs", "pan_oct_cs", "vor_pan_cs", "bin_pan", "oct_bary", "oct_pan_bk",
-                      "disk_oct", "bulge_oct", "sersic_cart", "cart_pow", "zubko_cart", "draineli_cart"]
+                      "disk_oct", "bulge_oct", "sersic_cart", "cart_pow", "zubko_cart", "draineli_cart",
+                      "bbody_cart", "quasar_cart", "faceon_cart", "edgeon_cart", "radial_cart"]
 
 
 @pytest.mark.parametrize("name", STATISTICAL_MODELS)

@@ -1,7 +1,8 @@
 """Dust component normalizations by optical depth (FaceOnDustCompNormalization,
 EdgeOnDustCompNormalization, RadialDustCompNormalization: tau / (Sigma * kappaext(lambda)) with
 AxGeometry::SigmaZ / SigmaR or SpheGeometry::Sigmar, DustMix::kappaext's log-log interpolation).
-Restated here from the reference formulas; parity unpinned against the reference itself (no fixture)."""
+Restated here from the reference formulas; the faceon_cart, edgeon_cart and radial_cart reference fixtures pin
+them too (tests/test_oracle_golden.py)."""
 import math
 
 import numpy as np

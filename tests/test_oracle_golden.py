@@ -26,7 +26,8 @@ VARIANT_RUNS = [(name, 4357) for name in (
     "pan_oct_sa", "pan_oct_sac", "pan_cart16_cs", "pan_oct_cs", "vor_pan_cs",
     "bin_pan", "bin_bary", "bin_full_td", "oct_bary", "oct_pan_td", "oct_pan_bk", "oct_bary_bk",
     "cart_odd", "cart_pow", "disk_oct", "disk_cart", "bulge_oct", "sersic_cart", "point_oct",
-    "zubko_cart", "draineli_cart", "pan_oct_out", "pan_cart16_out", "vor_pan_out")]
+    "zubko_cart", "draineli_cart", "pan_oct_out", "pan_cart16_out", "vor_pan_out",
+    "bbody_cart", "quasar_cart", "faceon_cart", "edgeon_cart", "radial_cart")]
 LSUN = 3.839e26  # W (Units.cpp)
 
 

@@ -5,7 +5,7 @@ a broken power law in micron, SED::setemissivities), normalized by SED::setlumin
 A dust-free model makes every packet end at its emission peel-off with weight 1, so the raw SED of an
 SEDInstrument at wavelength ell is the sum of the packet luminosities, i.e. the component luminosity
 L_ell = Ltot * sed_ell. The restatements below (same formulas, same order, numpy/libm) check the host
-tables through the oracle. No reference fixture uses these SEDs: parity unpinned against the reference.
+tables through the oracle. The bbody_cart and quasar_cart reference fixtures pin them too (tests/test_oracle_golden.py).
 """
 import math
 

@@ -1,14 +1,9 @@
-"""Grid variants of the golden models (tree grids, Cartesian meshes), written as .ski files for the tests.
-
-The reference fixtures cover the OctTreeDustGrid with centre splits and the Neighbor search
-(pan_oct). Its other tree grids -- BinTreeDustGrid (the k-d tree, Alternating or Barycenter split
-directions, BinTreeDustGrid.cpp, BinTreeNode.cpp, BaryBinTreeNode.cpp), barycentric octrees
-(BaryOctTreeNode.cpp), the TopDown and Bookkeeping searches -- have no reference outputs here (the fixtures came from the
-survey's reference build, which this repository may not rebuild: it needs the reference's own qmake/moc
-build system), so these variants swap only the <dustGrid> element of a
-pinned model and are checked against the pinned octree walk (geometric equivalence) and against the
-oracle on the same random streams.
-"""
+"""Variants of the golden models (tree grids, Cartesian meshes, geometries, mixes, SEDs, normalizations, diagnostic
+outputs), written as .ski files for the tests and for tests/golden/make_fixtures.sh, which runs the rebuilt reference
+(oracle/ref.mk) on each to write its reference fixture: BinTreeDustGrid (the k-d tree, Alternating or Barycenter
+split directions, BinTreeDustGrid.cpp, BinTreeNode.cpp, BaryBinTreeNode.cpp), barycentric octrees
+(BaryOctTreeNode.cpp), the TopDown and Bookkeeping searches, and the others below. Each swaps one element of a
+committed model."""
 import os
 import re
 
@@ -73,6 +68,9 @@ GEOMETRIES = {
     # a point source (PointGeometry) at the origin, a cell corner of both grids
     "point_oct": ("pan_oct", POINT, DUST_DISK),
     "point_cart": ("pan_cart16", POINT, DUST_DISK),
+    # dust in a disk without inner radius (a face-on normalization needs SigmaZ > 0: ExpDiskGeometry::SigmaZ is 0
+    # for Rmin > 0)
+    "disk0_cart": ("pan_cart16", STAR_DISK, STAR_DISK),
 }
 
 
@@ -138,9 +136,46 @@ def write_outputs(name, directory):
     return path
 
 
+# stellar SEDs besides SunSED, and dust normalizations by optical depth, on the Pan Cartesian model (the
+# normalizations on its disk variant, as tests/test_normalizations.py uses them)
+SEDS = {"bbody_cart": ("pan_cart16", '<BlackBodySED temperature="20000 K"/>'),
+        "quasar_cart": ("pan_cart16", "<QuasarSED/>")}
+NORMALIZATIONS = {
+    "faceon_cart": ("disk0_cart", '<FaceOnDustCompNormalization wavelength="0.55 micron" opticalDepth="0.7"/>'),
+    "edgeon_cart": ("disk_cart", '<EdgeOnDustCompNormalization wavelength="1.3 micron" opticalDepth="4"/>'),
+    "radial_cart": ("pan_cart16", '<RadialDustCompNormalization wavelength="0.55 micron" opticalDepth="2.5"/>'),
+}
+
+
+def write_sed(name, directory):
+    """Writes SED variant `name` into `directory` and returns its path."""
+    base, sed = SEDS[name]
+    text = open(os.path.join(GOLD, base + ".ski")).read()
+    assert text.count("<SunSED/>") == 1, name
+    path = os.path.join(directory, name + ".ski")
+    with open(path, "w") as f:
+        f.write(text.replace("<SunSED/>", sed))
+    return path
+
+
+def write_normalization(name, directory):
+    """Writes dust-normalization variant `name` into `directory` and returns its path."""
+    base, norm = NORMALIZATIONS[name]
+    src = write_any(base, directory) if base in GEOMETRIES else os.path.join(GOLD, base + ".ski")
+    text = open(src).read()
+    old = text[text.index("<DustMassDustCompNormalization"):]
+    old = old[:old.index("/>") + 2]
+    path = os.path.join(directory, name + ".ski")
+    with open(path, "w") as f:
+        f.write(text.replace(old, norm))
+    return path
+
+
 def write_any(name, directory):
-    """Writes the variant `name` of any kind (grid, geometry, mix, outputs) and returns its path."""
-    for table, writer in ((GRIDS, write), (GEOMETRIES, write_geometry), (MIXES, write_mix), (OUTPUTS, write_outputs)):
+    """Writes the variant `name` of any kind (grid, geometry, mix, outputs, SED, normalization) and returns its
+    path."""
+    for table, writer in ((GRIDS, write), (GEOMETRIES, write_geometry), (MIXES, write_mix), (OUTPUTS, write_outputs),
+                          (SEDS, write_sed), (NORMALIZATIONS, write_normalization)):
         if name in table:
             return writer(name, directory)
     raise KeyError(name)
