@@ -314,6 +314,7 @@ struct Args {
     int store, hasDust;
     // tallies
     double* labs;                // [nlambda][labsStride], device cell order
+    unsigned labsBytes;          // its size (< 4 GiB: the trace kernel addresses it through a buffer descriptor)
     double* tally;
     unsigned int* error;
     unsigned long long* stats;   // packets, seg_fill, seg_walk, seg_peel, detects, absorbs, lane slots
@@ -428,6 +429,19 @@ __device__ __forceinline__ void atomicAddF64(double* p, double v) {
     // explicit global address space: global_atomic_add_f64 instead of a flat atomic
     __hip_atomic_fetch_add((__attribute__((address_space(1))) double*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+
+// The trace kernel's Labs drain as buffer atomics (buffer_atomic_add_f64 through a raw buffer descriptor of
+// the Labs table): every lane of the drain instruction issues, the lanes without an add at an offset past
+// the table, which the buffer range check drops (tools/buffer_atomic_oob.hip). A global atomic under
+// `if (lane has an add)` is a branch the compiler's waitcnt pass cannot see through: the next load of the
+// walk then waited with vmcnt(0), i.e. for the drain's atomics too, which stay counted for thousands of
+// cycles under load (MI355X_MICROARCH.md, float atomic add row). With a fixed count of vector-memory
+// operations per step the load that the previous step requested is waited for alone.
+#ifndef SKIRT_LABS_BUFFER_ATOMICS
+#define SKIRT_LABS_BUFFER_ATOMICS 1
+#endif
+__device__ double bufferAtomicAddF64(double v, __amdgpu_buffer_rsrc_t rsrc, int voffset, int soffset, int aux)
+    __asm("llvm.amdgcn.raw.ptr.buffer.atomic.fadd.f64");
 
 // the small tables staged in LDS
 struct Shared {
@@ -1396,10 +1410,9 @@ struct Grid<SKIRT_GRID_VORONOI> {
         vorEntries(s.B, 0, e);
         vorEntries(s.B, kVorUnroll, f);
         if (!head(a, r, s, seg)) return false;
-        // The next groups are loaded unconditionally (a conditional load makes the compiler merge old and new
-        // values of the group's registers with moves at the join, and a move waits for its load: the loads
-        // then stalled right after issue instead of staying in flight). Past the list they read the next
-        // block, or the kVorPad slots after the last one; those entries are masked as invalid.
+        // (the next groups are loaded only while the list lasts: loading them unconditionally -- past the list
+        // into the next block -- let the compiler drop the register moves at the join, but made C4 24 % slower,
+        // 9.53e7 -> 7.37e7 pkt/s, profiles/r04_ab_c4_vor_uncond_loads_c3c5_prefetch.txt)
         for (int q0 = 0; q0 < s.cnt; q0 += 2 * kVorUnroll) {
 #pragma unroll
             for (int u = 0; u < kVorUnroll; u++) {
@@ -1407,7 +1420,7 @@ struct Grid<SKIRT_GRID_VORONOI> {
                 bounds(s, e[u], q0 + u < s.cnt, lo, uc);
                 take(b, lo, uc, e[u].next);
             }
-            vorEntries(s.B, q0 + 2 * kVorUnroll, e);
+            if (q0 + 2 * kVorUnroll < s.cnt) vorEntries(s.B, q0 + 2 * kVorUnroll, e);
             if (q0 + kVorUnroll < s.cnt) {
 #pragma unroll
                 for (int u = 0; u < kVorUnroll; u++) {
@@ -1415,8 +1428,8 @@ struct Grid<SKIRT_GRID_VORONOI> {
                     bounds(s, f[u], q0 + kVorUnroll + u < s.cnt, lo, uc);
                     take(b, lo, uc, f[u].next);
                 }
+                if (q0 + 3 * kVorUnroll < s.cnt) vorEntries(s.B, q0 + 3 * kVorUnroll, f);
             }
-            vorEntries(s.B, q0 + 3 * kVorUnroll, f);
         }
 #else
         VorEntry e[kVorUnroll];
@@ -1542,6 +1555,9 @@ struct Tracer {
     // atomic round trip per burst instead of one per step.
     double* pendVal;    // LDS, [kLabsBuf][kBlock]
     unsigned* pendIdx;  // LDS, [kLabsBuf][kBlock]
+#if SKIRT_LABS_BUFFER_ATOMICS
+    __amdgpu_buffer_rsrc_t labsRsrc;  // the Labs table as a raw buffer of labsBytes (SKIRT_LABS_BUFFER_ATOMICS)
+#endif
     int npend = 0;
     unsigned gstep = 0;  // grid steps of the wave (drainStep's round robin)
 
@@ -1613,6 +1629,10 @@ struct Tracer {
 #endif
 #ifdef SKIRT_EXPERIMENT_NO_LABS_ATOMICS  // tuning experiment only: the cost of the Labs atomics
         if (j < n && pendVal[q] == -1.0) atomicAddF64(a.labs + idx, pendVal[q]);
+#elif SKIRT_LABS_BUFFER_ATOMICS
+        // every lane issues; a lane without an add adds 0 at the first byte past the table (dropped)
+        const double v = j < n ? pendVal[q] : 0.0;
+        bufferAtomicAddF64(v, labsRsrc, (int)(j < n ? idx * 8u : a.labsBytes), 0, 0);
 #else
         if (j < n) atomicAddF64(a.labs + idx, pendVal[q]);
 #endif
@@ -2111,6 +2131,9 @@ __device__ __forceinline__ void traceBody(const Args& a) {
     Shared sh = stageTables(a, lds, gridParts<GRID>() | STAGE_OPTICS);
 
     Tracer<GRID, ONECOMP, CONT> T{a, sh};
+#if SKIRT_LABS_BUFFER_ATOMICS
+    T.labsRsrc = __builtin_amdgcn_make_buffer_rsrc(a.labs, 0, (int)a.labsBytes, 0x00020000);
+#endif
     T.pendVal = lds + a.ldsInstrOff;  // after the grid and optics tables
     T.pendIdx = reinterpret_cast<unsigned*>(lds + a.ldsInstrOff + kLabsBuf * kBlock);
     T.waveSegs = T.pendIdx + kLabsBuf * kBlock;
@@ -4423,8 +4446,12 @@ static int runPhase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, uint6
     a.store = phase == SKIRT_PHASE_STELLAR ? (p->store_absorption ? 1 : 0) : (phase == SKIRT_PHASE_DUST_SELFABS ? 1 : 0);
     a.hasDust = p->has_dust ? 1 : 0;
     if (a.store && !c->dLabs) return fail(c, SKIRT_ERR_STATE, "no Labs buffer");
-    if ((uint64_t)c->labsStride * (uint64_t)c->nlambda >= (1ull << 32)) return fail(c, SKIRT_ERR_UNSUPPORTED, "Labs table exceeds 2^32 entries");
+    // the trace kernel addresses Labs through a buffer descriptor (32-bit byte offsets, one byte past the end
+    // for the drain's empty lanes): at most 4 GiB - 8 (e.g. 2^21 cells x 255 wavelengths)
+    if ((uint64_t)c->labsStride * (uint64_t)c->nlambda * sizeof(double) > 0xfffffff8ull)
+        return fail(c, SKIRT_ERR_UNSUPPORTED, "Labs table larger than 4 GiB");
     a.labs = phase == SKIRT_PHASE_DUST_SELFABS ? c->dLabsDust : c->dLabs;
+    a.labsBytes = (unsigned)((size_t)c->labsStride * c->nlambda * sizeof(double));
     a.tally = c->dTally;
     a.error = c->dError; a.stats = c->dStats;
     a.crossed = c->dCrossed; a.crossedBins = c->crossedBins;
