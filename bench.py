@@ -207,17 +207,20 @@ def main():
         elapsed = float(t.item())
 
     delta = {k: sum(st[k] for st in per_step) for k in ("packets", "segments_fill", "segments_walk", "segments_peel",
-                                                        "detects", "absorb_adds", "lane_slots", "labs_requests")}
+                                                        "detects", "absorb_adds", "lane_slots", "labs_requests",
+                                                        "packages")}
     delta["trace_ms"] = s1["trace_ms"] - s0["trace_ms"]
     delta["trace_launches"] = s1["trace_launches"] - s0["trace_launches"]
     trace_ms, trace_launches = delta["trace_ms"], delta["trace_launches"]
-    packets_all = ppl * world * info.nlambda * args.steps
-    if dust_phases:
-        # every phase's launched packets (stellar, self-absorption cycles, dust emission), all ranks
-        n = torch.tensor([float(delta["packets"])], dtype=torch.float64, device="cuda")
-        if world > 1:
-            dist.all_reduce(n)
-        packets_all = float(n.item())
+    # one unit for every config, SURVEY 8(d)'s: the packages x wavelengths of every phase the step ran (stellar;
+    # C5 also its self-absorption cycles and dust emission), launched or not, over all ranks; the packets
+    # actually launched (wavelengths and cells without luminosity launch none) are reported beside it
+    n = torch.tensor([float(delta["packages"])], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(n)
+    packets_all = float(n.item())
+    if packets_all == 0 and not dust_phases:  # a library from before SkirtStats::packages (A/B against old builds)
+        packets_all = float(ppl * world * info.nlambda * args.steps)
     value = packets_all / elapsed
     launched = torch.tensor([float(delta["packets"])], dtype=torch.float64, device="cuda")
     if world > 1:
@@ -263,10 +266,11 @@ def main():
             "device_cells": s1["device_cells"],
             "wavelengths": info.nlambda,
             "packets_per_step_per_gpu": share,
-            # BASELINE.md section 2 counts packages x wavelengths; the stellar SED emits nothing at the
-            # longest wavelengths, whose packets the reference (dostellaremissionchunk) and the engine
-            # skip alike. The rate of packets actually launched:
+            # value counts packages x wavelengths of every phase; the
+            # stellar SED emits nothing at the longest wavelengths, whose packets the reference
+            # (dostellaremissionchunk) and the engine skip alike. The rate of packets actually launched:
             "launched_packets_per_s": launched_rate,
+            "packages_per_step": packets_all / args.steps,
             "parallelism": "dp%d (packet sharding, RCCL all-reduce of Labs + instrument tallies per phase)" % world,
             "segments_per_packet": segs / max(1, delta["packets"]),
             "lane_use": (delta["segments_fill"] + delta["segments_walk"] + delta["segments_peel"]) / max(1, delta["lane_slots"]),

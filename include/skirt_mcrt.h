@@ -185,6 +185,10 @@ typedef struct {
                                    one wave instruction share a request) */
     uint64_t device_cells;      /* device cell numbers, >= ncells (octree sibling groups start on a line) */
     uint64_t trace_blocks_per_cu; /* trace-kernel workgroups per CU the last phase ran (register and LDS bound) */
+    uint64_t packages;          /* packet indices shot, launched or not (per phase: the slice's packages x
+                                   wavelengths; wavelengths or cells without luminosity launch none):
+                                   SURVEY 8(d)'s throughput unit, summed over the phases since the last
+                                   skirt_mcrt_zero_tallies */
 } SkirtStats;
 
 /* grid walks of the trace kernel (SkirtStats::grid_walk) */

@@ -39,7 +39,7 @@ class SkirtStats(ctypes.Structure):
                 ("iterations", ctypes.c_uint64), ("kernel_ms", ctypes.c_double), ("trace_ms", ctypes.c_double),
                 ("trace_launches", ctypes.c_uint64), ("grid_walk", ctypes.c_int32), ("map_level", ctypes.c_int32),
                 ("labs_requests", ctypes.c_uint64), ("device_cells", ctypes.c_uint64),
-                ("trace_blocks_per_cu", ctypes.c_uint64)]
+                ("trace_blocks_per_cu", ctypes.c_uint64), ("packages", ctypes.c_uint64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -237,6 +237,17 @@ constexpr int kVorCand = 4;  // possible winners the exact re-evaluation collect
 #define SKIRT_VOR_WIDE 0
 #endif
 constexpr int kVorWideMax = SKIRT_VOR_WIDE;
+// the trace kernel's Labs drain as unconditional buffer atomics (see bufferAtomicAddF64)
+#ifndef SKIRT_LABS_BUFFER_ATOMICS
+#define SKIRT_LABS_BUFFER_ATOMICS 1
+#endif
+// Voronoi walk: the Labs drain as two unconditional instructions per step, issued between the step's loads
+// and their use (Tracer::drainStep2, Grid<SKIRT_GRID_VORONOI>::stepLoad/stepRest), instead of a burst of
+// kLabsBuf instructions whenever a lane's buffer fills up, which the next step's header then waited for
+#ifndef SKIRT_VOR_SPLIT_DRAIN
+#define SKIRT_VOR_SPLIT_DRAIN 1
+#endif
+constexpr bool kVorSplitDrain = SKIRT_VOR_SPLIT_DRAIN && SKIRT_LABS_BUFFER_ATOMICS && kVorWideMax == 0;
 // slots after the last cell's block: a step loads whole groups of entries (kVorUnroll lane-serial, 16
 // for the first round of a neighbour-parallel step)
 constexpr int kVorPad = 4 * kVorUnroll > 16 ? 4 * kVorUnroll : 16;  // a step loads up to 4 groups past its list
@@ -437,9 +448,6 @@ __device__ __forceinline__ void atomicAddF64(double* p, double v) {
 // walk then waited with vmcnt(0), i.e. for the drain's atomics too, which stay counted for thousands of
 // cycles under load (MI355X_MICROARCH.md, float atomic add row). With a fixed count of vector-memory
 // operations per step the load that the previous step requested is waited for alone.
-#ifndef SKIRT_LABS_BUFFER_ATOMICS
-#define SKIRT_LABS_BUFFER_ATOMICS 1
-#endif
 __device__ double bufferAtomicAddF64(double v, __amdgpu_buffer_rsrc_t rsrc, int voffset, int soffset, int aux)
     __asm("llvm.amdgcn.raw.ptr.buffer.atomic.fadd.f64");
 
@@ -1287,6 +1295,11 @@ struct Grid<SKIRT_GRID_VORONOI> {
         const double2 h0 = *reinterpret_cast<const double2*>(s.B);
         const double2 h1 = *reinterpret_cast<const double2*>(s.B + 1);
         const int4 h2 = *reinterpret_cast<const int4*>(s.B + 2);
+        return headFrom(a, r, s, h0, h1, h2, seg);
+    }
+    template <class SegFn>
+    __device__ static __forceinline__ bool headFrom(const Args& a, Ray& r, StepIn& s, const double2& h0, const double2& h1,
+                                                    const int4& h2, SegFn seg) {
         s.pwx = h0.x; s.pwy = h0.y; s.pwz = h1.x; s.rhow = h1.y;
         s.idw = h2.x; s.cnt = h2.y;
         const float eA = __int_as_float(h2.z), eBn = __int_as_float(h2.w);  // the cell's terms (upload)
@@ -1397,8 +1410,34 @@ struct Grid<SKIRT_GRID_VORONOI> {
     // the block of the cell the ray is in. A step issues one round of loads (this cell's header and first
     // entries) in the common case. It adds at most two segments (the pending one, and one more when the
     // bounds leave several possible winners), see kSegsPerStep.
+    // the loads a step starts with: the cell's header and its first two groups of entries (one round)
+    struct Load {
+        double2 h0, h1;
+        int4 h2;
+        VorEntry e[kVorUnroll], f[kVorUnroll];
+    };
+    __device__ static __forceinline__ void stepLoad(const Args& a, const Ray& r, Load& L, bool act = true) {
+        // lanes without a ray load block 0: an unconditional load needs no merge of old and new register
+        // values (moves, which would wait for the loads right after their issue)
+        const VorEntry* B = a.vorSlots + (act ? r.cj : 0);
+        L.h0 = *reinterpret_cast<const double2*>(B);
+        L.h1 = *reinterpret_cast<const double2*>(B + 1);
+        L.h2 = *reinterpret_cast<const int4*>(B + 2);
+        vorEntries(B, 0, L.e);
+        vorEntries(B, kVorUnroll, L.f);
+    }
+
     template <class SegFn>
-    __device__ static __forceinline__ bool step(const Args& a, const Shared&, Ray& r, SegFn seg) {
+    __device__ static __forceinline__ bool step(const Args& a, const Shared& sh, Ray& r, SegFn seg) {
+        Load L;
+        stepLoad(a, r, L);
+        return stepRest(a, sh, r, L, seg);
+    }
+
+    // the step from its loads (stepLoad): the trace kernel issues the Labs drain between the two, so the
+    // header's wait does not include the drain's atomics (vmcnt counts in issue order)
+    template <class SegFn>
+    __device__ static __forceinline__ bool stepRest(const Args& a, const Shared&, Ray& r, Load& L, SegFn seg) {
         StepIn s;
         s.B = a.vorSlots + r.cj;
         Best b{FLT_MAX, FLT_MAX, FLT_MAX, 0};
@@ -1406,10 +1445,9 @@ struct Grid<SKIRT_GRID_VORONOI> {
         // two groups of entries in flight: the first two load with the header, and each group's next load
         // is issued as soon as the group is consumed, so a cell with more than kVorUnroll neighbours does
         // not wait for a second round trip
-        VorEntry e[kVorUnroll], f[kVorUnroll];
-        vorEntries(s.B, 0, e);
-        vorEntries(s.B, kVorUnroll, f);
-        if (!head(a, r, s, seg)) return false;
+        VorEntry (&e)[kVorUnroll] = L.e;
+        VorEntry (&f)[kVorUnroll] = L.f;
+        if (!headFrom(a, r, s, L.h0, L.h1, L.h2, seg)) return false;
         // (the next groups are loaded only while the list lasts: loading them unconditionally -- past the list
         // into the next block -- let the compiler drop the register moves at the join, but made C4 24 % slower,
         // 9.53e7 -> 7.37e7 pkt/s, profiles/r04_ab_c4_vor_uncond_loads_c3c5_prefetch.txt)
@@ -1432,9 +1470,8 @@ struct Grid<SKIRT_GRID_VORONOI> {
             }
         }
 #else
-        VorEntry e[kVorUnroll];
-        vorEntries(s.B, 0, e);
-        if (!head(a, r, s, seg)) return false;
+        VorEntry (&e)[kVorUnroll] = L.e;
+        if (!headFrom(a, r, s, L.h0, L.h1, L.h2, seg)) return false;
         for (int q0 = 0; q0 < s.cnt; q0 += kVorUnroll) {
             if (q0) vorEntries(s.B, q0, e);
 #pragma unroll
@@ -1647,6 +1684,17 @@ struct Tracer {
         const int i = (int)(gstep++ & (kLabsBuf - 1));
         issue(i);
         if (((threadIdx.x & 63) / G) == i) npend = 0;
+    }
+
+    // Two drain instructions per grid step, for walks that add up to two segments per step (Voronoi): every
+    // lane's buffer is emptied every kLabsBuf / 2 steps, which holds its at most kLabsBuf adds.
+    __device__ __forceinline__ void drainStep2() {
+        constexpr int G = 64 / kLabsBuf;
+        const int i = (int)((gstep++ & (kLabsBuf / 2 - 1)) * 2);
+        issue(i);
+        issue(i + 1);
+        const int grp = (threadIdx.x & 63) / G;
+        if (grp == i || grp == i + 1) npend = 0;
     }
 
     __device__ __forceinline__ double rho(int m, int h) const { return a.rho[(size_t)m * a.ncomp + h]; }
@@ -2207,6 +2255,19 @@ __device__ __forceinline__ void traceBody(const Args& a) {
                     if (__ballot(T.npend > kLabsBuf - kSegsPerStep<GRID>)) T.drain();
                     continue;
                 }
+            }
+            if constexpr (GRID == SKIRT_GRID_VORONOI && kVorSplitDrain) {
+                // the step's loads, then the wave's two drain instructions, then the rest of the step: the
+                // header's wait then covers the loads only (SKIRT_VOR_SPLIT_DRAIN)
+                typename Grid<GRID>::Load L;
+                const bool act = r.mode != RAY_NONE;
+                Grid<GRID>::stepLoad(a, r, L, act);
+                T.drainStep2();
+                if (act && !Grid<GRID>::stepRest(a, sh, r, L, seg)) {
+                    T.finish(r);
+                    r.mode = RAY_NONE;
+                }
+                continue;
             }
             if (r.mode != RAY_NONE) {
                 if (!Grid<GRID>::step(a, sh, r, seg)) {
@@ -3239,6 +3300,10 @@ struct SkirtMcrt {
     // sources
     int nstar = 0;
     double *dGeomParam = nullptr, *dLum = nullptr, *dLumtot = nullptr, *dCdf = nullptr;
+    // the first and last wavelength with stellar luminosity: a stellar phase shoots only the packet indices of
+    // [lumLo, lumHi] (the others launch nothing, MonteCarloSimulation.cpp:272-273; each packet's stream is
+    // keyed by its own index, so skipping them changes no other packet)
+    int lumLo = 0, lumHi = -1;
     double* dGeomTable = nullptr;  // SersicGeometry tables, kSersicTable per component
     double emissionBias = 0.5;
     // dust-phase cell sources and the dust Labs tally
@@ -3292,6 +3357,7 @@ struct SkirtMcrt {
     double lastMs = 0;
     std::vector<hipEvent_t> traceEv;  // pairs around the trace launches not yet timed
     int traceLaunches = 0;
+    uint64_t packagesTotal = 0;       // packet indices of the phases run since the last zero_tallies (SkirtStats::packages)
     double traceMs = 0;               // all timed trace launches since the context was created
     uint64_t traceLaunchesTotal = 0;
     int numCUs = 0;
@@ -4025,6 +4091,13 @@ int skirt_mcrt_upload_sources(SkirtMcrt* c, const SkirtSourceDesc* s) {
     }
     if ((rc = upload(c, c->dLum, s->lum, (size_t)s->ncomp * s->nlambda))) return rc;
     if ((rc = upload(c, c->dLumtot, s->lumtot, (size_t)s->nlambda))) return rc;
+    c->lumLo = 0;
+    c->lumHi = -1;
+    for (int ell = 0; ell < s->nlambda; ell++)
+        if (s->lumtot[ell] > 0) {
+            if (c->lumHi < 0) c->lumLo = ell;
+            c->lumHi = ell;
+        }
     if ((rc = upload(c, c->dCdf, s->cdf, (size_t)s->nlambda * (s->ncomp + 1)))) return rc;
     return SKIRT_OK;
 }
@@ -4126,6 +4199,7 @@ int skirt_mcrt_zero_tallies(SkirtMcrt* c) {
     if (c->dCrossed)
         HIPCHECK(c, hipMemsetAsync(c->dCrossed, 0, (size_t)kCrossedCopies * c->crossedBins * sizeof(unsigned long long), c->stream));
     c->instrReduced = false;
+    c->packagesTotal = 0;
     return SKIRT_OK;
 }
 
@@ -4391,6 +4465,16 @@ static int runPhase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, uint6
             if (hipEventElapsedTime(&ms, c->traceEv[2 * k], c->traceEv[2 * k + 1]) == hipSuccess) c->traceMs += ms;
         c->traceLaunchesTotal += (uint64_t)c->traceLaunches;
         c->traceLaunches = 0;
+    }
+    c->packagesTotal += count;
+    if (!cellPhase) {
+        // the wavelengths outside [lumLo, lumHi] launch nothing: their packet indices (per wavelength sliceCnt
+        // of them, wavelength-slowest) are left out of the phase instead of being claimed and skipped one by one
+        const uint64_t lo = c->lumHi < 0 ? 0 : (uint64_t)c->lumLo * sliceCnt;
+        const uint64_t hi = c->lumHi < 0 ? 0 : (uint64_t)(c->lumHi + 1) * sliceCnt;
+        const uint64_t b = std::max(first, lo), e = std::min(first + count, hi);
+        first = b;
+        count = e > b ? e - b : 0;
     }
     if (count == 0) return SKIRT_OK;
     if (!c->dOptics) {  // a dust-free simulation still stages (zero) optical tables
@@ -4849,6 +4933,7 @@ int skirt_mcrt_stats(SkirtMcrt* c, SkirtStats* out) {
     out->labs_requests = v[7];
     out->device_cells = c->ndev;
     out->trace_blocks_per_cu = (uint64_t)c->traceBlocksPerCU;
+    out->packages = c->packagesTotal;
     return SKIRT_OK;
 }
 
