@@ -234,7 +234,9 @@ def main():
     launch_s = trace_ms / max(1, trace_launches) / 1e3
     bytes_per_launch = trace_bytes / max(1, trace_launches)
     achieved = bytes_per_launch / launch_s / 1e9
-    traffic = pmc_traffic(args.config)
+    # the PMC passes were taken on this config's own bench command (its default packets per rank); another
+    # launch size would misprice them
+    traffic = pmc_traffic(args.config) if ppl == ppl_default else None
     hbm_frac = achieved / HBM_PEAK_GBS
     traffic_frac = traffic["bytes_per_launch"] / launch_s / 1e9 / HBM_PEAK_GBS if traffic else None
     # instruction issue: VALU wave-instructions per second (PMC) over the chip's issue peak

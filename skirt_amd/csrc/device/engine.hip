@@ -225,8 +225,14 @@ constexpr bool kLabsSmooth = SKIRT_LABS_SMOOTH;
 #define SKIRT_EXACT_ATTENUATION 1  // exp(-tau) per FILL segment, as the reference (0: the running product)
 #endif
 #ifndef SKIRT_VOR_PIPE
-#define SKIRT_VOR_PIPE 1  // two groups of entries in flight per step (see Grid<SKIRT_GRID_VORONOI>::step)
+#define SKIRT_VOR_PIPE 1  // groups of entries in flight per step (see Grid<SKIRT_GRID_VORONOI>::step)
 #endif
+#ifndef SKIRT_VOR_GROUPS
+// how many (SKIRT_VOR_PIPE): loaded with the header, each reloaded once consumed. 3: C4 trace launch
+// 23.64 -> 23.19 ms, 9.64e7 -> 9.89e7 pkt/s (4: the same as 3), profiles/r04_ktrace_groups_nolicm.txt
+#define SKIRT_VOR_GROUPS 3
+#endif
+constexpr int kVorGroups = SKIRT_VOR_PIPE ? SKIRT_VOR_GROUPS : 1;
 #ifndef SKIRT_VOR_FALLBACK_GROUP
 #define SKIRT_VOR_FALLBACK_GROUP 2  // neighbour sites loaded together by the exact re-evaluation (<= kVorUnroll)
 #endif
@@ -250,7 +256,8 @@ constexpr int kVorWideMax = SKIRT_VOR_WIDE;
 constexpr bool kVorSplitDrain = SKIRT_VOR_SPLIT_DRAIN && SKIRT_LABS_BUFFER_ATOMICS && kVorWideMax == 0;
 // slots after the last cell's block: a step loads whole groups of entries (kVorUnroll lane-serial, 16
 // for the first round of a neighbour-parallel step)
-constexpr int kVorPad = 4 * kVorUnroll > 16 ? 4 * kVorUnroll : 16;  // a step loads up to 4 groups past its list
+constexpr int kVorPadGroups = kVorGroups + 2 > 4 ? kVorGroups + 2 : 4;
+constexpr int kVorPad = kVorPadGroups * kVorUnroll > 16 ? kVorPadGroups * kVorUnroll : 16;  // a step loads whole groups past its list
 
 // grid kinds of the kernels: SKIRT_GRID_CARTESIAN, SKIRT_GRID_OCTREE (leaf-map walk), the k-d tree
 // through its leaf map, and any tree walked through the node arrays (trees deeper than the leaf maps
@@ -448,8 +455,10 @@ __device__ __forceinline__ void atomicAddF64(double* p, double v) {
 // walk then waited with vmcnt(0), i.e. for the drain's atomics too, which stay counted for thousands of
 // cycles under load (MI355X_MICROARCH.md, float atomic add row). With a fixed count of vector-memory
 // operations per step the load that the previous step requested is waited for alone.
+}  // namespace (the intrinsic's declaration has external linkage)
 __device__ double bufferAtomicAddF64(double v, __amdgpu_buffer_rsrc_t rsrc, int voffset, int soffset, int aux)
     __asm("llvm.amdgcn.raw.ptr.buffer.atomic.fadd.f64");
+namespace {
 
 // the small tables staged in LDS
 struct Shared {
@@ -1410,11 +1419,11 @@ struct Grid<SKIRT_GRID_VORONOI> {
     // the block of the cell the ray is in. A step issues one round of loads (this cell's header and first
     // entries) in the common case. It adds at most two segments (the pending one, and one more when the
     // bounds leave several possible winners), see kSegsPerStep.
-    // the loads a step starts with: the cell's header and its first two groups of entries (one round)
+    // the loads a step starts with: the cell's header and its first kVorGroups groups of entries (one round)
     struct Load {
         double2 h0, h1;
         int4 h2;
-        VorEntry e[kVorUnroll], f[kVorUnroll];
+        VorEntry g[kVorGroups][kVorUnroll];
     };
     __device__ static __forceinline__ void stepLoad(const Args& a, const Ray& r, Load& L, bool act = true) {
         // lanes without a ray load block 0: an unconditional load needs no merge of old and new register
@@ -1423,8 +1432,8 @@ struct Grid<SKIRT_GRID_VORONOI> {
         L.h0 = *reinterpret_cast<const double2*>(B);
         L.h1 = *reinterpret_cast<const double2*>(B + 1);
         L.h2 = *reinterpret_cast<const int4*>(B + 2);
-        vorEntries(B, 0, L.e);
-        vorEntries(B, kVorUnroll, L.f);
+#pragma unroll
+        for (int gi = 0; gi < kVorGroups; gi++) vorEntries(B, gi * kVorUnroll, L.g[gi]);
     }
 
     template <class SegFn>
@@ -1442,35 +1451,30 @@ struct Grid<SKIRT_GRID_VORONOI> {
         s.B = a.vorSlots + r.cj;
         Best b{FLT_MAX, FLT_MAX, FLT_MAX, 0};
 #if SKIRT_VOR_PIPE
-        // two groups of entries in flight: the first two load with the header, and each group's next load
-        // is issued as soon as the group is consumed, so a cell with more than kVorUnroll neighbours does
-        // not wait for a second round trip
-        VorEntry (&e)[kVorUnroll] = L.e;
-        VorEntry (&f)[kVorUnroll] = L.f;
+        // kVorGroups groups of entries in flight: they load with the header, and each group's next load is
+        // issued as soon as the group is consumed, so a cell with more than kVorUnroll neighbours does not
+        // wait for a second round trip
         if (!headFrom(a, r, s, L.h0, L.h1, L.h2, seg)) return false;
         // (the next groups are loaded only while the list lasts: loading them unconditionally -- past the list
         // into the next block -- let the compiler drop the register moves at the join, but made C4 24 % slower,
         // 9.53e7 -> 7.37e7 pkt/s, profiles/r04_ab_c4_vor_uncond_loads_c3c5_prefetch.txt)
-        for (int q0 = 0; q0 < s.cnt; q0 += 2 * kVorUnroll) {
+        constexpr int NG = kVorGroups;
+        for (int q0 = 0; q0 < s.cnt; q0 += NG * kVorUnroll) {
 #pragma unroll
-            for (int u = 0; u < kVorUnroll; u++) {
-                float lo, uc;
-                bounds(s, e[u], q0 + u < s.cnt, lo, uc);
-                take(b, lo, uc, e[u].next);
-            }
-            if (q0 + 2 * kVorUnroll < s.cnt) vorEntries(s.B, q0 + 2 * kVorUnroll, e);
-            if (q0 + kVorUnroll < s.cnt) {
+            for (int gi = 0; gi < NG; gi++) {
+                const int qb = q0 + gi * kVorUnroll;
+                if (gi > 0 && qb >= s.cnt) break;
 #pragma unroll
                 for (int u = 0; u < kVorUnroll; u++) {
                     float lo, uc;
-                    bounds(s, f[u], q0 + kVorUnroll + u < s.cnt, lo, uc);
-                    take(b, lo, uc, f[u].next);
+                    bounds(s, L.g[gi][u], qb + u < s.cnt, lo, uc);
+                    take(b, lo, uc, L.g[gi][u].next);
                 }
-                if (q0 + 3 * kVorUnroll < s.cnt) vorEntries(s.B, q0 + 3 * kVorUnroll, f);
+                if (qb + NG * kVorUnroll < s.cnt) vorEntries(s.B, qb + NG * kVorUnroll, L.g[gi]);
             }
         }
 #else
-        VorEntry (&e)[kVorUnroll] = L.e;
+        VorEntry (&e)[kVorUnroll] = L.g[0];
         if (!headFrom(a, r, s, L.h0, L.h1, L.h2, seg)) return false;
         for (int q0 = 0; q0 < s.cnt; q0 += kVorUnroll) {
             if (q0) vorEntries(s.B, q0, e);
@@ -3083,7 +3087,7 @@ __global__ void __launch_bounds__(kBlock) SKIRT_EVENT_ATTR eventKernel(const Arg
         for (int k = 0; k < nray; k++) {
             double dx, dy, dz, prm;
             int idx;
-            unsigned flags;
+            unsigned flags, at;
             if (k < npeel) {
                 int i = inext, l;
                 while (true) {  // the next instrument that receives this peel-off
@@ -3112,17 +3116,15 @@ __global__ void __launch_bounds__(kBlock) SKIRT_EVENT_ATTR eventKernel(const Arg
                 // grid leaves tau = 0)
                 idx = (int)(dpos + k);
                 a.det[idx] = DetRec{Lp, 0.0, l, flags};
+                at = pos++;
             } else {
                 dx = p.kx; dy = p.ky; dz = p.kz;
                 prm = mainParam;
                 idx = slot;
                 flags = mainMode | ((unsigned)p.ell << 18);
-                if (back) {
-                    E.emitRay((unsigned)a.rayCap - 1u - wpos, p, dx, dy, dz, prm, idx, flags, vcell);
-                    continue;
-                }
+                at = back ? (unsigned)a.rayCap - 1u - wpos : pos++;
             }
-            E.emitRay(pos++, p, dx, dy, dz, prm, idx, flags, vcell);
+            E.emitRay(at, p, dx, dy, dz, prm, idx, flags, vcell);  // (one call site: one inlined grid entry)
         }
         // the slot stays active while it has a FILL/WALK ray in flight
         if (active) actOut[apos] = slot;

@@ -6,7 +6,7 @@ tag=$1; shift
 cd "$(dirname "$0")/../skirt_amd/csrc"
 HOST="build/xml.o build/units.o build/build.o build/outputs.o build/dustemission.o build/voronoi.o build/sim.o"
 make -s $HOST
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -munsafe-fp-atomics -ffp-contract=off "$@" \
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -munsafe-fp-atomics -ffp-contract=off -mllvm -disable-machine-licm "$@" \
     -c -o build/engine_$tag.o ${SRC:-device/engine.hip}
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o ../libskirt_amd_$tag.so build/engine_$tag.o \
     $HOST -ldl -lpthread

@@ -10,6 +10,9 @@
 #                    the previous commit by hand or tools/build_variant.sh): same-stream parity, then
 #                    alternating benches new/base/new/base (pkt/s, ms/step, trace ms per launch);
 #                    AB_NEW / AB_BASE name other builds, AB_NO_TESTS=1 skips the parity step
+#   multi CFG...     MULTI_LIBS="tagA tagB" (- = the default library): alternating benches of several builds;
+#                    MULTI_TESTS=1 runs the same-stream parity tests on each first
+#   ktrace CFG...    MULTI_LIBS as for multi: per-kernel average times (rocprofv3 kernel trace) of each build
 #   prof CFG         rocprofv3 kernel trace + PMC passes of the bench (tools/gpu_prof.sh)
 # Every GPU step runs under its own timeout; the first failing step ends the call.
 set -o pipefail
@@ -71,6 +74,50 @@ ab)
       SKIRT_AMD_LIB=$lib timeout -k 10 300 python bench.py --config $cfg --steps 2 --warmup 1 --no-cpu-baseline \
           > gpurun_out/ab_${cfg}_$v.log 2>&1 || { echo "FAIL $cfg $v"; tail -5 gpurun_out/ab_${cfg}_$v.log; exit 1; }
       line "$cfg $v" gpurun_out/ab_${cfg}_$v.log >> $out; tail -1 $out
+    done
+  done ;;
+multi)
+  # MULTI_LIBS="tagA tagB ..." (libskirt_amd_TAG.so; "-" = libskirt_amd.so): same-stream parity of each
+  # (MULTI_TESTS=1), then two alternating bench rounds over the libraries per config
+  libs=${MULTI_LIBS:?}; out=gpurun_out/multi.txt; : > $out
+  libof() { [ "$1" = - ] && echo libskirt_amd.so || echo libskirt_amd_$1.so; }
+  if [ -n "${MULTI_TESTS:-}" ]; then
+    for t in $libs; do
+      SKIRT_AMD_LIB=$(libof $t) TAILN=2 run multi_tests_$t 600 python -u -m pytest -x -q --timeout 200 --timeout-method thread \
+          -m gpu tests/test_gpu_parity.py tests/test_gpu_counts.py -k "same_streams or counts or crossed" || exit 1
+    done
+  fi
+  [ -n "${MULTI_TESTS:-}" ] && [ $# -eq 0 ] && exit 0  # tests only
+  for cfg in "${@:-c3}"; do
+    v=MULTI_LIBS_$cfg; cl=${!v:-$libs}  # MULTI_LIBS_c4=... : another set for one config
+    for rep in 1 2; do
+      for t in $cl; do
+        SKIRT_AMD_LIB=$(libof $t) timeout -k 10 300 python bench.py --config $cfg --steps 2 --warmup 1 --no-cpu-baseline \
+            > gpurun_out/multi_${cfg}_${t}_$rep.log 2>&1 || { echo "FAIL $cfg $t"; tail -5 gpurun_out/multi_${cfg}_${t}_$rep.log; exit 1; }
+        line "$cfg $t" gpurun_out/multi_${cfg}_${t}_$rep.log >> $out; tail -1 $out
+      done
+    done
+  done ;;
+ktrace)
+  # MULTI_LIBS as for multi: a rocprofv3 kernel trace of one short bench per library and config, the
+  # per-kernel averages side by side (gpurun_out/ktrace.txt)
+  libs=${MULTI_LIBS:?}; out=gpurun_out/ktrace.txt; : > $out
+  libof() { [ "$1" = - ] && echo libskirt_amd.so || echo libskirt_amd_$1.so; }
+  for cfg in "${@:-c3}"; do
+    v=MULTI_LIBS_$cfg; cl=${!v:-$libs}
+    for t in $cl; do
+      d=gpurun_out/kt_${cfg}_$t
+      SKIRT_AMD_LIB=$(libof $t) timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $d -o run -- \
+          python3 bench.py --config $cfg --steps 2 --warmup 1 --no-cpu-baseline > $d.log 2>&1 || { echo "FAIL $cfg $t"; tail -5 $d.log; exit 1; }
+      python3 - "$cfg $t" $d >> $out <<'PY'
+import csv, glob, re, sys
+rows = list(csv.DictReader(open(glob.glob(sys.argv[2] + "/**/*kernel_stats.csv", recursive=True)[0])))
+short = lambda n: re.search(r"\w+Kernel\w*(<[^>]*>)?", n).group(0).replace(" ", "")
+parts = ["%s %.3f ms x %s" % (short(r["Name"]), float(r["AverageNs"]) / 1e6, r["Calls"]) for r in rows
+         if any(k in r["Name"] for k in ("traceKernel", "eventKernel", "detectKernel", "contKernel"))]
+print("%-16s %s" % (sys.argv[1], " | ".join(parts)))
+PY
+      tail -1 $out
     done
   done ;;
 prof)
