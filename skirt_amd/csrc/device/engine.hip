@@ -248,10 +248,12 @@ constexpr int kVorWideMax = SKIRT_VOR_WIDE;
 #define SKIRT_LABS_BUFFER_ATOMICS 1
 #endif
 // Voronoi walk: the Labs drain as two unconditional instructions per step, issued between the step's loads
-// and their use (Tracer::drainStep2, Grid<SKIRT_GRID_VORONOI>::stepLoad/stepRest), instead of a burst of
-// kLabsBuf instructions whenever a lane's buffer fills up, which the next step's header then waited for
+// and their use (Tracer::drainStep2, Grid<SKIRT_GRID_VORONOI>::stepLoad/stepRest), instead of the drain
+// every grid kind runs (kLabsSmooth: one instruction per step). With two entry groups in flight and the
+// branchy drain this took C4 from 9.53e7 to 9.63e7 pkt/s; with three groups, buffer atomics and no machine
+// LICM it is 1.8 % slower (trace launch 23.21 against 22.80 ms, profiles/r04_c4_variants.txt): off
 #ifndef SKIRT_VOR_SPLIT_DRAIN
-#define SKIRT_VOR_SPLIT_DRAIN 1
+#define SKIRT_VOR_SPLIT_DRAIN 0
 #endif
 constexpr bool kVorSplitDrain = SKIRT_VOR_SPLIT_DRAIN && SKIRT_LABS_BUFFER_ATOMICS && kVorWideMax == 0;
 // slots after the last cell's block: a step loads whole groups of entries (kVorUnroll lane-serial, 16

@@ -12,6 +12,7 @@
 #                    AB_NEW / AB_BASE name other builds, AB_NO_TESTS=1 skips the parity step
 #   multi CFG...     MULTI_LIBS="tagA tagB" (- = the default library): alternating benches of several builds;
 #                    MULTI_TESTS=1 runs the same-stream parity tests on each first
+#   envs CFG...      ENV_SETS="-|VAR=1|VAR=2 OTHER=3": alternating benches of the default build under settings
 #   ktrace CFG...    MULTI_LIBS as for multi: per-kernel average times (rocprofv3 kernel trace) of each build
 #   prof CFG         rocprofv3 kernel trace + PMC passes of the bench (tools/gpu_prof.sh)
 # Every GPU step runs under its own timeout; the first failing step ends the call.
@@ -25,7 +26,7 @@ line() {  # line LABEL LOG: the bench line's headline numbers
 import json, sys
 r = json.loads([l for l in open(sys.argv[2]) if l.startswith("{")][-1])
 f = r["roofline"]
-print("%-14s %.4e pkt/s  %.1f ms/step  trace %.3f ms x %.0f  frac %.3f  atomic %.3f" % (
+print("%-24s %.4e pkt/s  %.1f ms/step  trace %.3f ms x %.0f  frac %.3f  atomic %.3f" % (
     sys.argv[1], r["value"], r["ms_per_step"], f["launch_ms_avg"], f["launches_per_step"], f["frac"], f["atomic_frac"]))
 PY
 }
@@ -95,6 +96,21 @@ multi)
         SKIRT_AMD_LIB=$(libof $t) timeout -k 10 300 python bench.py --config $cfg --steps 2 --warmup 1 --no-cpu-baseline \
             > gpurun_out/multi_${cfg}_${t}_$rep.log 2>&1 || { echo "FAIL $cfg $t"; tail -5 gpurun_out/multi_${cfg}_${t}_$rep.log; exit 1; }
         line "$cfg $t" gpurun_out/multi_${cfg}_${t}_$rep.log >> $out; tail -1 $out
+      done
+    done
+  done ;;
+envs)
+  # ENV_SETS="-|SKIRT_AMD_EVENT_BPC=3|..." ("-": none): two alternating bench rounds per config over engine
+  # environment settings (gpurun_out/envs.txt)
+  out=gpurun_out/envs.txt; : > $out
+  IFS='|' read -ra sets <<< "${ENV_SETS:?}"
+  for cfg in "${@:-c3}"; do
+    for rep in 1 2; do
+      for e in "${sets[@]}"; do
+        tag=$(echo "$e" | tr -c 'A-Za-z0-9=\n' _)
+        ( [ "$e" != - ] && export $e; timeout -k 10 300 python bench.py --config $cfg --steps 2 --warmup 1 --no-cpu-baseline ) \
+            > gpurun_out/envs_${cfg}_${tag}_$rep.log 2>&1 || { echo "FAIL $cfg $e"; tail -5 gpurun_out/envs_${cfg}_${tag}_$rep.log; exit 1; }
+        line "$cfg $e" gpurun_out/envs_${cfg}_${tag}_$rep.log >> $out; tail -1 $out
       done
     done
   done ;;
