@@ -42,7 +42,10 @@ enum {
     SKIRT_ERR_HIP = 2,       /* a HIP runtime call failed */
     SKIRT_ERR_STATE = 3,     /* call order violated (e.g. run before upload) */
     SKIRT_ERR_NUMERIC = 4,   /* "optical depth along the path is not a positive number" (DustSystem.cpp:976-979) */
-    SKIRT_ERR_UNSUPPORTED = 5
+    SKIRT_ERR_UNSUPPORTED = 5  /* a model outside the engine's limits, e.g. a Labs table (cells x wavelengths,
+                                  f64) above 4 GiB, a Voronoi mesh above 2^31 slots, tables that do not fit
+                                  one workgroup's LDS, or (skirt_sim_write) a path reaching the last
+                                  ds_crossed bin; the message names the limit and the sizes */
 };
 
 enum { SKIRT_GRID_CARTESIAN = 0, SKIRT_GRID_OCTREE = 1, SKIRT_GRID_VORONOI = 2 };

@@ -12,7 +12,8 @@
 #                    AB_NEW / AB_BASE name other builds, AB_NO_TESTS=1 skips the parity step
 #   multi CFG...     MULTI_LIBS="tagA tagB" (- = the default library): alternating benches of several builds;
 #                    MULTI_TESTS=1 runs the same-stream parity tests on each first
-#   envs CFG...      ENV_SETS="-|VAR=1|VAR=2 OTHER=3": alternating benches of the default build under settings
+#   envs CFG...      ENV_SETS="-|VAR=1|VAR=2 OTHER=3|-::--slots 16777216": alternating benches of the default
+#                    build under environment settings and extra bench.py arguments (after "::")
 #   ktrace CFG...    MULTI_LIBS as for multi: per-kernel average times (rocprofv3 kernel trace) of each build
 #   prof CFG         rocprofv3 kernel trace + PMC passes of the bench (tools/gpu_prof.sh)
 # Every GPU step runs under its own timeout; the first failing step ends the call.
@@ -108,7 +109,8 @@ envs)
     for rep in 1 2; do
       for e in "${sets[@]}"; do
         tag=$(echo "$e" | tr -c 'A-Za-z0-9=\n' _)
-        ( [ "$e" != - ] && export $e; timeout -k 10 300 python bench.py --config $cfg --steps 2 --warmup 1 --no-cpu-baseline ) \
+        envpart=${e%%::*}; argpart=; [[ "$e" == *::* ]] && argpart=${e#*::}
+        ( [ "$envpart" != - ] && [ -n "$envpart" ] && export $envpart; timeout -k 10 300 python bench.py --config $cfg --steps 2 --warmup 1 --no-cpu-baseline $argpart ) \
             > gpurun_out/envs_${cfg}_${tag}_$rep.log 2>&1 || { echo "FAIL $cfg $e"; tail -5 gpurun_out/envs_${cfg}_${tag}_$rep.log; exit 1; }
         line "$cfg $e" gpurun_out/envs_${cfg}_${tag}_$rep.log >> $out; tail -1 $out
       done
