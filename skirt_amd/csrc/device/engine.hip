@@ -4486,10 +4486,11 @@ static int runPhase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, uint6
         if ((rc = upload(c, c->dOptics, z.data(), z.size()))) return rc;
     }
     // slot pool: enough packets in flight to fill the chip many times over, bounded by the phase size.
-    // 2^23 slots (3.3 GB of packet state and ray queues with one instrument) make each iteration's trace
-    // launch long enough that its drain tail and the event kernel amortise (C3: 2^21 slots 1.87e8 pkt/s,
-    // 2^22 1.98e8, 2^23 2.04e8, 2^24 2.05e8; tools/archive/gpu_sweep3.sh)
-    int slots = c->slotsWanted > 0 ? c->slotsWanted : (1 << 23);
+    // 2^24 slots (6.6 GB of packet state and ray queues with one instrument) make each iteration's trace
+    // launch long enough that its drain tail and the event kernel amortise (round 1, C3: 2^21 slots 1.87e8
+    // pkt/s, 2^22 1.98e8, 2^23 2.04e8, 2^24 2.05e8; round 4 at the configurations' sizes, 2^24 against
+    // 2^23: C3 +1.5 %, C2 +0.7 %, C4 +0.7 %, C5 +0.3 %, profiles/r04_slots_2e24.txt)
+    int slots = c->slotsWanted > 0 ? c->slotsWanted : (1 << 24);
     // continuous scattering (MonteCarloSimulation::continuousScattering): peel-offs from every dust segment
     // of every path replace the ones at the interaction points; fewer slots, each with a longer queue
     const bool continuous = p->continuous_scattering && phase != SKIRT_PHASE_DUST_SELFABS && p->has_dust &&
