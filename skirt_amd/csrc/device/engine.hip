@@ -227,6 +227,10 @@ constexpr bool kLabsSmooth = SKIRT_LABS_SMOOTH;
 #ifndef SKIRT_VOR_PIPE
 #define SKIRT_VOR_PIPE 1  // groups of entries in flight per step (see Grid<SKIRT_GRID_VORONOI>::step)
 #endif
+#ifndef SKIRT_VOR_PAD_NAN
+#define SKIRT_VOR_PAD_NAN 1  // each cell's entries padded to whole groups with NaN entries (no per-entry count check)
+#endif
+constexpr bool kVorPadNaN = SKIRT_VOR_PAD_NAN && SKIRT_VOR_PIPE;
 #ifndef SKIRT_VOR_GROUPS
 // how many (SKIRT_VOR_PIPE): loaded with the header, each reloaded once consumed. 3: C4 trace launch
 // 23.64 -> 23.19 ms, 9.64e7 -> 9.89e7 pkt/s (4: the same as 3), profiles/r04_ktrace_groups_nolicm.txt
@@ -1278,12 +1282,13 @@ struct Grid<SKIRT_GRID_VORONOI> {
         const float sa = num * inv;
         const float err = fmaf(fmaf(fabsf(sa), s.eA2, s.eB2), inv, fabsf(sa) * kVorEpsF);
         // den > 2 eA: the sign of n.k and the interval [sa - err, sa + err] are certain (an interval at or
-        // below 0: no exit); den <= -eA: moving away for certain; otherwise (or NaN offsets: a degenerate
-        // wall) the sign is uncertain: lo = -FLT_MAX. Entries past the count: no exit. ucand: the upper
+        // below 0: no exit); den <= -eA: moving away for certain; otherwise (den = 0 included: m = 0 is a
+        // degenerate wall) the sign is uncertain: lo = -FLT_MAX. Entries past the count (`valid`), and the
+        // NaN padding after a cell's list (den NaN, so neither sure nor maybe): no exit. ucand: the upper
         // bound of a certain exit (lo > 0), else FLT_MAX. Selected as floats, no bool temporaries.
         const float lov = sa - err, hiv = sa + err;
         const bool sure = valid && den > s.eA2;
-        const bool maybe = valid && !(den <= -s.eA);
+        const bool maybe = valid && den > -s.eA;
         const float loSure = hiv > 0.f ? lov : FLT_MAX;
         lo = sure ? loSure : (maybe ? -FLT_MAX : FLT_MAX);
         ucand = (sure && lov > 0.f) ? hiv : FLT_MAX;
@@ -1469,7 +1474,8 @@ struct Grid<SKIRT_GRID_VORONOI> {
 #pragma unroll
                 for (int u = 0; u < kVorUnroll; u++) {
                     float lo, uc;
-                    bounds(s, L.g[gi][u], qb + u < s.cnt, lo, uc);
+                    // (a cell's list is padded to whole groups with NaN entries: no count check per entry)
+                    bounds(s, L.g[gi][u], kVorPadNaN || qb + u < s.cnt, lo, uc);
                     take(b, lo, uc, L.g[gi][u].next);
                 }
                 if (qb + NG * kVorUnroll < s.cnt) vorEntries(s.B, qb + NG * kVorUnroll, L.g[gi]);
@@ -3947,7 +3953,9 @@ int skirt_mcrt_upload_grid(SkirtMcrt* c, const SkirtGridDesc* g) {
             const int m = refOf[d];
             const int cnt = g->cell_nbr_offset[m + 1] - g->cell_nbr_offset[m];
             if (cnt < 1) return fail(c, SKIRT_ERR_ARG, "Voronoi cell without neighbours");
-            start[d + 1] = start[d] + kVorHead + ((cnt + 1) & ~1);  // pairs of entries
+            // pairs of entries; with kVorPadNaN whole groups of kVorUnroll (even)
+            const int per = kVorPadNaN ? kVorUnroll : 2;
+            start[d + 1] = start[d] + kVorHead + (cnt + per - 1) / per * per;
         }
         if ((size_t)start[N] + kVorPad >= (size_t)INT32_MAX) return fail(c, SKIRT_ERR_UNSUPPORTED, "Voronoi mesh too large");
         std::vector<VorEntry> slots((size_t)start[N] + kVorPad, VorEntry{0.f, 0.f, 0.f, -1});
@@ -3992,6 +4000,14 @@ int skirt_mcrt_upload_grid(SkirtMcrt* c, const SkirtGridDesc* g) {
                 P[h] = e.ox; P[2 + h] = e.oy; P[4 + h] = e.oz;
                 std::memcpy(P + 6 + h, &e.next, 4);
                 off[3 * (size_t)o] = e.ox; off[3 * (size_t)o + 1] = e.oy; off[3 * (size_t)o + 2] = e.oz;
+            }
+            // the padding up to the next block: NaN entries, no exit for any direction (bounds())
+            for (int q = cnt; q < start[d + 1] - start[d] - kVorHead; q++) {
+                float* P = reinterpret_cast<float*>(blk + kVorHead + (q & ~1));
+                const int h = q & 1;
+                P[h] = P[2 + h] = P[4 + h] = NAN;
+                const int none = -1;
+                std::memcpy(P + 6 + h, &none, 4);
             }
             // the header's last words: id, count and the cell's error terms of the bounds (vor_terms.hpp)
             float eA, eB;

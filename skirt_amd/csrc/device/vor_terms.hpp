@@ -33,12 +33,13 @@ inline void vorErrorTerms(const float* off, int n, int stride, float* eA, float*
 // no |n|^2 to form per entry. Rounding m to float errs by 2^-24 |m_i| per component, as rounding n did, so
 // the same Cauchy-Schwarz terms hold with m in place of n and the constant 1/2 in place of |n|^2/2:
 // eA = kVorEpsF max |m|_1 and eB = kVorEpsF / 2 (the numerator's error <= eA |D|_1 + eB).
-// n: the scaled offset in double; out: m in float, NaN for a degenerate offset (the step then evaluates
-// the cell's list exactly).
+// n: the scaled offset in double; out: m in float, 0 for a degenerate offset (a site on a wall): its m.k is
+// 0 for every direction, so the bounds call the entry's sign uncertain and the step evaluates the cell's
+// list exactly. (NaN marks the padding after a cell's list instead: no exit.)
 inline void vorRecipOffset(double nx, double ny, double nz, float out[3]) {
     const double q = nx * nx + ny * ny + nz * nz;
     if (!(q > 0.0) || !std::isfinite(q)) {
-        out[0] = out[1] = out[2] = NAN;
+        out[0] = out[1] = out[2] = 0.0f;
         return;
     }
     out[0] = (float)(nx / q);

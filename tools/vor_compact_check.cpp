@@ -178,7 +178,7 @@ static int compactStepF(const Mesh& M, int m, const double r[3], const double k[
             (void)n2;
             const float lov = sa - err, hiv = sa + err;
             const bool sure = den > 2.0f * eA;
-            const bool maybe = !(den <= -eA);
+            const bool maybe = den > -eA;  // (den = 0 for a degenerate wall's m = 0: uncertain)
             const float loSure = hiv > 0.f ? lov : FLT_MAX;
             const float lo = sure ? loSure : (maybe ? -FLT_MAX : FLT_MAX);
             const float ucand = (sure && lov > 0.f) ? hiv : FLT_MAX;
@@ -279,7 +279,7 @@ int main(int argc, char** argv) {
                 const double lim = (-mi - 1) % 2 ? g.extent[3 + axis] : g.extent[axis];
                 const double w = lim - sm[axis];
                 for (int d = 0; d < 3; d++) M.off[3 * (size_t)q + d] = 0.f;
-                M.off[3 * (size_t)q + axis] = w != 0.0 ? (float)(2.0 * w * gScale) : NAN;
+                M.off[3 * (size_t)q + axis] = w != 0.0 ? (float)(2.0 * w * gScale) : 0.0f;  // degenerate: n = 0, den = 0, sign uncertain
                 if (gRecip) {  // as the engine's Voronoi upload: m = n / |n|^2 (vor_terms.hpp)
                     double n[3] = {0.0, 0.0, 0.0};
                     n[axis] = w != 0.0 ? 2.0 * w * gScale : NAN;
