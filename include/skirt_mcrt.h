@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define SKIRT_MCRT_ABI_VERSION 10
+#define SKIRT_MCRT_ABI_VERSION 11  /* 11: SkirtStats::packages */
 
 enum {
     SKIRT_OK = 0,
