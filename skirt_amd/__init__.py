@@ -18,6 +18,7 @@ import os
 import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+ABI_VERSION = 11  # SKIRT_MCRT_ABI_VERSION of include/skirt_mcrt.h
 # SKIRT_AMD_LIB selects another build of the same library (e.g. a tuning variant built by
 # tools/build_variant.sh next to the default one)
 LIB_PATH = os.path.join(PKG_DIR, os.environ.get("SKIRT_AMD_LIB", "libskirt_amd.so"))
@@ -87,6 +88,11 @@ def lib():
             raise SkirtError("native library %s is missing: run `make -C skirt_amd/csrc` "
                              "(or __graft_entry__.build())" % LIB_PATH)
         L = ctypes.CDLL(LIB_PATH)
+        # the structs below follow include/skirt_mcrt.h at ABI_VERSION; a library built from another header
+        # would read or write them at other offsets (a tuning build chosen by SKIRT_AMD_LIB may be older)
+        v = L.skirt_mcrt_abi_version()
+        if v != ABI_VERSION and "SKIRT_AMD_LIB" not in os.environ:
+            raise SkirtError("native library %s has C ABI %d, this binding expects %d: rebuild it" % (LIB_PATH, v, ABI_VERSION))
         vp, c_int, c_u64, c_dbl = ctypes.c_void_p, ctypes.c_int, ctypes.c_uint64, ctypes.c_double
         L.skirt_sim_load.restype = vp
         L.skirt_sim_load.argtypes = [ctypes.c_char_p, ctypes.c_char_p, c_dbl, c_u64]
