@@ -233,8 +233,9 @@ constexpr bool kLabsSmooth = SKIRT_LABS_SMOOTH;
 constexpr bool kVorPadNaN = SKIRT_VOR_PAD_NAN && SKIRT_VOR_PIPE;
 #ifndef SKIRT_VOR_GROUPS
 // how many (SKIRT_VOR_PIPE): loaded with the header, each reloaded once consumed. 3: C4 trace launch
-// 23.64 -> 23.19 ms, 9.64e7 -> 9.89e7 pkt/s (4: the same as 3), profiles/r04_ktrace_groups_nolicm.txt
-#define SKIRT_VOR_GROUPS 3
+// 23.64 -> 23.19 ms, 9.64e7 -> 9.89e7 pkt/s (4 then the same as 3), profiles/r04_ktrace_groups_nolicm.txt;
+// 4 with the NaN-padded groups: 1.0155e8 -> 1.0243e8 (profiles/r04_vor_groups4.txt)
+#define SKIRT_VOR_GROUPS 4
 #endif
 constexpr int kVorGroups = SKIRT_VOR_PIPE ? SKIRT_VOR_GROUPS : 1;
 #ifndef SKIRT_VOR_FALLBACK_GROUP
