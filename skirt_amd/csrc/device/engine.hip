@@ -139,8 +139,11 @@ constexpr int kContSlots = 1 << 15;  // packet slots in flight with continuous s
 enum ErrorBits : unsigned { ERR_TAU = 1u, ERR_PATH_CAP = 2u, ERR_QUEUE = 4u };
 template <int GRID>
 constexpr bool kEnterInEvent = GRID == SKIRT_GRID_VORONOI;
+// Voronoi cellIndex: block-list candidates loaded per round trip. Round 3 chose 4; with the round-4
+// registers 2 lets the Voronoi event kernel run 3 waves/SIMD (165 VGPRs): event 2.59 -> 2.26 ms, C4
+// 1.0225e8 -> 1.0345e8 (8: 1.021e8), profiles/r04_cellindex_group.txt
 #ifndef SKIRT_CELLINDEX_GROUP
-#define SKIRT_CELLINDEX_GROUP 4
+#define SKIRT_CELLINDEX_GROUP 2
 #endif
 constexpr int kCellIndexGroup = SKIRT_CELLINDEX_GROUP;  // Voronoi cellIndex: block-list candidates per load round
 constexpr int kNoCell = -2;  // a cached cell index not known yet (-1 is a located point without a cell)
