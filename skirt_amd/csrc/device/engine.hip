@@ -4635,8 +4635,10 @@ static int runPhase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, uint6
         tgrid = std::max(1, c->nCusT) * per;
         c->traceBlocksPerCU = per;
     }
-    // event kernel blocks per CU (SKIRT_AMD_EVENT_BPC: tuning knob)
-    static const int ebpc = getenv("SKIRT_AMD_EVENT_BPC") ? std::max(1, atoi(getenv("SKIRT_AMD_EVENT_BPC"))) : 2;
+    // event kernel blocks per CU (SKIRT_AMD_EVENT_BPC: tuning knob). Voronoi: 3, since its event kernel fits
+    // 3 waves/SIMD (C4 +0.6 %, profiles/r04_event_bpc_sweep.txt); the others are within the spread at 2-4
+    static const int ebpcEnv = getenv("SKIRT_AMD_EVENT_BPC") ? std::max(1, atoi(getenv("SKIRT_AMD_EVENT_BPC"))) : 0;
+    const int ebpc = ebpcEnv ? ebpcEnv : (kind == SKIRT_GRID_VORONOI ? 3 : 2);
     const int egrid = std::max(1, std::min((slots + kBlock - 1) / kBlock, std::max(1, c->nCusE) * ebpc));
     const int dgrid = std::max(1, std::max(1, c->nCusE) * 4);
 
