@@ -482,6 +482,10 @@ constexpr size_t kCrossedBins = 1 << 16;
 static std::atomic<bool> g_engineAttenuation{false};
 static bool engineAttenuation() { return g_engineAttenuation.load(std::memory_order_relaxed); }
 
+// study hook (oracle_set_fill_hook): the cells of every storing FILL path
+static OracleFillHook g_fillHook = nullptr;
+static void* g_fillUser = nullptr;
+
 struct Tallies {
     bool shared = false;       // threaded mode: one set of arrays updated with lock-free adds
     void add(std::vector<double>& v, size_t i, double x) {
@@ -672,6 +676,13 @@ public:
             if (taupath < 0.0 || std::isnan(taupath) || std::isinf(taupath))
                 throw std::runtime_error("the optical depth along the path is not a positive number");
             if (peel && M.continuousScattering) continuousPeelOff(t, rng, pp, p, tmp);
+            if (g_fillHook && store) {
+                std::vector<int> cells;
+                for (auto& s : p.v)
+                    if (s.m != -1) cells.push_back(s.m);
+                const double r0[3] = {pp.r.x, pp.r.y, pp.r.z}, k0[3] = {pp.k.x, pp.k.y, pp.k.z};
+                g_fillHook(g_fillUser, pp.ell, r0, k0, cells.data(), (int)cells.size());
+            }
             // simulateescapeandabsorption
             double L = pp.L;
             if (Ncomp == 1) {
@@ -941,6 +952,11 @@ extern "C" {
 const char* oracle_last_error(void) { return g_error.c_str(); }
 
 void oracle_set_engine_attenuation(int on) { g_engineAttenuation = on != 0; }
+
+void oracle_set_fill_hook(OracleFillHook hook, void* user) {
+    g_fillUser = user;
+    g_fillHook = hook;
+}
 
 void oracle_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) { philox(ctr, key, out); }
 

@@ -110,6 +110,12 @@ void oracle_free(OracleRun* r);
  * running product of 1 - (-expm1(-dtau)) along the path, instead of the reference's exp(-taustart) */
 void oracle_set_engine_attenuation(int on);
 
+/* study hook (tools/labs_locality.cpp): called, from the worker threads, for every FILL path that stores
+ * absorption, with the packet's wavelength, start position and direction, and the reference cell numbers
+ * of the path's dust segments in path order (the cells its Labs adds go to). NULL turns it off. */
+typedef void (*OracleFillHook)(void* user, int ell, const double r[3], const double k[3], const int* cells, int n);
+void oracle_set_fill_hook(OracleFillHook hook, void* user);
+
 /* Philox4x32-10 known-answer access for tests: out[4] = philox(ctr[4], key[2]) */
 void oracle_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);
 

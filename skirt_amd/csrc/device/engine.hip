@@ -3091,7 +3091,7 @@ __global__ void __launch_bounds__(kBlock) SKIRT_EVENT_ATTR eventKernel(const Arg
         // kernel checks that the front and the WALK region do not meet
         if ((unsigned long long)pos + (unsigned)(nray - (back ? 1 : 0)) > (unsigned long long)a.rayCap ||
             (back && wpos >= (unsigned)a.rayCap) ||
-            (unsigned long long)dpos + (unsigned)npeel > (unsigned long long)a.rayCap) {
+            (unsigned long long)dpos + (unsigned)npeel > (unsigned long long)(a.rayCap - a.nslots)) {
             atomicOr(a.error, ERR_QUEUE);
             nray = 0;
         }

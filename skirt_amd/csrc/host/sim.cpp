@@ -18,7 +18,8 @@ using namespace skirt;
 
 namespace {
 
-constexpr int kCrossedBins = 16384;  // cells-crossed histogram bins (ds_crossed; the last counts longer paths)
+constexpr int kCrossedBins = 16384;  // cells-crossed histogram bins written to ds_crossed (paths of 0 .. 16383 cells);
+// the device keeps one more, which counts the longer paths
 thread_local std::string g_err;
 }
 
@@ -269,7 +270,7 @@ int skirt_sim_attach(SkirtSim* s, int device) {
     // the device tally pads each frame pixel's slots to a 64-byte line; downloads restore this layout
     if (ni < s->instrAll.size()) { g_err = "instrument tally size mismatch"; return SKIRT_ERR_STATE; }
     // DustSystem writeCellsCrossed: the engine keeps the cells-crossed histogram for ds_crossed
-    if (m.hasDust && m.writeCellsCrossed && (rc = check(s, skirt_mcrt_set_crossed(s->eng, kCrossedBins)))) return rc;
+    if (m.hasDust && m.writeCellsCrossed && (rc = check(s, skirt_mcrt_set_crossed(s->eng, kCrossedBins + 1)))) return rc;
     return check(s, skirt_mcrt_zero_tallies(s->eng));
 }
 
@@ -452,21 +453,23 @@ int skirt_sim_set_tallies(SkirtSim* s, const double* labs, const double* instr) 
 
 int skirt_sim_write(SkirtSim* s, const char* prefix) {
     if (!s || !prefix) return SKIRT_ERR_ARG;
+    std::string overflow;  // a limit met by ds_crossed, reported after every other output is written
     try {
         writeOutputs(s->m, prefix, s->frames, s->seds,
                      totalLabs(s->m, s->labs, s->labsDust.empty() ? nullptr : &s->labsDust));
         if (s->m.hasDust && s->m.writeCellsCrossed && s->eng) {
-            std::vector<uint64_t> hist(kCrossedBins);
-            int rc = check(s, skirt_mcrt_download_crossed(s->eng, hist.data(), kCrossedBins));
+            std::vector<uint64_t> hist(kCrossedBins + 1);
+            int rc = check(s, skirt_mcrt_download_crossed(s->eng, hist.data(), kCrossedBins + 1));
             if (rc) return rc;
-            // the last bin counts every longer path: the reference's _crossed grows without limit
-            // (DustSystem.cpp:969), so a path that reached it cannot be written as an exact count
-            if (hist[kCrossedBins - 1]) {
-                g_err = "ds_crossed: " + std::to_string(hist[kCrossedBins - 1]) + " paths crossed " +
-                         std::to_string(kCrossedBins - 1) + " or more cells, beyond the histogram's bins";
-                return SKIRT_ERR_UNSUPPORTED;
+            // the device's extra bin counts every longer path: the reference's _crossed grows without limit
+            // (DustSystem.cpp:969), so such a path cannot be written as an exact count
+            if (hist[kCrossedBins])
+                overflow = "ds_crossed: " + std::to_string(hist[kCrossedBins]) + " paths crossed " +
+                           std::to_string(kCrossedBins) + " or more cells, beyond the histogram's bins";
+            else {
+                hist.resize(kCrossedBins);
+                writeCellsCrossed(s->m, prefix, hist);
             }
-            writeCellsCrossed(s->m, prefix, hist);
         }
         if (s->m.hasDust && s->m.writeConvergence && s->eng) {
             // the six half axes from the origin (DustSystem.cpp:213-242), walked by the engine
@@ -486,6 +489,10 @@ int skirt_sim_write(SkirtSim* s, const char* prefix) {
     } catch (std::exception& e) {
         g_err = e.what();
         return SKIRT_ERR_ARG;
+    }
+    if (!overflow.empty()) {
+        g_err = overflow;
+        return SKIRT_ERR_UNSUPPORTED;
     }
     return SKIRT_OK;
 }
