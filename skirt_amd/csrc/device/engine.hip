@@ -62,6 +62,21 @@ constexpr int kSersicTable = 202;  // SersicFunction: 101 radii, then 101 cumula
 constexpr int kDetectCopies = 8;   // most LDS copies of the SED sums in the detect kernel (one per 8 lanes)
 constexpr int kPollEvery = 1;      // iterations between two counter copies of a half
 constexpr int kPollRing = 3;       // copies in flight per half (the host reads each kPollRing copies late)
+// Sorted FILL rays and the LDS line cache of the Labs adds (traceBodyCached).
+// The sort key of a FILL ray: its wavelength (2 bits: the few wavelengths in flight stay apart), its
+// direction (cube-map face x 4 x 4 bins) and the 16^3 region of its start point (Morton order).
+constexpr int kSortRegionBits = 4;
+constexpr int kSortKeyBits = 2 + 7 + 3 * kSortRegionBits;
+constexpr unsigned kSortBuckets = 1u << kSortKeyBits;
+constexpr int kScanChunk = 1024;                         // buckets per block of the scan kernels
+#ifndef SKIRT_CACHE_BLOCK
+#define SKIRT_CACHE_BLOCK 768
+#endif
+constexpr int kCacheBlock = SKIRT_CACHE_BLOCK;           // the cached trace kernel: 12 waves, one workgroup per CU
+constexpr int kCacheWays = 8;                            // lines per set
+constexpr int kEvictLines = 8;                           // evicted lines a wave hands out per grid step
+constexpr unsigned kCacheEmpty = 0xFFFFFFFFu;            // the tag of a free line
+constexpr int kCtrFill = 10;                             // ctr[10 + q]: FILL rays of the iteration
 // occupancy attribute of the trace kernel (a build knob for tuning variants, tools/build_variant.sh):
 // 3 waves per SIMD, i.e. at most 168 VGPRs (the grid entry on the pull path would otherwise take the
 // octree kernel to 175 and 2 waves; C3 1.91e8 -> 2.15e8 pkt/s at 3). The Voronoi walk has its own
@@ -358,6 +373,21 @@ struct Args {
     uint32_t *splo, *sphi, *sblock, *sw2, *sw3, *shave;
     double *resA, *resB;         // per slot: FILL -> tau, Lsca | WALK -> distance
     RayRec* rays;
+    // the FILL rays of an iteration, in a queue of their own (at most one per slot): ctr[10 + q] of them.
+    // With sortFill they are traced in the order of a sort key (fillSortKey: wavelength, direction bin, region
+    // of the start point) through fillPerm, so that the rays a workgroup traces together cross the same
+    // cells and their Labs adds merge in its LDS cache (traceBodyCached)
+    RayRec* fillRays;
+    unsigned* fillKey;           // [nslots] sort keys (sortFill)
+    unsigned* fillRank;          // [nslots] rank among the rays of the same key (sortFill)
+    unsigned* fillPerm;          // [nslots] FILL rays in key order (sortFill), null: queue order
+    unsigned* sortHist;          // [kSortBuckets] counts, then first positions, per key
+    unsigned* sortBlockSums;     // [kSortBuckets / kScanChunk] (the scan's partial sums)
+    int sortFill;
+    int cacheDebug;              // tests of the cached walk (SKIRT_AMD_CACHE_DEBUG): 1 every add straight to Labs,
+                                 // 2 FILL rays unsorted, 4 (timing only) no Labs adds at all
+    int cacheSets;               // the cached trace kernel's LDS line cache: sets of kCacheWays lines
+    int ldsCacheOff;             // its byte offset in the dynamic LDS
     DetRec* det;                 // detection records of the peel-off rays
     int* act[2];                 // active slot lists (double buffered)
     unsigned long long* claim;   // next packet index (relative to first)
@@ -549,7 +579,6 @@ struct Ray {
     int pfx, pfy, pfz;     //   and the finest-level cell it was requested for (SKIRT_LEAF_PREFETCH)
     int idx, ell;
     unsigned flags, mode;
-    unsigned id;           // queue index of the ray (a PEEL ray writes its optical depth back there)
 };
 
 // ------------------------------------------------------------------ grids
@@ -1589,7 +1618,47 @@ struct Grid<SKIRT_GRID_VORONOI> {
 };
 
 // ================================================================== trace kernel
-template <int GRID, bool ONECOMP, bool CONT>
+// The iteration's rays in pull order. Without sortFill every ray is in the queue: ctr[q] from its bottom
+// (event order: a packet's FILL or WALK ray beside its peel-offs), then the WALK rays ctr[8 + q] queued from
+// its top (Args::walkBack). With sortFill the FILL rays have a queue of their own, traced in key order, and
+// are spread evenly among the others: pull index v is a FILL ray when floor((v + 1) nfill / n) >
+// floor(v nfill / n), so that waves keep both kinds in flight, the absorbing FILL paths and the atomic-free
+// peel-off paths, at the same mix throughout the launch (round 2: the two kinds pulled one after the other
+// are 15 % slower on C3; alternating them 1:1 until the shorter kind runs out, 7 %).
+struct PullMap {
+    unsigned nfill, nfront, nback;
+    unsigned long long n;
+    double inv;  // 1 / n
+    __device__ __forceinline__ void init(const Args& a) {
+        nfill = a.ctr[kCtrFill + a.parity];
+        nfront = a.ctr[a.parity];
+        nback = a.ctr[8 + a.parity];
+        n = (unsigned long long)nfill + nfront + nback;
+        inv = n ? 1.0 / (double)n : 0.0;
+    }
+    // floor(v nfill / n): the quotient in double (v nfill < 2^53 is exact), corrected to the integer one
+    __device__ __forceinline__ unsigned fillsBefore(unsigned v) const {
+        const unsigned long long num = (unsigned long long)v * nfill;
+        unsigned q = (unsigned)((double)num * inv);
+        if ((unsigned long long)q * n > num) q--;
+        else if ((unsigned long long)(q + 1u) * n <= num) q++;
+        return q;
+    }
+    __device__ __forceinline__ const RayRec* rec(const Args& a, unsigned v) const {
+        unsigned k = v;  // index within its kind
+        if (nfill) {
+            const unsigned q = fillsBefore(v);
+            if ((unsigned long long)(v + 1u) * nfill >= (unsigned long long)(q + 1u) * n)
+                return a.fillRays + (a.fillPerm ? a.fillPerm[q] : q);
+            k = v - q;
+        }
+        return a.rays + (k < nfront ? k : (unsigned)a.rayCap - 1u - (k - nfront));
+    }
+};
+
+// CACHED: the Labs add of a step waits in registers (addIdx, addVal) for the workgroup's LDS line cache
+// (LabsCache, traceBodyCached) instead of the lane's LDS buffer
+template <int GRID, bool ONECOMP, bool CONT, bool CACHED = false>
 struct Tracer {
     const Args& a;
     const Shared& sh;
@@ -1613,6 +1682,10 @@ struct Tracer {
 #endif
     int npend = 0;
     unsigned gstep = 0;  // grid steps of the wave (drainStep's round robin)
+    // CACHED: this step's Labs add (a step adds at most one segment: kSegsPerStep == 1)
+    unsigned addIdx = 0;
+    double addVal = 0.0;
+    bool hasAdd = false;
 
     __device__ __forceinline__ void drain() {
         static_assert(kLabsBuf >= 2 && kLabsBuf <= 64 && (kLabsBuf & (kLabsBuf - 1)) == 0, "kLabsBuf: power of 2");
@@ -1766,9 +1839,15 @@ struct Tracer {
                     r.f2 += albedo * Lintm;
                 }
                 if (a.store) {
-                    pendVal[npend * kBlock + threadIdx.x] = (1.0 - albedo) * Lintm;
-                    pendIdx[npend * kBlock + threadIdx.x] = (unsigned)r.ell * (unsigned)a.labsStride + (unsigned)m;
-                    npend++;
+                    if constexpr (CACHED) {
+                        addVal = (1.0 - albedo) * Lintm;
+                        addIdx = (unsigned)r.ell * (unsigned)a.labsStride + (unsigned)m;
+                        hasAdd = true;
+                    } else {
+                        pendVal[npend * kBlock + threadIdx.x] = (1.0 - albedo) * Lintm;
+                        pendIdx[npend * kBlock + threadIdx.x] = (unsigned)r.ell * (unsigned)a.labsStride + (unsigned)m;
+                        npend++;
+                    }
                 }
             }
         } else if (r.mode == RAY_WALK) {
@@ -1779,13 +1858,12 @@ struct Tracer {
         return true;
     }
 
-    // load queued ray `id` and enter the grid: the part of the path before the grid (segments outside
+    // load a queued ray and enter the grid: the part of the path before the grid (segments outside
     // it, m = -1) and the first cell (DustGrid::path); an empty path finishes the ray at once
-    __device__ __forceinline__ void load(Ray& r, unsigned id) {
-        const double2* c = reinterpret_cast<const double2*>(a.rays + id);
+    __device__ __forceinline__ void load(Ray& r, const RayRec* rec) {
+        const double2* c = reinterpret_cast<const double2*>(rec);
         const double2 c0 = c[0], c1 = c[1], c2 = c[2], c3 = c[3];
         const int4 c6 = reinterpret_cast<const int4*>(c)[4];
-        r.id = id;
         r.x = c0.x; r.y = c0.y; r.z = c1.x;
         r.dx = c1.y; r.dy = c2.x; r.dz = c2.y;
         // 1/direction, 0 where |k| <= 1e-15 (that axis is never crossed), as the event kernel computed it
@@ -2175,12 +2253,16 @@ __device__ __forceinline__ void traceBody(const Args& a) {
         a.ctr[5 + (1 - a.parity)] = 0;  // and its detection records (the last ones were detected already)
         a.ctr[2 + a.parity] = 0;  // active list just consumed by the event kernel
         a.ctr[8 + (1 - a.parity)] = 0;  // the next iteration's WALK rays
+        a.ctr[kCtrFill + (1 - a.parity)] = 0;  // and FILL rays
     }
-    // the iteration's rays: ctr[q] from the bottom of the queue, then the WALK rays ctr[8 + q] from its top
-    // (Args::walkBack), pulled last: the short WALK paths fill the lanes that the long FILL and peel-off
-    // paths free at the end of a launch, instead of idling until the launch's longest path ends
-    const unsigned int nfront = a.ctr[a.parity];
-    if (nfront + a.ctr[8 + a.parity] == 0) return;  // an iteration after the end of the phase
+    // the iteration's rays (PullMap): the FILL rays among ctr[q] from the bottom of the queue, then the WALK
+    // rays ctr[8 + q] from its top (Args::walkBack), pulled last: the short WALK paths fill the lanes that the
+    // long FILL and peel-off paths free at the end of a launch, instead of idling until the launch's longest
+    // path ends
+    PullMap pm;
+    pm.init(a);
+    const unsigned int nfront = pm.nfront;
+    if (pm.n == 0) return;  // an iteration after the end of the phase
     // the front rays (growing up from 0) and the WALK rays (growing down from rayCap - 1) must not meet:
     // the event and continuous peel-off kernels reserved them independently, so this is the first point
     // where both totals are final; an overflow fails the phase instead of tracing overwritten records
@@ -2204,7 +2286,7 @@ __device__ __forceinline__ void traceBody(const Args& a) {
     if (threadIdx.x < 3 * (kBlock / 64)) T.waveSegs[threadIdx.x] = 0;
     __syncthreads();
     const int lane = threadIdx.x & 63;
-    const unsigned int nrays = nfront + a.ctr[8 + a.parity];
+    const unsigned int nrays = (unsigned)pm.n;
     Ray r;
     r.mode = RAY_NONE;
     bool done = false;
@@ -2245,7 +2327,7 @@ __device__ __forceinline__ void traceBody(const Args& a) {
 #endif
             if (idle) {
                 if (id >= nrays) done = true;
-                else T.load(r, id < nfront ? id : (unsigned)a.rayCap - 1u - (id - nfront));  // a RAY_NONE record (empty path) leaves the lane idle
+                else T.load(r, pm.rec(a, id));  // a RAY_NONE record (empty path) leaves the lane idle
             }
 #ifdef SKIRT_EXPERIMENT_TIMELINE
             tlRays += (unsigned long long)__popcll(__ballot(idle && id < nrays));
@@ -2323,6 +2405,416 @@ __global__ void __launch_bounds__(kBlock) SKIRT_TRACE_ATTR traceKernel(const Arg
 template <bool ONECOMP, bool CONT>
 __global__ void __launch_bounds__(kBlock) SKIRT_VOR_TRACE_ATTR traceKernelVor(const Args a) {
     traceBody<SKIRT_GRID_VORONOI, ONECOMP, CONT>(a);
+}
+
+// ------------------------------------------------------------------ the cached trace kernel
+// Labs adds through an LDS line cache (Args::sortFill; DESIGN.md section 4, "C3: the Labs line cache").
+// f64 atomics execute memory-side at one chip-wide rate of 64-byte requests (2.36e10/s), and a ray's
+// consecutive adds share a line only 1.85 times on C3. With the FILL rays sorted (fillSortKey) and each
+// workgroup pulling consecutive rays of that order, the rays a workgroup traces together start close
+// together and head the same way, so the workgroup's adds fall into far fewer lines than its rays cross
+// alone (tools/labs_locality.cpp models 4.2-5.1 adds per line for C3 with 2048 cached lines). The cache
+// holds whole lines of one wavelength's Labs row, kCacheWays per set, shared by the workgroup's 12 waves:
+//  * a hit pins its line (+1 on the line's word), adds into LDS, unpins;
+//  * a miss takes a free way (compare-and-swap from the free tag), or evicts the set's round-robin victim:
+//    the evicting lane locks the victim (compare-and-swap of its word with no pins to "locked"), copies its
+//    8 sums to the wave's eviction buffer, zeroes them, writes its own add and retags the way in one atomic
+//    add that also unlocks it. A lane that finds its line locked, retagged, or cannot lock a victim adds
+//    straight to Labs. No lane ever waits for another, so no wave can block the workgroup.
+//  * once per grid step a wave issues its evicted lines (8 lanes per line: one 64-byte request each) and
+//    its direct adds as buffer atomics; after the last ray the workgroup adds the cached lines to Labs.
+// LDS operations of one wave execute in program order, and the compiler is kept from reordering them
+// (signal fences), which is all the protocol relies on.
+typedef __attribute__((address_space(3))) unsigned long long LdsU64;
+typedef __attribute__((address_space(3))) double LdsF64;
+typedef __attribute__((address_space(3))) unsigned LdsU32;
+typedef unsigned long long VecU64x2 __attribute__((ext_vector_type(2)));
+typedef double VecF64x2 __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) VecU64x2 LdsU64x2;
+typedef __attribute__((address_space(3))) VecF64x2 LdsF64x2;
+typedef unsigned VecU32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) VecU32x4 LdsU32x4;
+constexpr unsigned kPoolChunk = 1536;  // pull indices a workgroup reserves at once (about half FILL rays)
+constexpr int kCacheWaves = kCacheBlock / 64;
+
+__device__ __forceinline__ unsigned long long ldsAdd64(LdsU64* p, unsigned long long v) {
+    return __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ bool ldsCas64(LdsU64* p, unsigned long long& expect, unsigned long long want) {
+    return __hip_atomic_compare_exchange_strong(p, &expect, want, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void ldsAddF64(LdsF64* p, double v) {
+    (void)__hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ unsigned ldsAdd32(LdsU32* p, unsigned v) {
+    return __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void ldsOrder() { __atomic_signal_fence(__ATOMIC_SEQ_CST); }
+
+struct LabsCache {
+    LdsU32* tag;               // [sets][kCacheWays]: the Labs line cached in the way (kCacheEmpty: free)
+    LdsU32* pin;               // [sets][kCacheWays]: lanes adding into the way; kPinLock: being evicted
+    LdsF64* data;              // [sets][kCacheWays][8]: the line's sums
+    LdsF64* evData;            // this wave's evicted lines [kEvictLines][8]
+    LdsU32* evTag;             // [kEvictLines]: their Labs lines
+    LdsU32* rr;                // [sets]: the next victim of each set
+    unsigned setShift;         // set of a line: (line * 2654435761) >> setShift
+    __amdgpu_buffer_rsrc_t rsrc;
+    unsigned oob;              // a byte offset past Labs: the buffer range check drops the lane
+    unsigned requests = 0;     // 64-byte atomic requests issued (wave-uniform)
+    bool debugDirect = false;  // Args::cacheDebug & 1
+
+    static constexpr unsigned kPinLock = 0x80000000u;
+
+    // add into way w if it holds `line`: pinned, the way cannot be evicted meanwhile (the tag is read after
+    // the pin; a tag only changes while its way is locked, which needs no pins)
+    __device__ __forceinline__ bool tryHit(unsigned w, unsigned line, unsigned e, double v) {
+        const unsigned old = ldsAdd32(pin + w, 1u);
+        ldsOrder();
+        const unsigned t = tag[w];
+        const bool ok = !(old & kPinLock) && t == line;
+        if (ok) ldsAddF64(data + w * 8 + e, v);
+        ldsOrder();
+        (void)ldsAdd32(pin + w, ~0u);  // unpin
+        return ok;
+    }
+    // take the free way w for `line` (its sums are zero), or add into it if another lane just took it for
+    // the same line
+    __device__ __forceinline__ bool tryInsert(unsigned w, unsigned line, unsigned e, double v) {
+        const unsigned old = ldsAdd32(pin + w, 1u);
+        ldsOrder();
+        unsigned expect = kCacheEmpty;
+        const bool took = __hip_atomic_compare_exchange_strong(tag + w, &expect, line, __ATOMIC_RELAXED,
+                                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        const bool ok = !(old & kPinLock) && (took || expect == line);
+        if (ok) ldsAddF64(data + w * 8 + e, v);
+        ldsOrder();
+        (void)ldsAdd32(pin + w, ~0u);
+        return ok;
+    }
+    // lock way w (no pins), hand its line to eviction slot `slot`, take the way for `line` with the add
+    __device__ __forceinline__ bool tryEvict(unsigned w, unsigned line, unsigned e, double v, unsigned slot) {
+        unsigned expect = 0u;
+        if (!__hip_atomic_compare_exchange_strong(pin + w, &expect, kPinLock, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_WORKGROUP))
+            return false;
+        ldsOrder();
+        const unsigned victim = tag[w];
+        LdsF64x2* d2 = reinterpret_cast<LdsF64x2*>(data + w * 8);
+        const VecF64x2 q0 = d2[0], q1 = d2[1], q2 = d2[2], q3 = d2[3];
+        LdsF64x2* o2 = reinterpret_cast<LdsF64x2*>(evData + slot * 8);
+        o2[0] = q0; o2[1] = q1; o2[2] = q2; o2[3] = q3;
+        evTag[slot] = victim;
+        const VecF64x2 z = {0.0, 0.0};
+        d2[0] = z; d2[1] = z; d2[2] = z; d2[3] = z;
+        data[w * 8 + e] = v;
+        tag[w] = line;
+        ldsOrder();
+        (void)ldsAdd32(pin + w, 0u - kPinLock);  // unlock (pins of lanes that found it locked stay counted)
+        return true;
+    }
+
+    // the step's adds of the wave (lanes with `has`): cached, or straight to Labs
+    __device__ __forceinline__ void addStep(bool has, unsigned idx, double v) {
+        const int lane = threadIdx.x & 63;
+        const unsigned line = idx >> 3, e = idx & 7u;
+        unsigned doff = oob;
+        double dval = 0.0;
+        bool evict = false;
+        unsigned w0 = 0, vway = 0;
+#ifdef SKIRT_EXP_NOCACHE
+        if (has) {
+#else
+        if (has && debugDirect) {
+#endif
+            doff = idx * 8u;
+            dval = v;
+        } else if (has) {
+            w0 = ((line * 2654435761u) >> setShift) * kCacheWays;
+            const LdsU32x4* tp = reinterpret_cast<const LdsU32x4*>(tag + w0);
+            const VecU32x4 t0 = tp[0], t1 = tp[1];
+            int hit = -1, freeWay = -1;
+#pragma unroll
+            for (int k = kCacheWays - 1; k >= 0; k--) {
+                const unsigned t = k < 4 ? t0[k & 3] : t1[k & 3];
+                if (t == line) hit = k;
+                if (t == kCacheEmpty) freeWay = k;
+            }
+            bool done = false;
+            if (hit >= 0) done = tryHit(w0 + (unsigned)hit, line, e, v);
+            else if (freeWay >= 0) done = tryInsert(w0 + (unsigned)freeWay, line, e, v);
+            else {
+                evict = true;
+                vway = ldsAdd32(rr + w0 / kCacheWays, 1u) & (kCacheWays - 1);
+            }
+            if (!done && !evict) { doff = idx * 8u; dval = v; }
+        }
+        const unsigned long long em = __ballot(evict);
+        if (em) {
+            const unsigned slot = (unsigned)__popcll(em & ((1ull << lane) - 1ull));
+            if (evict) {
+                const bool ok = slot < (unsigned)kEvictLines && tryEvict(w0 + vway, line, e, v, slot);
+                if (!ok) {
+                    if (slot < (unsigned)kEvictLines) evTag[slot] = kCacheEmpty;
+                    doff = idx * 8u;
+                    dval = v;
+                }
+            }
+            ldsOrder();
+            // the evicted lines: lane q adds entry q & 7 of line q >> 3
+            const unsigned nev = min((unsigned)__popcll(em), (unsigned)kEvictLines);
+            const unsigned j = (unsigned)lane >> 3, ee = (unsigned)lane & 7u;
+            const unsigned tg = j < nev ? evTag[j] : kCacheEmpty;
+            const double ev = evData[j * 8 + ee];
+            bufferAtomicAddF64(ev, rsrc, (int)((tg != kCacheEmpty && ev != 0.0) ? tg * 64u + ee * 8u : oob), 0, 0);
+            requests += (unsigned)__popcll(__ballot(ee == 0 && tg != kCacheEmpty));
+            ldsOrder();
+        }
+        const unsigned long long dm = __ballot(doff != oob);
+        if (dm) {
+            bufferAtomicAddF64(dval, rsrc, (int)doff, 0, 0);
+            requests += (unsigned)__popcll(dm);
+        }
+    }
+
+    // after the workgroup's last ray: every cached line to Labs (8 lanes per line)
+    __device__ __forceinline__ void flushAll(unsigned nlines) {
+        const unsigned ee = threadIdx.x & 7u;
+        unsigned lines = 0;
+        for (unsigned L = threadIdx.x >> 3; L < nlines; L += blockDim.x >> 3) {
+            const unsigned tg = tag[L];
+            const double dv = data[L * 8 + ee];
+            bufferAtomicAddF64(dv, rsrc, (int)((tg != kCacheEmpty && dv != 0.0) ? tg * 64u + ee * 8u : oob), 0, 0);
+            if (ee == 0 && tg != kCacheEmpty) lines++;
+        }
+        requests = lines;  // (per lane: the lines this lane's group flushed)
+    }
+};
+
+template <int GRID, bool ONECOMP>
+__device__ __forceinline__ void traceBodyCached(const Args& a) {
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        // reset the counters the next event iteration appends to (nobody else uses them now)
+        a.ctr[1 - a.parity] = 0;
+        a.ctr[5 + (1 - a.parity)] = 0;
+        a.ctr[2 + a.parity] = 0;
+        a.ctr[8 + (1 - a.parity)] = 0;
+        a.ctr[kCtrFill + (1 - a.parity)] = 0;
+    }
+    PullMap pm;
+    pm.init(a);
+    if (pm.n == 0) return;  // an iteration after the end of the phase
+    if ((unsigned long long)pm.nfront + pm.nback > (unsigned long long)a.rayCap) {
+        if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(a.error, ERR_QUEUE);
+        return;
+    }
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    // LDS: tables | cache words | cache sums | eviction buffers | pull pool | round-robin counters | eviction
+    // tags | segment counts | pool-exhausted flag
+    typedef __attribute__((address_space(3))) char LdsByte;
+    LdsByte* cb = (LdsByte*)((char*)lds) + a.ldsCacheOff;  // (a C cast: the address-space cast)
+    const unsigned sets = (unsigned)a.cacheSets, nlines = sets * kCacheWays;
+    LabsCache C;
+    C.tag = reinterpret_cast<LdsU32*>(cb); cb += nlines * 4;
+    C.pin = reinterpret_cast<LdsU32*>(cb); cb += nlines * 4;
+    C.data = reinterpret_cast<LdsF64*>(cb); cb += nlines * 64;
+    LdsF64* evAll = reinterpret_cast<LdsF64*>(cb); cb += kCacheWaves * kEvictLines * 64;
+    LdsU64* pool = reinterpret_cast<LdsU64*>(cb); cb += 8;
+    C.rr = reinterpret_cast<LdsU32*>(cb); cb += sets * 4;
+    LdsU32* evTagAll = reinterpret_cast<LdsU32*>(cb); cb += kCacheWaves * kEvictLines * 4;
+    unsigned* waveSegs = (unsigned*)(LdsU32*)cb; cb += kCacheWaves * 3 * 4;
+    volatile LdsU32* poolDone = reinterpret_cast<volatile LdsU32*>(cb);
+    const int uwave = __builtin_amdgcn_readfirstlane(wave);
+    C.evData = evAll + uwave * kEvictLines * 8;
+    C.evTag = evTagAll + uwave * kEvictLines;
+    C.setShift = 32u - (unsigned)(31 - __builtin_clz(sets));
+    C.rsrc = __builtin_amdgcn_make_buffer_rsrc(a.labs, 0, (int)a.labsBytes, 0x00020000);
+    C.oob = a.labsBytes;
+    C.debugDirect = (a.cacheDebug & 1) != 0;
+    for (unsigned q = threadIdx.x; q < nlines; q += blockDim.x) { C.tag[q] = kCacheEmpty; C.pin[q] = 0u; }
+    for (unsigned q = threadIdx.x; q < nlines * 8; q += blockDim.x) C.data[q] = 0.0;
+    for (unsigned q = threadIdx.x; q < sets; q += blockDim.x) C.rr[q] = 0u;
+    if (threadIdx.x < 3 * kCacheWaves) waveSegs[threadIdx.x] = 0u;
+    if (threadIdx.x == 0) { *pool = 0ull; *poolDone = 0u; }
+    Shared sh = stageTables(a, lds, gridParts<GRID>() | STAGE_OPTICS);  // (ends with a barrier)
+
+    Tracer<GRID, ONECOMP, false, true> T{a, sh};
+    T.waveSegs = waveSegs;
+    const unsigned nvirt = (unsigned)pm.n;
+    Ray r;
+    r.mode = RAY_NONE;
+    bool done = false;
+    while (true) {
+        const bool idle = (r.mode == RAY_NONE) && !done;
+        const unsigned long long imask = __ballot(idle);
+        const unsigned long long amask = __ballot(r.mode != RAY_NONE);
+        if (imask == 0 && amask == 0) break;
+        if (imask != 0 && (amask == 0 || __popcll(imask) >= a.threshold)) {
+#ifdef SKIRT_EXP_WAVEPULL
+            {
+                const unsigned k = (unsigned)__popcll(imask);
+                const unsigned rank = (unsigned)__popcll(imask & ((1ull << lane) - 1ull));
+                unsigned base = 0;
+                if (lane == 0) base = atomicAdd(a.ctr + 4, k);
+                base = __shfl(base, 0);
+                if (idle) {
+                    if (base + rank < nvirt) T.load(r, pm.rec(a, base + rank));
+                    else done = true;
+                }
+            }
+#else
+            // the idle lanes pull consecutive indices from the workgroup's chunk (one LDS atomic per wave);
+            // the wave that crosses the chunk's end reserves the next chunk for the workgroup
+            const unsigned k = (unsigned)__popcll(imask);
+            const unsigned rank = (unsigned)__popcll(imask & ((1ull << lane) - 1ull));
+            unsigned long long old = 0;
+            if (lane == 0) old = ldsAdd64(pool, (unsigned long long)k);
+            old = __shfl(old, 0);
+            const unsigned nxt = (unsigned)old, end = (unsigned)(old >> 32);
+            // (signed 64-bit arithmetic: with unsigned 32-bit compares the device compiler dropped the nxt <=
+            // end test of the crossing condition -- an unconditional `sub nuw` from min(k, end - nxt) -- and
+            // every wave that found the chunk used up took a chunk of its own)
+            const long long avail = (long long)end - (long long)nxt;
+            const unsigned got = avail > 0 ? (unsigned)min((long long)k, avail) : 0u;
+            unsigned base2 = 0, got2 = 0;
+            if (avail >= 0 && avail < (long long)k) {
+                unsigned b = 0;
+                if (lane == 0) b = atomicAdd(a.ctr + 4, kPoolChunk);
+                b = __shfl(b, 0);
+                if (b >= nvirt) {
+                    if (lane == 0) {
+                        (void)__hip_atomic_exchange(pool, 0x80000000ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        *poolDone = 1u;
+                    }
+                } else {
+                    const unsigned e2 = min(b + kPoolChunk, nvirt);
+                    got2 = min(k - got, e2 - b);
+                    base2 = b;
+                    if (lane == 0)
+                        (void)__hip_atomic_exchange(pool, ((unsigned long long)e2 << 32) | (b + got2),
+                                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                }
+            }
+            // (one call site of load: the grid entry is inlined once)
+            const bool have = rank < got + got2;
+            const unsigned id = rank < got ? nxt + rank : base2 + (rank - got);
+            if (idle) {
+                if (have) T.load(r, pm.rec(a, id));
+                else if (*poolDone) done = true;
+            }
+#endif
+        }
+#pragma unroll 1
+        for (int it = 0; it < kStepsPerPull; it++) {
+            const unsigned long long live = __ballot(r.mode != RAY_NONE);
+            if (live == 0) break;
+            T.laneSlots += 64;
+            if (r.mode != RAY_NONE) {
+                if (!Grid<GRID>::step(a, sh, r, [&](int m, double rho0, double ds) { return T.segment(r, m, rho0, ds); })) {
+                    T.finish(r);
+                    r.mode = RAY_NONE;
+                }
+            }
+            T.absorbs += (unsigned)__popcll(__ballot(T.hasAdd));
+            if (!(a.cacheDebug & 4)) C.addStep(T.hasAdd, T.addIdx, T.addVal);
+            T.hasAdd = false;
+        }
+    }
+    __syncthreads();  // every wave's rays are done: the cache holds the workgroup's remaining sums
+    const unsigned stepRequests = C.requests;
+    C.flushAll(nlines);
+    unsigned flushed = C.requests;
+    for (int off = 32; off > 0; off >>= 1) flushed += __shfl_xor(flushed, off);
+    const unsigned* ws = waveSegs + wave * 3;
+    const bool l0 = lane == 0;
+    const unsigned long long vals[8] = {0, l0 ? ws[0] : 0u, l0 ? ws[1] : 0u, l0 ? ws[2] : 0u, 0,
+                                        l0 ? T.absorbs : 0u, l0 ? T.laneSlots : 0u,
+                                        l0 ? (unsigned long long)stepRequests + flushed : 0ull};
+    flushStats(a, vals);
+}
+
+template <int GRID, bool ONECOMP>
+__global__ void __launch_bounds__(kCacheBlock) traceKernelCached(const Args a) {
+    traceBodyCached<GRID, ONECOMP>(a);
+}
+
+// ------------------------------------------------------------------ FILL ray sort (Args::sortFill)
+// Between the event kernel and the trace kernel of an iteration, a counting sort of the FILL queue by
+// fillSortKey: sortRankKernel gives every ray its rank among the rays of its key (one returning atomic per
+// ray on the key's count), the scan kernels turn the counts into each key's first position, and
+// sortPlaceKernel writes fillPerm[first[key] + rank] = ray. The ray count is read on the device.
+
+// exclusive scan of one value per thread over the block; returns the thread's prefix, *total the block's sum
+template <int NT>
+__device__ __forceinline__ unsigned blockExclusiveScan(unsigned v, unsigned* part, unsigned* total) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    unsigned inc = v;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const unsigned u = __shfl_up(inc, off);
+        if (lane >= off) inc += u;
+    }
+    if (lane == 63) part[wave] = inc;
+    __syncthreads();
+    unsigned before = 0, all = 0;
+#pragma unroll
+    for (int w = 0; w < NT / 64; w++) {
+        const unsigned pw = part[w];
+        if (w < wave) before += pw;
+        all += pw;
+    }
+    __syncthreads();  // part is reused by the next call
+    *total = all;
+    return before + inc - v;
+}
+
+__global__ void __launch_bounds__(kBlock) sortRankKernel(const Args a) {
+    const unsigned n = a.ctr[kCtrFill + a.parity];
+    for (unsigned f = blockIdx.x * kBlock + threadIdx.x; f < n; f += gridDim.x * kBlock)
+        a.fillRank[f] = atomicAdd(a.sortHist + a.fillKey[f], 1u);
+}
+
+// block b: the sum of the counts of keys [b kScanChunk, (b + 1) kScanChunk)
+__global__ void __launch_bounds__(kBlock) sortScanSumsKernel(const Args a) {
+    if (a.ctr[kCtrFill + a.parity] == 0) return;
+    __shared__ unsigned part[kBlock / 64];
+    const uint4* h = reinterpret_cast<const uint4*>(a.sortHist + (size_t)blockIdx.x * kScanChunk);
+    static_assert(kScanChunk == 4 * kBlock, "one uint4 of counts per thread");
+    const uint4 c = h[threadIdx.x];
+    unsigned total;
+    (void)blockExclusiveScan<kBlock>(c.x + c.y + c.z + c.w, part, &total);
+    if (threadIdx.x == 0) a.sortBlockSums[blockIdx.x] = total;
+}
+
+// the chunk sums' exclusive scan, in place (kSortBuckets / kScanChunk sums, two per thread)
+constexpr int kScanTop = (int)(kSortBuckets / kScanChunk);
+__global__ void __launch_bounds__(kScanTop / 2) sortScanTopKernel(const Args a) {
+    if (a.ctr[kCtrFill + a.parity] == 0) return;
+    __shared__ unsigned part[kScanTop / 2 / 64];
+    uint2* s2 = reinterpret_cast<uint2*>(a.sortBlockSums);
+    const uint2 v = s2[threadIdx.x];
+    unsigned total;
+    const unsigned pre = blockExclusiveScan<kScanTop / 2>(v.x + v.y, part, &total);
+    s2[threadIdx.x] = make_uint2(pre, pre + v.x);
+}
+
+// the counts of chunk b become first positions: the chunk's exclusive scan plus the sums before the chunk
+__global__ void __launch_bounds__(kBlock) sortScanApplyKernel(const Args a) {
+    if (a.ctr[kCtrFill + a.parity] == 0) return;
+    __shared__ unsigned part[kBlock / 64];
+    uint4* h = reinterpret_cast<uint4*>(a.sortHist + (size_t)blockIdx.x * kScanChunk);
+    const uint4 c = h[threadIdx.x];
+    unsigned total;
+    const unsigned pre = blockExclusiveScan<kBlock>(c.x + c.y + c.z + c.w, part, &total) + a.sortBlockSums[blockIdx.x];
+    h[threadIdx.x] = make_uint4(pre, pre + c.x, pre + c.x + c.y, pre + c.x + c.y + c.z);
+}
+
+__global__ void __launch_bounds__(kBlock) sortPlaceKernel(const Args a) {
+    const unsigned n = a.ctr[kCtrFill + a.parity];
+    for (unsigned f = blockIdx.x * kBlock + threadIdx.x; f < n; f += gridDim.x * kBlock)
+        a.fillPerm[a.sortHist[a.fillKey[f]] + a.fillRank[f]] = f;
 }
 
 // the detections of this iteration's peel-off rays (their optical depths are in the queue now)
@@ -2405,8 +2897,8 @@ struct Events {
     // queues ray `pos`. The trace kernel enters the grid, except for Voronoi grids (kEnterInEvent): their
     // cellIndex loops over a block's site list, which costs the trace kernel more than it costs here. A
     // path found empty here (no dust system, or a Voronoi ray missing the grid) is finished here.
-    __device__ __forceinline__ void emitRay(unsigned pos, const Packet& p, double dx, double dy, double dz, double prm,
-                                            int idx, unsigned flags, int& vcell) {
+    __device__ __forceinline__ void emitRay(RayRec* queue, unsigned pos, const Packet& p, double dx, double dy, double dz,
+                                            double prm, int idx, unsigned flags, int& vcell) {
         Ray r;
         r.x = p.rx; r.y = p.ry; r.z = p.rz;
         r.dx = dx; r.dy = dy; r.dz = dz;
@@ -2416,7 +2908,7 @@ struct Events {
         r.s = 0;
         r.ci = r.cj = 0;
         const unsigned mode = rayMode(flags);
-        int4* dst = reinterpret_cast<int4*>(a.rays + pos);
+        int4* dst = reinterpret_cast<int4*>(queue + pos);
         bool entered = a.hasDust;
         unsigned nseg = 0;
         if constexpr (kEnterInEvent<GRID>) {
@@ -2869,47 +3361,75 @@ __device__ __forceinline__ void blockReserve3(unsigned* ctr0, unsigned c0, unsig
     __syncthreads();  // the scratch words are reused by the next call
 }
 
-// four counters at once (scratch: 4 * (kBlock / 64) + 4 words); the first lane of wave q issues counter q's atomic
-static_assert(kBlock >= 256, "blockReserve4 needs four waves per block");
-__device__ __forceinline__ void blockReserve4(unsigned* const (&ctr)[4], const unsigned (&c)[4], unsigned (&r)[4],
+// N counters at once (scratch: N * (kBlock / 64) + N words); counter q's atomic is issued by lane q / W of
+// wave q % W (W waves per block)
+template <int N>
+__device__ __forceinline__ void blockReserveN(unsigned* const (&ctr)[N], const unsigned (&c)[N], unsigned (&r)[N],
                                               unsigned long long* scratch) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     constexpr int W = kBlock / 64;
-    unsigned in[4];
+    unsigned in[N];
 #pragma unroll
-    for (int q = 0; q < 4; q++) in[q] = c[q];
+    for (int q = 0; q < N; q++) in[q] = c[q];
 #pragma unroll
     for (int off = 1; off < 64; off <<= 1) {
-        unsigned v[4];
+        unsigned v[N];
 #pragma unroll
-        for (int q = 0; q < 4; q++) v[q] = __shfl_up(in[q], off);
+        for (int q = 0; q < N; q++) v[q] = __shfl_up(in[q], off);
         if (lane >= off) {
 #pragma unroll
-            for (int q = 0; q < 4; q++) in[q] += v[q];
+            for (int q = 0; q < N; q++) in[q] += v[q];
         }
     }
     if (lane == 63) {
 #pragma unroll
-        for (int q = 0; q < 4; q++) scratch[q * W + wave] = in[q];
+        for (int q = 0; q < N; q++) scratch[q * W + wave] = in[q];
     }
     __syncthreads();
-    unsigned w[4] = {0, 0, 0, 0}, t[4] = {0, 0, 0, 0};
+    unsigned w[N], t[N];
+#pragma unroll
+    for (int q = 0; q < N; q++) w[q] = t[q] = 0;
 #pragma unroll
     for (int ww = 0; ww < W; ww++) {
 #pragma unroll
-        for (int q = 0; q < 4; q++) {
+        for (int q = 0; q < N; q++) {
             const unsigned sv = (unsigned)scratch[q * W + ww];
             if (ww < wave) w[q] += sv;
             t[q] += sv;
         }
     }
 #pragma unroll
-    for (int q = 0; q < 4; q++)
-        if (threadIdx.x == 64 * q) scratch[4 * W + q] = t[q] ? atomicAdd(ctr[q], t[q]) : 0u;
+    for (int q = 0; q < N; q++)
+        if (threadIdx.x == 64 * (q % W) + q / W) scratch[N * W + q] = t[q] ? atomicAdd(ctr[q], t[q]) : 0u;
     __syncthreads();
 #pragma unroll
-    for (int q = 0; q < 4; q++) r[q] = (unsigned)scratch[4 * W + q] + w[q] + in[q] - c[q];
+    for (int q = 0; q < N; q++) r[q] = (unsigned)scratch[N * W + q] + w[q] + in[q] - c[q];
     __syncthreads();  // the scratch words are reused by the next call
+}
+
+// The sort key of a FILL ray (Args::sortFill): wavelength (2 bits), direction bin (cube-map face x 4 x 4)
+// and the 16^3 region of the start point in Morton order. Rays of one key start close together and head
+// the same way, so their paths cross the same cells for a while.
+__device__ __forceinline__ unsigned fillSortKey(const Args& a, double x, double y, double z, double kx, double ky,
+                                                double kz, int ell) {
+    const float fx = (float)kx, fy = (float)ky, fz = (float)kz;
+    const float ax = fabsf(fx), ay = fabsf(fy), az = fabsf(fz);
+    unsigned face;
+    float u, v, m;
+    if (ax >= ay && ax >= az) { face = fx > 0.f ? 0u : 1u; m = ax; u = fy; v = fz; }
+    else if (ay >= az) { face = fy > 0.f ? 2u : 3u; m = ay; u = fx; v = fz; }
+    else { face = fz > 0.f ? 4u : 5u; m = az; u = fx; v = fy; }
+    const float im = m > 0.f ? 1.f / m : 0.f;
+    const unsigned iu = (unsigned)min(3, max(0, (int)((u * im * 0.5f + 0.5f) * 4.f)));
+    const unsigned iv = (unsigned)min(3, max(0, (int)((v * im * 0.5f + 0.5f) * 4.f)));
+    const unsigned dir = (face * 4u + iu) * 4u + iv;
+    constexpr int R = 1 << kSortRegionBits;
+    auto cell = [](double t, double lo, double hi) {
+        return (unsigned)min(R - 1, max(0, (int)((float)((t - lo) / (hi - lo)) * (float)R)));
+    };
+    const unsigned mort = spread3(cell(x, a.gx0, a.gx1)) | (spread3(cell(y, a.gy0, a.gy1)) << 1) |
+                          (spread3(cell(z, a.gz0, a.gz1)) << 2);
+    return ((unsigned)(ell & 3) << (7 + 3 * kSortRegionBits)) | (dir << (3 * kSortRegionBits)) | mort;
 }
 
 // Global packet index of the j-th packet of this call. A sharded call (IdenticalAssigner,
@@ -2924,7 +3444,7 @@ __device__ __forceinline__ unsigned long long globalPacket(const Args& a, unsign
 
 template <int GRID, bool ONECOMP>
 __global__ void __launch_bounds__(kBlock) SKIRT_EVENT_ATTR eventKernel(const Args a) {
-    __shared__ unsigned long long resv[4 * (kBlock / 64) + 4];
+    __shared__ unsigned long long resv[5 * (kBlock / 64) + 5];
     extern __shared__ __attribute__((aligned(16))) double lds[];
     if (blockIdx.x == 0 && threadIdx.x == 0) a.ctr[4] = 0;  // the trace kernel's pull counter
     if (!a.init && a.ctr[2 + a.parity] == 0) return;  // an iteration after the end of the phase
@@ -3072,15 +3592,18 @@ __global__ void __launch_bounds__(kBlock) SKIRT_EVENT_ATTR eventKernel(const Arg
         // the peel-offs: one atomic each per block
         const bool active = mainMode != RAY_NONE;
         const int npeel = nray - (mainMode != RAY_NONE ? 1 : 0);
-        // a WALK ray goes to the top of the queue (Args::walkBack)
+        // a WALK ray goes to the top of the queue (Args::walkBack), a FILL ray to the FILL queue
         const bool back = a.walkBack && mainMode == RAY_WALK;
-        unsigned int pos, apos, dpos, wpos;
+        const bool fill = mainMode == RAY_FILL && a.sortFill;  // (sortFill: the FILL queue)
+        unsigned int pos, apos, dpos, wpos, fpos;
         {
-            unsigned* const ctrs[4] = {a.ctr + a.parity, a.ctr + 2 + (1 - a.parity), a.ctr + 5 + a.parity, a.ctr + 8 + a.parity};
-            const unsigned cnt[4] = {(unsigned)nray - (back ? 1u : 0u), active ? 1u : 0u, (unsigned)npeel, back ? 1u : 0u};
-            unsigned res[4];
-            blockReserve4(ctrs, cnt, res, resv);
-            pos = res[0]; apos = res[1]; dpos = res[2]; wpos = res[3];
+            unsigned* const ctrs[5] = {a.ctr + a.parity, a.ctr + 2 + (1 - a.parity), a.ctr + 5 + a.parity,
+                                       a.ctr + 8 + a.parity, a.ctr + kCtrFill + a.parity};
+            const unsigned cnt[5] = {(unsigned)nray - ((back || fill) ? 1u : 0u), active ? 1u : 0u, (unsigned)npeel,
+                                     back ? 1u : 0u, fill ? 1u : 0u};
+            unsigned res[5];
+            blockReserveN<5>(ctrs, cnt, res, resv);
+            pos = res[0]; apos = res[1]; dpos = res[2]; wpos = res[3]; fpos = res[4];
         }
 #ifdef SKIRT_EXPERIMENT_TIMELINE
         unsigned long long ts3 = stamp();
@@ -3089,8 +3612,8 @@ __global__ void __launch_bounds__(kBlock) SKIRT_EVENT_ATTR eventKernel(const Arg
         // the queue holds rayCap records (ensurePool sizes it for the slots' most rays per iteration): a
         // lane whose records would fall outside it writes none and fails the phase (ERR_QUEUE); the trace
         // kernel checks that the front and the WALK region do not meet
-        if ((unsigned long long)pos + (unsigned)(nray - (back ? 1 : 0)) > (unsigned long long)a.rayCap ||
-            (back && wpos >= (unsigned)a.rayCap) ||
+        if ((unsigned long long)pos + (unsigned)(nray - ((back || fill) ? 1 : 0)) > (unsigned long long)a.rayCap ||
+            (back && wpos >= (unsigned)a.rayCap) || (fill && fpos >= (unsigned)a.nslots) ||
             (unsigned long long)dpos + (unsigned)npeel > (unsigned long long)(a.rayCap - a.nslots)) {
             atomicOr(a.error, ERR_QUEUE);
             nray = 0;
@@ -3134,9 +3657,11 @@ __global__ void __launch_bounds__(kBlock) SKIRT_EVENT_ATTR eventKernel(const Arg
                 prm = mainParam;
                 idx = slot;
                 flags = mainMode | ((unsigned)p.ell << 18);
-                at = back ? (unsigned)a.rayCap - 1u - wpos : pos++;
+                at = fill ? fpos : back ? (unsigned)a.rayCap - 1u - wpos : pos++;
+                if (fill) a.fillKey[fpos] = fillSortKey(a, p.rx, p.ry, p.rz, dx, dy, dz, p.ell);
             }
-            E.emitRay(at, p, dx, dy, dz, prm, idx, flags, vcell);  // (one call site: one inlined grid entry)
+            // (one call site: one inlined grid entry)
+            E.emitRay((k >= npeel && fill) ? a.fillRays : a.rays, at, p, dx, dy, dz, prm, idx, flags, vcell);
         }
         // the slot stays active while it has a FILL/WALK ray in flight
         if (active) actOut[apos] = slot;
@@ -3251,7 +3776,7 @@ __global__ void __launch_bounds__(kBlock) contKernel(const Args a) {
                     const unsigned level = (unsigned)min(p.nscatt + 1, 255);
                     const unsigned flags = RAY_PEEL | (cat << 2) | ((unsigned)i << 4) | (level << 10) | ((unsigned)p.ell << 18);
                     a.det[dpos] = DetRec{Lp, 0.0, l, flags};
-                    E.emitRay(pos++, q, ins.kobs[0], ins.kobs[1], ins.kobs[2], Lp, (int)dpos, flags, qcell);
+                    E.emitRay(a.rays, pos++, q, ins.kobs[0], ins.kobs[1], ins.kobs[2], Lp, (int)dpos, flags, qcell);
                     dpos++;
                 }
             }
@@ -3366,6 +3891,10 @@ struct SkirtMcrt {
     // runs without the atomic-free WALK paths between the absorbing FILL paths: C3 2.16e8 -> 2.08e8, C2
     // 2.9e8 -> 2.8e8; C4 9.30e7 -> 9.38e7 (profiles/r03_walk_back_ab.txt)
     int walkBack = getenv("SKIRT_AMD_WALK_BACK") ? atoi(getenv("SKIRT_AMD_WALK_BACK")) : -1;
+    // the Labs line cache with sorted FILL rays (traceKernelCached) for absorbing phases on Cartesian grids and
+    // octree / k-d tree leaf maps: SKIRT_AMD_LABS_CACHE=0 turns it off (the per-lane buffered drain instead)
+    int labsCache = getenv("SKIRT_AMD_LABS_CACHE") ? atoi(getenv("SKIRT_AMD_LABS_CACHE")) : 0;
+    int lastCached = 0;        // whether the last phase traced through the cache
     int traceBlocksPerCU = 0;  // the occupancy the last trace launch was sized for
     int lastDetCopies = 0;  // SED copies of the last run's detect kernel
     double lastMs = 0;
@@ -3416,8 +3945,10 @@ int ensurePool(SkirtMcrt* c, int nslots, bool continuous, int halves) {
     if (rays >= (size_t)INT32_MAX) return fail(c, SKIRT_ERR_UNSUPPORTED, "ray queue too large");
     const int rayCap = (int)rays;
     const size_t path = continuous ? (size_t)nslots * (kPathCap * sizeof(PathRec) + sizeof(int)) : 0;
+    // + the FILL queue with its sort keys, ranks and order, and the sort's key counts
+    const size_t fillq = (size_t)nslots * (sizeof(RayRec) + 3 * 4) + (size_t)kSortBuckets * 4 + (size_t)kScanTop * 4 + 64;
     const size_t half = (size_t)rayCap * sizeof(RayRec) + (size_t)(rayCap - nslots) * sizeof(DetRec) +
-                        (size_t)nslots * (10 * 8 + 5 * 4 + 6 * 4 + 2 * 4) + path + 4096;
+                        (size_t)nslots * (10 * 8 + 5 * 4 + 6 * 4 + 2 * 4) + path + fillq + 4096;
     if (c->dPool && c->nslots == nslots && c->rayCap == rayCap && c->poolPath == (path > 0) && c->poolHalves == halves)
         return SKIRT_OK;
     c->poolPath = path > 0;
@@ -3494,6 +4025,15 @@ void carvePool(SkirtMcrt* c, Args& a, int h) {
         p += n * kPathCap * sizeof(PathRec);
         takeI(a.pathCnt);
     }
+    p = reinterpret_cast<char*>(((uintptr_t)p + 15) & ~(uintptr_t)15);
+    a.fillRays = reinterpret_cast<RayRec*>(p);
+    p += n * sizeof(RayRec);
+    takeU(a.fillKey); takeU(a.fillRank); takeU(a.fillPerm);
+    p = reinterpret_cast<char*>(((uintptr_t)p + 15) & ~(uintptr_t)15);
+    a.sortHist = reinterpret_cast<uint32_t*>(p);
+    p += (size_t)kSortBuckets * 4;
+    a.sortBlockSums = reinterpret_cast<uint32_t*>(p);
+    p += (size_t)kScanTop * 4;
     a.nslots = c->nslots;
     a.rayCap = c->rayCap;
     a.ctr = c->dCtr + kCtrWords * h;
@@ -4584,6 +5124,28 @@ static int runPhase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, uint6
                             + (size_t)kLabsBuf * kBlock * (sizeof(double) + sizeof(unsigned))  // + Labs buffers
                             + (size_t)3 * (kBlock / 64) * sizeof(unsigned);               // + segment counts
     const size_t ldsEvent = (size_t)a.ldsSedOff * sizeof(double);           // + instruments
+    // the cached trace kernel (absorbing phases on the grids whose walk adds one segment per step): the
+    // largest power-of-two number of cache sets that fits next to the tables
+    const bool leafKind = c->gridKind == SKIRT_GRID_OCTREE && leafMap;
+    const bool cacheGrid = (c->gridKind == SKIRT_GRID_CARTESIAN || leafKind) && a.hasDust;
+    size_t ldsCached = 0;
+    a.sortFill = 0;
+    a.cacheSets = 0;
+    if (c->labsCache && cacheGrid && a.store && !continuous) {
+        const size_t tables = (((size_t)a.ldsInstrOff * sizeof(double)) + 15) & ~(size_t)15;
+        const size_t fixed = (size_t)kCacheWaves * kEvictLines * (64 + 4) + 8 + (size_t)kCacheWaves * 3 * 4 + 16;
+        const size_t perSet = (size_t)kCacheWays * (8 + 64) + 4;
+        int sets = 1 << 12;
+        while (sets >= 8 && tables + fixed + (size_t)sets * perSet > c->ldsMax) sets >>= 1;
+        if (sets >= 8) {
+            a.sortFill = 1;
+            a.cacheSets = sets;
+            a.ldsCacheOff = (int)tables;
+            ldsCached = tables + fixed + (size_t)sets * perSet;
+        }
+    }
+    c->lastCached = a.sortFill;
+    a.cacheDebug = getenv("SKIRT_AMD_CACHE_DEBUG") ? atoi(getenv("SKIRT_AMD_CACHE_DEBUG")) : 0;
     // budget: what one workgroup may allocate (160 KiB on gfx950). The trace and event kernels need their
     // tables; the detect kernel keeps as many SED copies as fit (8, 4, 2, 1), or none (SEDs to the tally)
     const size_t budget = c->ldsMax;
@@ -4614,11 +5176,19 @@ static int runPhase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, uint6
                                                : SKIRT_WALK_TREE_NODES;
     const bool one = a.ncomp == 1;
     const void* traceFn = nullptr;
+    if (a.sortFill) {
+        if (kind == SKIRT_GRID_CARTESIAN) traceFn = one ? (const void*)traceKernelCached<SKIRT_GRID_CARTESIAN, true>
+                                                        : (const void*)traceKernelCached<SKIRT_GRID_CARTESIAN, false>;
+        else if (kind == SKIRT_GRID_OCTREE) traceFn = one ? (const void*)traceKernelCached<SKIRT_GRID_OCTREE, true>
+                                                          : (const void*)traceKernelCached<SKIRT_GRID_OCTREE, false>;
+        else traceFn = one ? (const void*)traceKernelCached<kBinTreeMap, true> : (const void*)traceKernelCached<kBinTreeMap, false>;
+    }
     auto pick = [&](auto fn1, auto fnN, auto fn1c, auto fnNc) {
         traceFn = continuous ? (one ? (const void*)fn1c : (const void*)fnNc) : (one ? (const void*)fn1 : (const void*)fnN);
     };
 #define SKIRT_PICK(G) pick(traceKernel<G, true, false>, traceKernel<G, false, false>, traceKernel<G, true, true>, traceKernel<G, false, true>)
-    if (kind == SKIRT_GRID_CARTESIAN) SKIRT_PICK(SKIRT_GRID_CARTESIAN);
+    if (a.sortFill) {}
+    else if (kind == SKIRT_GRID_CARTESIAN) SKIRT_PICK(SKIRT_GRID_CARTESIAN);
     else if (kind == SKIRT_GRID_OCTREE) SKIRT_PICK(SKIRT_GRID_OCTREE);
     else if (kind == kBinTreeMap) SKIRT_PICK(kBinTreeMap);
     else if (kind == kOctreeBookkeeping) SKIRT_PICK(kOctreeBookkeeping);
@@ -4626,10 +5196,15 @@ static int runPhase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, uint6
         pick(traceKernelVor<true, false>, traceKernelVor<false, false>, traceKernelVor<true, true>, traceKernelVor<false, true>);
     else SKIRT_PICK(kOctreeNodes);
 #undef SKIRT_PICK
-    if (ldsTrace > 64 * 1024)
-        HIPCHECK(c, hipFuncSetAttribute(traceFn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ldsTrace));
+    const size_t ldsT = a.sortFill ? ldsCached : ldsTrace;
+    const int tblock = a.sortFill ? kCacheBlock : kBlock;
+    if (ldsT > 64 * 1024)
+        HIPCHECK(c, hipFuncSetAttribute(traceFn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ldsT));
     int tgrid = c->traceGrid;
-    if (tgrid <= 0) {
+    if (a.sortFill) {
+        tgrid = std::max(1, c->nCusT);  // one workgroup of 12 waves per CU
+        c->traceBlocksPerCU = 1;
+    } else if (tgrid <= 0) {
         int per = 0;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, traceFn, kBlock, ldsTrace) != hipSuccess || per < 1) per = 2;
         tgrid = std::max(1, c->nCusT) * per;
@@ -4673,7 +5248,7 @@ static int runPhase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, uint6
     auto launchTrace = [&](const Args& aa, hipStream_t st) {
         // the kernel picked above (traceFn), launched through its generic entry
         void* args[] = {const_cast<Args*>(&aa)};
-        return hipLaunchKernel(traceFn, dim3(tgrid), dim3(kBlock), args, ldsTrace, st);
+        return hipLaunchKernel(traceFn, dim3(tgrid), dim3(tblock), args, ldsT, st);
     };
     if ((int)c->pollEv.size() < kMaxHalves * kPollRing) {
         while ((int)c->pollEv.size() < kMaxHalves * kPollRing) {
@@ -4715,6 +5290,7 @@ static int runPhase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, uint6
     for (int h = 0; h < halves; h++) {
         ah[h] = a;
         carvePool(c, ah[h], h);
+        if (!a.sortFill || (a.cacheDebug & 2)) ah[h].fillPerm = nullptr;  // FILL rays traced in queue order
     }
     // the detect kernel of half h's last trace launch (on sE, after that launch), then the counter copy
     auto detect = [&](int h) -> int {
@@ -4759,6 +5335,16 @@ static int runPhase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, uint6
             launchEvent(aa, sE);
             HIPCHECK(c, hipGetLastError());
             if (!a.hasDust) { done[h] = true; its[h]++; continue; }  // every packet completes in the event kernel
+            if (aa.sortFill && aa.fillPerm) {  // the FILL rays in key order (their count is on the device)
+                const int sgrid = std::max(1, std::min((c->nslots + kBlock - 1) / kBlock, c->numCUs * 8));
+                HIPCHECK(c, hipMemsetAsync(aa.sortHist, 0, (size_t)kSortBuckets * 4, sE));
+                hipLaunchKernelGGL(sortRankKernel, dim3(sgrid), dim3(kBlock), 0, sE, aa);
+                hipLaunchKernelGGL(sortScanSumsKernel, dim3(kScanTop), dim3(kBlock), 0, sE, aa);
+                hipLaunchKernelGGL(sortScanTopKernel, dim3(1), dim3(kScanTop / 2), 0, sE, aa);
+                hipLaunchKernelGGL(sortScanApplyKernel, dim3(kScanTop), dim3(kBlock), 0, sE, aa);
+                hipLaunchKernelGGL(sortPlaceKernel, dim3(sgrid), dim3(kBlock), 0, sE, aa);
+                HIPCHECK(c, hipGetLastError());
+            }
             if (sE != sT[h]) {
                 HIPCHECK(c, hipEventRecord(c->evE[h], sE));
                 HIPCHECK(c, hipStreamWaitEvent(sT[h], c->evE[h], 0));

@@ -90,22 +90,27 @@ struct Result {
 // set-associative LRU cache of lines (8 ways); returns misses that evict (requests), flushes at the end
 struct LineCache {
     int sets, ways = 8;
+    int policy = 0;  // 0 LRU, 1 FIFO (round robin victim per set), 2 a victim chosen by the line's hash
+    std::vector<unsigned> rr;
     std::vector<long long> tag;
     std::vector<unsigned> age;
     unsigned clock = 0;
     double requests = 0;
-    explicit LineCache(int lines) : sets(std::max(1, lines / 8)), tag((size_t)sets * 8, -1), age((size_t)sets * 8, 0) {}
+    explicit LineCache(int lines, int pol = 0) : policy(pol), rr(std::max(1, lines / 8), 0), sets(std::max(1, lines / 8)), tag((size_t)sets * 8, -1), age((size_t)sets * 8, 0) {}
     void touch(long long line) {
         const size_t s = (size_t)(((unsigned long long)line * 0x9E3779B97F4A7C15ull) >> 40) % (size_t)sets;
         long long* t = &tag[s * 8];
         unsigned* a = &age[s * 8];
         clock++;
         int victim = 0;
+        bool empty = false;
         for (int w = 0; w < ways; w++) {
-            if (t[w] == line) { a[w] = clock; return; }
-            if (t[w] < 0) { victim = w; a[victim] = 0; break; }
+            if (t[w] == line) { if (policy == 0) a[w] = clock; return; }
+            if (t[w] < 0) { victim = w; a[victim] = 0; empty = true; break; }
             if (a[w] < a[victim]) victim = w;
         }
+        if (!empty && policy == 1) victim = (int)(rr[s]++ % 8);
+        if (!empty && policy == 2) victim = (int)(((unsigned long long)line * 0xD6E8FEB86659FD93ull) >> 61);
         if (t[victim] >= 0) requests += 1;
         t[victim] = line;
         a[victim] = clock;
@@ -146,7 +151,7 @@ struct EpochCache {
 };
 
 Result simulate(const std::vector<Ray>& rays, const std::vector<int>& lines, const std::vector<uint32_t>& order,
-                int W, const std::vector<int>& cacheSizes, int kWavesPerWG, bool randomPulls, int K, bool coldFlush) {
+                int W, const std::vector<int>& cacheSizes, int kWavesPerWG, bool randomPulls, int K, bool coldFlush, bool missMerge, int policy) {
     constexpr int kChunk = 64, kBuf = 16, kLanes = 64;
     Result res;
     res.cache.assign(cacheSizes.size(), 0.0);
@@ -154,7 +159,7 @@ Result simulate(const std::vector<Ray>& rays, const std::vector<int>& lines, con
     const size_t nchunks = (order.size() + kChunk - 1) / kChunk;
     for (int g = 0; g < W / kWavesPerWG; g++) {
         std::vector<LineCache> caches;
-        for (int c : cacheSizes) caches.emplace_back(c);
+        for (int c : cacheSizes) caches.emplace_back(c, policy);
         std::vector<EpochCache> ecaches;
         for (int c : cacheSizes) ecaches.emplace_back(c, coldFlush);
         std::vector<std::vector<long long>> lastDirect(cacheSizes.size(), std::vector<long long>((size_t)kWavesPerWG * kLanes, -1));
@@ -202,7 +207,9 @@ Result simulate(const std::vector<Ray>& rays, const std::vector<int>& lines, con
                     for (size_t q = 0; q < ecaches.size(); q++) {
                         long long& ld = lastDirect[q][(size_t)(&wv - &waves[0]) * kLanes + l];
                         if (!ecaches[q].touch(line)) {
-                            if (ld != line) ecaches[q].requests += 1;
+                            // a miss leaves at once, one request per add (LOC_MISS_MERGE=1: consecutive misses of
+                            // a lane into one line share one)
+                            if (!missMerge || ld != line) ecaches[q].requests += 1;
                             ld = line;
                         } else {
                             ld = -1;
@@ -337,6 +344,10 @@ int main(int argc, char** argv) {
     add("region16^3+octant", [&](const Ray& y) { return ((unsigned long long)cellOf(y, 4) << 3) | octant(y); });
     add("octant+region32^3", [&](const Ray& y) { return ((unsigned long long)octant(y) << 15) | cellOf(y, 5); });
     add("dir6x4^2+region16^3", [&](const Ray& y) { return ((unsigned long long)dirBin(y.k, 4) << 12) | cellOf(y, 4); });
+    add("dir6x4^2+region32^3", [&](const Ray& y) { return ((unsigned long long)dirBin(y.k, 4) << 15) | cellOf(y, 5); });
+    add("dir6x4^2+region8^3", [&](const Ray& y) { return ((unsigned long long)dirBin(y.k, 4) << 9) | cellOf(y, 3); });
+    add("dir6x2^2+region16^3", [&](const Ray& y) { return ((unsigned long long)dirBin(y.k, 2) << 12) | cellOf(y, 4); });
+    add("dir6x3^2+region16^3", [&](const Ray& y) { return ((unsigned long long)dirBin(y.k, 3) << 12) | cellOf(y, 4); });
     add("dir6x8^2+region8^3", [&](const Ray& y) { return ((unsigned long long)dirBin(y.k, 8) << 9) | cellOf(y, 3); });
     add("dir6x8^2+region32^3", [&](const Ray& y) { return ((unsigned long long)dirBin(y.k, 8) << 15) | cellOf(y, 5); });
     add("dir6x8^2+region64^3", [&](const Ray& y) { return ((unsigned long long)dirBin(y.k, 8) << 18) | cellOf(y, 6); });
@@ -369,7 +380,7 @@ int main(int argc, char** argv) {
         std::vector<uint32_t> idx(nr);
         std::iota(idx.begin(), idx.end(), 0u);
         std::stable_sort(idx.begin(), idx.end(), [&](uint32_t a, uint32_t b) { return o.key[a] < o.key[b]; });
-        Result r = simulate(st.rays, lines, idx, W, cacheSizes, G, randomPulls, K, env("LOC_COLD", 1) != 0);
+        Result r = simulate(st.rays, lines, idx, W, cacheSizes, G, randomPulls, K, env("LOC_COLD", 1) != 0, env("LOC_MISS_MERGE", 0) != 0, env("LOC_POLICY", 0));
         std::printf("%-24s %8.3f %8.3f %8.3f %8s", o.name.c_str(), r.adds / r.run, r.adds / r.instr, r.adds / r.window, "");
         for (double c : r.cache) std::printf(" %9.3f", r.adds / c);
         for (double c : r.epoch) std::printf(" %9.3f", r.adds / c);
