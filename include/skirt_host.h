@@ -97,6 +97,31 @@ SkirtVoronoi* skirt_host_voronoi_build(const double* sites, int nsites, const do
 int skirt_host_voronoi_describe(const SkirtVoronoi* v, SkirtGridDesc* grid);
 void skirt_host_voronoi_free(SkirtVoronoi* v);
 
+/* The cross-GPU sums in C++: RCCL (NCCL API) all-reduces over xGMI, the MI355X counterpart of the
+ * reference's MPI_Allreduce of the absorption tables and instrument arrays (PanDustSystem.cpp:394-404,
+ * Instrument.cpp:57-66, MPIsupport/ProcessManager.cpp:133-137).
+ * skirt_rccl_create makes one communicator per device of this process (ncclCommInitAll over `devices`);
+ * skirt_rccl_reducer is the engine's reducer callback (skirt_mcrt_set_reducer) and skirt_rccl_rank(r, rank)
+ * its user pointer for the engine of rank `rank`: the callback sums the tally in place, ncclSum of doubles,
+ * on the stream the engine hands it. Each rank's engine must then be driven by its own host thread (the
+ * collectives of the ranks meet on the devices). A process that runs one rank of a multi-process job
+ * creates its communicator through its own bootstrap (e.g. ncclCommInitRank, or torch.distributed) and can
+ * use the same callback through skirt_rccl_wrap. */
+typedef struct SkirtRccl SkirtRccl;
+int skirt_rccl_create(int ndev, const int* devices, SkirtRccl** out);
+/* wraps an existing communicator (an ncclComm_t) of one rank: ndev = 1, rank 0 */
+int skirt_rccl_wrap(void* nccl_comm, SkirtRccl** out);
+void* skirt_rccl_rank(SkirtRccl* r, int rank);
+SkirtReduceTallyFn skirt_rccl_reducer(void);
+void skirt_rccl_destroy(SkirtRccl* r);
+/* The driver of `skirt-mi355x -g N`: loads the ski once per device, runs every phase of the simulation
+ * with each device shooting its rank's slice of every wavelength (one host thread per device) and the
+ * tallies summed by skirt_rccl at each phase end, then writes the outputs from rank 0. packages > 0 and
+ * seed != 0 override the ski's. stats (may be NULL) receives rank 0's statistics; seconds (may be NULL)
+ * the wall time of the photon phases. */
+int skirt_sim_run_devices(const char* ski, const char* datadir, int ndev, double packages, uint64_t seed,
+                          const char* outprefix, SkirtStats* stats, double* seconds);
+
 #ifdef __cplusplus
 }
 #endif

@@ -2546,36 +2546,35 @@ struct LabsCache {
             else if (freeWay >= 0) done = tryInsert(w0 + (unsigned)freeWay, line, e, v);
             else {
                 evict = true;
-                vway = ldsAdd32(rr + w0 / kCacheWays, 1u) & (kCacheWays - 1);
+                vway = ldsAdd32(rr + w0 / kCacheWays, 1u) & (kCacheWays - 1);  // round robin (FIFO)
             }
             if (!done && !evict) { doff = idx * 8u; dval = v; }
         }
         const unsigned long long em = __ballot(evict);
-        if (em) {
-            const unsigned slot = (unsigned)__popcll(em & ((1ull << lane) - 1ull));
-            if (evict) {
-                const bool ok = slot < (unsigned)kEvictLines && tryEvict(w0 + vway, line, e, v, slot);
-                if (!ok) {
-                    if (slot < (unsigned)kEvictLines) evTag[slot] = kCacheEmpty;
-                    doff = idx * 8u;
-                    dval = v;
-                }
+        const unsigned slot = (unsigned)__popcll(em & ((1ull << lane) - 1ull));
+        if (evict) {
+            const bool ok = slot < (unsigned)kEvictLines && tryEvict(w0 + vway, line, e, v, slot);
+            if (!ok) {
+                if (slot < (unsigned)kEvictLines) evTag[slot] = kCacheEmpty;
+                doff = idx * 8u;
+                dval = v;
             }
-            ldsOrder();
-            // the evicted lines: lane q adds entry q & 7 of line q >> 3
-            const unsigned nev = min((unsigned)__popcll(em), (unsigned)kEvictLines);
-            const unsigned j = (unsigned)lane >> 3, ee = (unsigned)lane & 7u;
-            const unsigned tg = j < nev ? evTag[j] : kCacheEmpty;
-            const double ev = evData[j * 8 + ee];
-            bufferAtomicAddF64(ev, rsrc, (int)((tg != kCacheEmpty && ev != 0.0) ? tg * 64u + ee * 8u : oob), 0, 0);
-            requests += (unsigned)__popcll(__ballot(ee == 0 && tg != kCacheEmpty));
-            ldsOrder();
         }
-        const unsigned long long dm = __ballot(doff != oob);
-        if (dm) {
-            bufferAtomicAddF64(dval, rsrc, (int)doff, 0, 0);
-            requests += (unsigned)__popcll(dm);
-        }
+        ldsOrder();
+        // The evicted lines (lane q adds entry q & 7 of line q >> 3) and the direct adds leave as two buffer
+        // atomics that every step issues, lanes without an add at an offset past Labs (dropped): a fixed
+        // count of vector-memory operations per step, so that the next step's leaf-map load is waited for
+        // alone, not with these atomics (s_waitcnt vmcnt counts them all; an atomic under a branch makes
+        // the compiler wait with vmcnt(0))
+        const unsigned nev = min((unsigned)__popcll(em), (unsigned)kEvictLines);
+        const unsigned j = (unsigned)lane >> 3, ee = (unsigned)lane & 7u;
+        const unsigned tg = j < nev ? evTag[j] : kCacheEmpty;
+        const double ev = evData[j * 8 + ee];
+        bufferAtomicAddF64(ev, rsrc, (int)((tg != kCacheEmpty && ev != 0.0) ? tg * 64u + ee * 8u : oob), 0, 0);
+        requests += (unsigned)__popcll(__ballot(ee == 0 && tg != kCacheEmpty));
+        ldsOrder();
+        bufferAtomicAddF64(dval, rsrc, (int)doff, 0, 0);
+        requests += (unsigned)__popcll(__ballot(doff != oob));
     }
 
     // after the workgroup's last ray: every cached line to Labs (8 lanes per line)
@@ -3894,7 +3893,7 @@ struct SkirtMcrt {
     // the Labs line cache with sorted FILL rays (traceKernelCached) for absorbing phases on Cartesian grids and
     // octree / k-d tree leaf maps: SKIRT_AMD_LABS_CACHE=0 turns it off (the per-lane buffered drain instead)
     int labsCache = getenv("SKIRT_AMD_LABS_CACHE") ? atoi(getenv("SKIRT_AMD_LABS_CACHE")) : 0;
-    int lastCached = 0;        // whether the last phase traced through the cache
+    int lastCached = 0;        // the cache sets of the last phase's trace kernel (0: the per-lane drain)
     int traceBlocksPerCU = 0;  // the occupancy the last trace launch was sized for
     int lastDetCopies = 0;  // SED copies of the last run's detect kernel
     double lastMs = 0;
@@ -5144,7 +5143,7 @@ static int runPhase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, uint6
             ldsCached = tables + fixed + (size_t)sets * perSet;
         }
     }
-    c->lastCached = a.sortFill;
+    c->lastCached = a.sortFill ? a.cacheSets : 0;
     a.cacheDebug = getenv("SKIRT_AMD_CACHE_DEBUG") ? atoi(getenv("SKIRT_AMD_CACHE_DEBUG")) : 0;
     // budget: what one workgroup may allocate (160 KiB on gfx950). The trace and event kernels need their
     // tables; the detect kernel keeps as many SED copies as fit (8, 4, 2, 1), or none (SEDs to the tally)
@@ -5547,6 +5546,7 @@ int skirt_mcrt_stats(SkirtMcrt* c, SkirtStats* out) {
     out->device_cells = c->ndev;
     out->trace_blocks_per_cu = (uint64_t)c->traceBlocksPerCU;
     out->packages = c->packagesTotal;
+    out->labs_cache_sets = (uint64_t)c->lastCached;
     return SKIRT_OK;
 }
 

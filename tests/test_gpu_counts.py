@@ -33,7 +33,7 @@ CASES = [
     ("pan_oct", 3000, False),
     ("vor_pan", 1000, False),
     ("pan_cart16_sa", 1000, True),
-    ("c3_oct128", 20, False),  # the headline workload at full grid size (622,490 leaves)
+    ("c3_oct128", 20000, False),  # the headline workload at full grid size (622,490 leaves), 5e5 packets
 ]
 
 

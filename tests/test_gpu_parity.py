@@ -407,16 +407,23 @@ def test_many_wavelengths_match_oracle_same_streams(copies, monkeypatch):
 BENCH = os.path.join(os.path.dirname(GOLD), "..", "benchmarks")
 
 
-@pytest.mark.parametrize("config,packages", [("c2_cart64", 50), ("c3_oct128", 20), ("c4_vor1e5", 20),
-                                             ("c5_oct128_sa", 4)])
-def test_benchmark_models_match_oracle_same_streams(config, packages):
+@pytest.mark.parametrize("config,packages,cache", [("c2_cart64", 20000, "0"), ("c2_cart64", 20000, "1"),
+                                                   ("c3_oct128", 20000, "0"), ("c3_oct128", 20000, "1"),
+                                                   ("c4_vor1e5", 20000, "0"), ("c5_oct128_sa", 2000, "0"),
+                                                   ("c5_oct128_sa", 2000, "1")])
+def test_benchmark_models_match_oracle_same_streams(config, packages, cache, monkeypatch):
     """The BASELINE configurations at their full grid sizes (C2 64^3 Cartesian, C3 622,490-leaf octree, C4
-    1e5-site Voronoi, C5 = C3 with self-absorption and dust emission), with few packets per wavelength:
-    engine = oracle on the same Philox streams, every phase the model has."""
+    1e5-site Voronoi, C5 = C3 with self-absorption and dust emission), at 2e4 packages per wavelength (2e3
+    for C5, all of its phases): 5e5 C3 packets, whose paths reach the tree walk's rare branches (the on-face
+    neighbour search, the nextafter escape of TreeDustGrid.cpp:502-519) and the Voronoi walk's exact
+    re-evaluation. Engine = oracle on the same Philox streams, with the Labs line cache off and on
+    (SKIRT_AMD_LABS_CACHE; the cache takes the absorbing phases of the Cartesian and octree grids)."""
+    monkeypatch.setenv("SKIRT_AMD_LABS_CACHE", cache)
     path = os.path.join(BENCH, config + ".ski")
     sim = S.Simulation(path, packages=packages)
     sim.attach(0)
     sim.run_stellar()
+    cached = sim.stats()["labs_cache_sets"] > 0  # (the stellar phase's trace kernel)
     sim.run_dust()
     sim.fetch()
     orc = O.run(path, rng=O.RNG_PHILOX, threads=16, packages=packages, phases=O.PHASES_ALL)
@@ -431,6 +438,47 @@ def test_benchmark_models_match_oracle_same_streams(config, packages):
     np.testing.assert_allclose(seds, orc.seds[0], rtol=rtol, atol=1e-300)
     np.testing.assert_allclose(frames.sum(axis=2), orc.frames[0].sum(axis=2), rtol=rtol, atol=1e-300)
     assert_parity(frames, orc.frames[0], rtol, DUST_OUTLIERS if dust else STELLAR_OUTLIERS, "frames")
+    assert cached == (cache == "1" and not config.startswith("c4"))
+
+
+@pytest.mark.parametrize("config,cache", [("c3_oct128", "0"), ("c3_oct128", "1"), ("c4_vor1e5", "0")])
+def test_full_size_phase_properties(config, cache, monkeypatch):
+    """The benchmark workload at its full per-GPU size (5e6 packages per wavelength, 1.25e8 packets, the
+    2^24-slot pool and its ray queues under full pressure), checked through properties that hold at any
+    size: (1) the transparent flux is the emitted luminosity exactly (every launched packet is detected
+    once at its full weight: L_lambda / (4 pi d^2) per wavelength, FullInstrument.cpp:115); (2) two
+    halves of every wavelength's packets (the reference's IdenticalAssigner split over two ranks, shot
+    in their own phases with their own slot schedules) add up to the whole phase cell for cell, pixel for
+    pixel, to the order of the atomic additions."""
+    monkeypatch.setenv("SKIRT_AMD_LABS_CACHE", cache)
+    path = os.path.join(BENCH, config + ".ski")
+    packages = 5e6
+
+    def shoot(rank=None):
+        sim = S.Simulation(path, packages=packages)
+        sim.attach(0)
+        if rank is None:
+            sim.run_stellar()
+        else:
+            sim.set_reducer(lambda tally, ptr, n, stream: None)  # one process: the caller sums
+            sim.run_stellar_shard(rank, 2)
+        sim.fetch()
+        return sim
+
+    full = shoot()
+    st = full.stats()
+    assert st["packets"] > 1e8 and (st["labs_cache_sets"] > 0) == (cache == "1" and config.startswith("c3"))
+    # the emitted luminosity per wavelength: the transparent tally of one packet per wavelength (one stellar
+    # component: every packet carries L_lambda / Npp, FullInstrument.cpp:115 adds it unattenuated)
+    lum = O.run(path, rng=O.RNG_PHILOX, threads=1, packages=1).seds[0][0]
+    trav = full.instrument(0)[1][0]  # FullInstrument slot 0 (transparent), before calibration
+    assert np.count_nonzero(lum) >= 20
+    np.testing.assert_allclose(trav, lum, rtol=1e-10, atol=0)
+    halves = [shoot(r) for r in (0, 1)]
+    np.testing.assert_allclose(halves[0].labs() + halves[1].labs(), full.labs(), rtol=1e-10, atol=1e-300)
+    for k in (0, 1):
+        np.testing.assert_allclose(halves[0].instrument(0)[k] + halves[1].instrument(0)[k], full.instrument(0)[k],
+                                   rtol=1e-10, atol=1e-300)
 
 
 def test_continuous_scattering_with_several_instruments(tmp_path):
