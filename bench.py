@@ -52,10 +52,13 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip-level parameters (spec)
 ATOMIC_PEAK_REQUESTS = 2.36e10
 
 
-# VALU issue peak of the chip in wave-instructions per second: a wave issues one VALU instruction over 2
-# cycles (MI355X_MICROARCH.md, "32 lanes/cycle x 2"), so 0.5 per SIMD per cycle, 4 SIMDs x 256 CUs, at the
-# 2.4 GHz maximum clock (the clock under load is lower; f64 arithmetic takes more cycles per instruction)
-VALU_ISSUE_PEAK = 256 * 4 * 0.5 * 2.4e9
+# The chip's SIMDs and XCDs (MI355X_MICROARCH.md): the VALU-busy fraction is the gfx94x VALUBusy formula
+# (ROCm 7.2 applies it to gfx950, MI355X_MICROARCH.md "rocprofv3 PMC slots"): SQ_ACTIVE_INST_VALU counts the
+# quad-cycles (4 cycles) in which a wave issues a VALU instruction, summed over waves, over the SIMD-cycles of
+# the launch; GRBM_GUI_ACTIVE is summed over the 8 XCDs (per XCD it times the launch at the 2.37 GHz the
+# chip holds: profiles/r05_rocprof_*.txt)
+SIMDS = 256 * 4
+XCDS = 8
 
 
 def pmc_traffic(config):
@@ -67,8 +70,16 @@ def pmc_traffic(config):
         return None
     with open(path) as f:
         d = json.load(f)
-    return {"bytes_per_launch": d["traffic_bytes_per_launch"], "source": d["source"],
-            "valu_per_launch": d.get("valu_insts_per_launch")}
+    out = {"bytes_per_launch": d["traffic_bytes_per_launch"], "source": d["source"],
+           "valu_per_launch": d.get("valu_insts_per_launch")}
+    grbm = d.get("grbm_gui_active_per_launch")
+    if grbm and d.get("valu_active_quads_per_launch"):
+        simd_cycles = SIMDS * grbm / XCDS
+        out["valu_busy"] = 4 * d["valu_active_quads_per_launch"] / simd_cycles
+        if d.get("inst_active_quads_per_launch"):
+            # any instruction issued, summed over the waves of a SIMD (types issue in parallel: may pass 1)
+            out["inst_busy"] = 4 * d["inst_active_quads_per_launch"] / simd_cycles
+    return out
 
 
 def bound_of(hbm_frac, atomic_frac):
@@ -239,9 +250,8 @@ def main():
     traffic = pmc_traffic(args.config) if ppl == ppl_default else None
     hbm_frac = achieved / HBM_PEAK_GBS
     traffic_frac = traffic["bytes_per_launch"] / launch_s / 1e9 / HBM_PEAK_GBS if traffic else None
-    # instruction issue: VALU wave-instructions per second (PMC) over the chip's issue peak
-    issue_frac = (traffic["valu_per_launch"] / launch_s / VALU_ISSUE_PEAK
-                  if traffic and traffic.get("valu_per_launch") else None)
+    # instruction issue: the fraction of SIMD cycles the VALU is busy (PMC, cycle-based)
+    valu_busy = traffic.get("valu_busy") if traffic else None
     # the same launch priced at the bytes this engine's layouts read (ENGINE_SEGMENT_BYTES)
     engine_bytes = (segs * ENGINE_SEGMENT_BYTES[info.grid_kind] + delta["absorb_adds"] * 16) / max(1, trace_launches)
     requests_per_s = delta["labs_requests"] / max(1e-9, trace_ms / 1e3)
@@ -299,8 +309,8 @@ def main():
             "frac_basis": "algorithmic bytes (SURVEY 8(d))" if (hbm_frac <= 1.0 or traffic_frac is None) else
                           "measured HBM traffic (the SURVEY bytes model a cache-resident working set: %.2f of peak)" % hbm_frac,
             "atomic_frac": atomic_frac,
-            "issue_frac": issue_frac,
-            "valu_issue_peak": VALU_ISSUE_PEAK,
+            "valu_busy": valu_busy,
+            "inst_busy": traffic.get("inst_busy") if traffic else None,
             "traffic": traffic["bytes_per_launch"] if traffic else None,
             "kernel": {0: "traceKernel<cartesian>", 1: "traceKernel<octree leaf map>", 2: "traceKernel<voronoi>"}[info.grid_kind],
             "launch_ms_avg": launch_s * 1e3,

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define SKIRT_MCRT_ABI_VERSION 12  /* 11: SkirtStats::packages; 12: SkirtStats::labs_cache_sets */
+#define SKIRT_MCRT_ABI_VERSION 13  /* 11: SkirtStats::packages; 12: SkirtStats::labs_cache_sets; 13: without it */
 
 enum {
     SKIRT_OK = 0,
@@ -192,8 +192,6 @@ typedef struct {
                                    wavelengths; wavelengths or cells without luminosity launch none):
                                    SURVEY 8(d)'s throughput unit, summed over the phases since the last
                                    skirt_mcrt_zero_tallies */
-    uint64_t labs_cache_sets;   /* the last phase's trace kernel added Labs through an LDS line cache of this many
-                                   sets of 8 lines per workgroup (sorted FILL rays, SKIRT_AMD_LABS_CACHE); 0: without */
 } SkirtStats;
 
 /* grid walks of the trace kernel (SkirtStats::grid_walk) */

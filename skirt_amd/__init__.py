@@ -18,7 +18,7 @@ import os
 import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
-ABI_VERSION = 12  # SKIRT_MCRT_ABI_VERSION of include/skirt_mcrt.h
+ABI_VERSION = 13  # SKIRT_MCRT_ABI_VERSION of include/skirt_mcrt.h
 # SKIRT_AMD_LIB selects another build of the same library (e.g. a tuning variant built by
 # tools/build_variant.sh next to the default one)
 LIB_PATH = os.path.join(PKG_DIR, os.environ.get("SKIRT_AMD_LIB", "libskirt_amd.so"))
@@ -40,8 +40,7 @@ class SkirtStats(ctypes.Structure):
                 ("iterations", ctypes.c_uint64), ("kernel_ms", ctypes.c_double), ("trace_ms", ctypes.c_double),
                 ("trace_launches", ctypes.c_uint64), ("grid_walk", ctypes.c_int32), ("map_level", ctypes.c_int32),
                 ("labs_requests", ctypes.c_uint64), ("device_cells", ctypes.c_uint64),
-                ("trace_blocks_per_cu", ctypes.c_uint64), ("packages", ctypes.c_uint64),
-                ("labs_cache_sets", ctypes.c_uint64)]
+                ("trace_blocks_per_cu", ctypes.c_uint64), ("packages", ctypes.c_uint64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

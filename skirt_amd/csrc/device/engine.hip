@@ -42,17 +42,8 @@ namespace {
 
 constexpr double kDblMax = 1.7976931348623157e308;
 constexpr int kBlock = 256;
-#ifndef SKIRT_LABS_BUF
-#define SKIRT_LABS_BUF 16
-#endif
-constexpr int kLabsBuf = SKIRT_LABS_BUF;  // buffered Labs adds per trace lane (LDS)
-#ifndef SKIRT_STEPS_PER_PULL
-#define SKIRT_STEPS_PER_PULL 4
-#endif
-constexpr int kStepsPerPull = SKIRT_STEPS_PER_PULL;  // grid steps between two ray pulls of a trace wave
-#ifndef SKIRT_PULL_CHUNK
-#define SKIRT_PULL_CHUNK 64        // queue ids a trace wave reserves at once (0: exactly its idle lanes; >= 64)
-#endif
+constexpr int kLabsBuf = 16;      // buffered Labs adds per trace lane (LDS)
+constexpr int kStepsPerPull = 4;  // grid steps between two ray pulls of a trace wave
 // The slot pool runs as one or two independent pipelines ("halves", SkirtMcrt::halves): with two, one
 // half's event and detect kernels run beside the other half's trace kernel, on CUs of their own (CU-masked
 // streams, see runPhase).
@@ -62,52 +53,16 @@ constexpr int kSersicTable = 202;  // SersicFunction: 101 radii, then 101 cumula
 constexpr int kDetectCopies = 8;   // most LDS copies of the SED sums in the detect kernel (one per 8 lanes)
 constexpr int kPollEvery = 1;      // iterations between two counter copies of a half
 constexpr int kPollRing = 3;       // copies in flight per half (the host reads each kPollRing copies late)
-// Sorted FILL rays and the LDS line cache of the Labs adds (traceBodyCached).
-// The sort key of a FILL ray: its wavelength (2 bits: the few wavelengths in flight stay apart), its
-// direction (cube-map face x 4 x 4 bins) and the 16^3 region of its start point (Morton order).
-constexpr int kSortRegionBits = 4;
-constexpr int kSortKeyBits = 2 + 7 + 3 * kSortRegionBits;
-constexpr unsigned kSortBuckets = 1u << kSortKeyBits;
-constexpr int kScanChunk = 1024;                         // buckets per block of the scan kernels
-#ifndef SKIRT_CACHE_BLOCK
-#define SKIRT_CACHE_BLOCK 768
-#endif
-constexpr int kCacheBlock = SKIRT_CACHE_BLOCK;           // the cached trace kernel: 12 waves, one workgroup per CU
-constexpr int kCacheWays = 8;                            // lines per set
-constexpr int kEvictLines = 8;                           // evicted lines a wave hands out per grid step
-constexpr unsigned kCacheEmpty = 0xFFFFFFFFu;            // the tag of a free line
-constexpr int kCtrFill = 10;                             // ctr[10 + q]: FILL rays of the iteration
-// occupancy attribute of the trace kernel (a build knob for tuning variants, tools/build_variant.sh):
-// 3 waves per SIMD, i.e. at most 168 VGPRs (the grid entry on the pull path would otherwise take the
-// octree kernel to 175 and 2 waves; C3 1.91e8 -> 2.15e8 pkt/s at 3). The Voronoi walk has its own
-// kernel and attribute below.
-// leaf-map step: check the estimated finest cell against the found leaf's faces instead of the finest
-// cell's own split coordinates (see LeafMapGrid::step; 0 restores the finest-cell check: C3 2.154e8 ->
-// 2.162e8, C5 1.071e8 -> 1.091e8 pkt/s with 1)
-#ifndef SKIRT_LEAF_CHECK_FACES
-#define SKIRT_LEAF_CHECK_FACES 1
-#endif
-// leaf-map walk: the next step's leaf-map entry is requested at the end of a step (before the wave's Labs
-// drain), not at the start of the next one. A load waits for every older vector-memory operation of its
-// wave (vmcnt counts in issue order, atomics included), and a no-return f64 atomic stays counted for
-// thousands of cycles under load (MI355X_MICROARCH.md, float atomic add row): requested after the drain,
-// each step's entry waited for the previous step's Labs atomic too.
-#ifndef SKIRT_LEAF_PREFETCH
-#define SKIRT_LEAF_PREFETCH 1
-#endif
-#ifndef SKIRT_TRACE_ATTR
+// occupancy of the trace kernel: 3 waves per SIMD, i.e. at most 168 VGPRs (the grid entry on the pull
+// path would otherwise take the octree kernel to 175 and 2 waves; C3 1.91e8 -> 2.15e8 pkt/s at 3). The
+// Voronoi walk has its own kernel and attribute below.
 #define SKIRT_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(3)))
-#endif
 // the Voronoi trace kernel at 2 waves per SIMD: its branch-free bounds keep several entries in flight
 // and run without spills in 256 VGPRs (C4 5.72e7 pkt/s at 3 waves, 6.08e7 at 2)
-#ifndef SKIRT_VOR_TRACE_ATTR
 #define SKIRT_VOR_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(2)))
-#endif
 // the event kernel at 2 waves per SIMD: the Voronoi instantiation (cellIndex on the grid entry of every
 // queued ray) would otherwise take 256 VGPRs + AGPRs and run at 1
-#ifndef SKIRT_EVENT_ATTR
 #define SKIRT_EVENT_ATTR __attribute__((amdgpu_waves_per_eu(2)))
-#endif
 
 // ------------------------------------------------------------------ descriptors
 struct DevInstr {
@@ -157,10 +112,7 @@ constexpr bool kEnterInEvent = GRID == SKIRT_GRID_VORONOI;
 // Voronoi cellIndex: block-list candidates loaded per round trip. Round 3 chose 4; with the round-4
 // registers 2 lets the Voronoi event kernel run 3 waves/SIMD (165 VGPRs): event 2.59 -> 2.26 ms, C4
 // 1.0225e8 -> 1.0345e8 (8: 1.021e8), profiles/r04_cellindex_group.txt
-#ifndef SKIRT_CELLINDEX_GROUP
-#define SKIRT_CELLINDEX_GROUP 2
-#endif
-constexpr int kCellIndexGroup = SKIRT_CELLINDEX_GROUP;  // Voronoi cellIndex: block-list candidates per load round
+constexpr int kCellIndexGroup = 2;  // Voronoi cellIndex: block-list candidates per load round
 constexpr int kNoCell = -2;  // a cached cell index not known yet (-1 is a located point without a cell)
 // a ray entered by the event kernel carries the number of its segments before the grid in the top bits
 // of its first cell (Voronoi device cells < 2^28)
@@ -231,58 +183,19 @@ __device__ __forceinline__ void vorEntries(const VorEntry* B, int q0, VorEntry (
         e[2 * p + 1] = VorEntry{x.y, x.w, __int_as_float(y.y), y.w};
     }
 }
-#ifndef SKIRT_VOR_UNROLL
-#define SKIRT_VOR_UNROLL 4  // entries per load group, even (pairs), two groups in flight; with exp(-tau) per FILL segment 4 is best (C4 7.30e7; 6: 7.26e7 with 28 B/lane spilled; one group of 8: 7.25e7), without it 6 was (profiles/r03_vor_pipe.txt, r03_exact_attenuation.txt)
-#endif
-constexpr int kVorUnroll = SKIRT_VOR_UNROLL;
-#ifndef SKIRT_LABS_SMOOTH
-#define SKIRT_LABS_SMOOTH 1  // Labs adds leave one wave instruction per grid step (Tracer::drainStep)
-#endif
-constexpr bool kLabsSmooth = SKIRT_LABS_SMOOTH;
-#ifndef SKIRT_EXACT_ATTENUATION
-#define SKIRT_EXACT_ATTENUATION 1  // exp(-tau) per FILL segment, as the reference (0: the running product)
-#endif
-#ifndef SKIRT_VOR_PIPE
-#define SKIRT_VOR_PIPE 1  // groups of entries in flight per step (see Grid<SKIRT_GRID_VORONOI>::step)
-#endif
-#ifndef SKIRT_VOR_PAD_NAN
-#define SKIRT_VOR_PAD_NAN 1  // each cell's entries padded to whole groups with NaN entries (no per-entry count check)
-#endif
-constexpr bool kVorPadNaN = SKIRT_VOR_PAD_NAN && SKIRT_VOR_PIPE;
-#ifndef SKIRT_VOR_GROUPS
-// how many (SKIRT_VOR_PIPE): loaded with the header, each reloaded once consumed. 3: C4 trace launch
-// 23.64 -> 23.19 ms, 9.64e7 -> 9.89e7 pkt/s (4 then the same as 3), profiles/r04_ktrace_groups_nolicm.txt;
-// 4 with the NaN-padded groups: 1.0155e8 -> 1.0243e8 (profiles/r04_vor_groups4.txt)
-#define SKIRT_VOR_GROUPS 4
-#endif
-constexpr int kVorGroups = SKIRT_VOR_PIPE ? SKIRT_VOR_GROUPS : 1;
-#ifndef SKIRT_VOR_FALLBACK_GROUP
-#define SKIRT_VOR_FALLBACK_GROUP 2  // neighbour sites loaded together by the exact re-evaluation (<= kVorUnroll)
-#endif
+// Voronoi walk: entries per load group, even (pairs); with exp(-tau) per FILL segment 4 is best (C4 7.30e7;
+// 6: 7.26e7 with 28 B/lane spilled; one group of 8: 7.25e7; profiles/r03_vor_pipe.txt, r03_exact_attenuation.txt)
+constexpr int kVorUnroll = 4;
+// groups of entries in flight per step: loaded with the header, each reloaded once consumed. 3: C4 trace
+// launch 23.64 -> 23.19 ms, 9.64e7 -> 9.89e7 pkt/s, profiles/r04_ktrace_groups_nolicm.txt; 4 with each
+// cell's list padded to whole groups with NaN entries (no per-entry count check): 1.0155e8 -> 1.0243e8
+// (profiles/r04_vor_groups4.txt). Measured and removed (git history): the neighbour-parallel drain step
+// (profiles/r03_vor_wide.txt), the drain split around the step's loads (profiles/r04_c4_variants.txt).
+constexpr int kVorGroups = 4;
+constexpr int kVorFallbackGroup = 2;  // neighbour sites loaded together by the exact re-evaluation (<= kVorUnroll)
 constexpr int kVorCand = 4;  // possible winners the exact re-evaluation collects before it takes the whole list
-#ifndef SKIRT_VOR_WIDE
-// live rays at most for the neighbour-parallel drain step; 0 (off) is the default, as measured on C4:
-// lane-serial 6.69e7 pkt/s against 6.63e7 (16), 6.64e7 (8), 6.62e7 (4) (profiles/r03_vor_wide.txt)
-#define SKIRT_VOR_WIDE 0
-#endif
-constexpr int kVorWideMax = SKIRT_VOR_WIDE;
-// the trace kernel's Labs drain as unconditional buffer atomics (see bufferAtomicAddF64)
-#ifndef SKIRT_LABS_BUFFER_ATOMICS
-#define SKIRT_LABS_BUFFER_ATOMICS 1
-#endif
-// Voronoi walk: the Labs drain as two unconditional instructions per step, issued between the step's loads
-// and their use (Tracer::drainStep2, Grid<SKIRT_GRID_VORONOI>::stepLoad/stepRest), instead of the drain
-// every grid kind runs (kLabsSmooth: one instruction per step). With two entry groups in flight and the
-// branchy drain this took C4 from 9.53e7 to 9.63e7 pkt/s; with three groups, buffer atomics and no machine
-// LICM it is 1.8 % slower (trace launch 23.21 against 22.80 ms, profiles/r04_c4_variants.txt): off
-#ifndef SKIRT_VOR_SPLIT_DRAIN
-#define SKIRT_VOR_SPLIT_DRAIN 0
-#endif
-constexpr bool kVorSplitDrain = SKIRT_VOR_SPLIT_DRAIN && SKIRT_LABS_BUFFER_ATOMICS && kVorWideMax == 0;
-// slots after the last cell's block: a step loads whole groups of entries (kVorUnroll lane-serial, 16
-// for the first round of a neighbour-parallel step)
-constexpr int kVorPadGroups = kVorGroups + 2 > 4 ? kVorGroups + 2 : 4;
-constexpr int kVorPad = kVorPadGroups * kVorUnroll > 16 ? kVorPadGroups * kVorUnroll : 16;  // a step loads whole groups past its list
+// slots after the last cell's block: a step loads whole groups of entries past its list
+constexpr int kVorPad = (kVorGroups + 2) * kVorUnroll;
 
 // grid kinds of the kernels: SKIRT_GRID_CARTESIAN, SKIRT_GRID_OCTREE (leaf-map walk), the k-d tree
 // through its leaf map, and any tree walked through the node arrays (trees deeper than the leaf maps
@@ -358,6 +271,7 @@ struct Args {
     // tallies
     double* labs;                // [nlambda][labsStride], device cell order
     unsigned labsBytes;          // its size (< 4 GiB: the trace kernel addresses it through a buffer descriptor)
+    int labsGlobal;              // 1: a table of 4 GiB or more, added to with global atomics (no descriptor)
     double* tally;
     unsigned int* error;
     unsigned long long* stats;   // packets, seg_fill, seg_walk, seg_peel, detects, absorbs, lane slots
@@ -373,21 +287,6 @@ struct Args {
     uint32_t *splo, *sphi, *sblock, *sw2, *sw3, *shave;
     double *resA, *resB;         // per slot: FILL -> tau, Lsca | WALK -> distance
     RayRec* rays;
-    // the FILL rays of an iteration, in a queue of their own (at most one per slot): ctr[10 + q] of them.
-    // With sortFill they are traced in the order of a sort key (fillSortKey: wavelength, direction bin, region
-    // of the start point) through fillPerm, so that the rays a workgroup traces together cross the same
-    // cells and their Labs adds merge in its LDS cache (traceBodyCached)
-    RayRec* fillRays;
-    unsigned* fillKey;           // [nslots] sort keys (sortFill)
-    unsigned* fillRank;          // [nslots] rank among the rays of the same key (sortFill)
-    unsigned* fillPerm;          // [nslots] FILL rays in key order (sortFill), null: queue order
-    unsigned* sortHist;          // [kSortBuckets] counts, then first positions, per key
-    unsigned* sortBlockSums;     // [kSortBuckets / kScanChunk] (the scan's partial sums)
-    int sortFill;
-    int cacheDebug;              // tests of the cached walk (SKIRT_AMD_CACHE_DEBUG): 1 every add straight to Labs,
-                                 // 2 FILL rays unsorted, 4 (timing only) no Labs adds at all
-    int cacheSets;               // the cached trace kernel's LDS line cache: sets of kCacheWays lines
-    int ldsCacheOff;             // its byte offset in the dynamic LDS
     DetRec* det;                 // detection records of the peel-off rays
     int* act[2];                 // active slot lists (double buffered)
     unsigned long long* claim;   // next packet index (relative to first)
@@ -401,22 +300,7 @@ struct Args {
     int* pathCnt;
     int ldsMeshOff, ldsOptOff, ldsInstrOff, ldsSedOff;  // in doubles
     int detCopies;  // detect kernel: LDS copies of the SED sums (8, 4, 2, 1), 0 = SEDs straight to the tally
-#ifdef SKIRT_EXPERIMENT_TIMELINE
-    // tuning experiment only: per wave {start, queue found exhausted, end, rays} in 100 MHz ticks, per
-    // kernel kind (0 trace, 1 event, 2 detect) and iteration (< kTlLaunches)
-    unsigned long long* tl;
-    int tlLaunch;
-#endif
 };
-#ifdef SKIRT_EXPERIMENT_TIMELINE
-constexpr int kTlLaunches = 64, kTlWaves = 4096, kTlWords = 8;
-__device__ __forceinline__ unsigned long long* tlSlot(const Args& a, int kind) {
-    if (!a.tl || a.tlLaunch >= kTlLaunches) return nullptr;
-    const int wave = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
-    if (wave >= kTlWaves) return nullptr;
-    return a.tl + (((size_t)kind * kTlLaunches + a.tlLaunch) * kTlWaves + wave) * kTlWords;
-}
-#endif
 
 // One finest-level cell of the octree leaf map: the leaf node that covers it, that leaf's dust cell
 // number and level, and the leaf's density of dust component 0 (the one-component kernels need no
@@ -455,13 +339,8 @@ __host__ __device__ __forceinline__ unsigned morton3(unsigned x, unsigned y, uns
 // (SKIRT_LEAF_MORTON: full Morton order.)
 __host__ __device__ __forceinline__ unsigned leafBricks(int N) { return (unsigned)((N + 1) >> 1); }
 __host__ __device__ __forceinline__ unsigned leafIndex(int N, unsigned x, unsigned y, unsigned z) {
-#ifdef SKIRT_LEAF_MORTON
-    (void)N;
-    return morton3(x, y, z);
-#else
     const unsigned nb = leafBricks(N);
     return ((((x >> 1) * nb + (y >> 1)) * nb + (z >> 1)) << 3) | ((x & 1u) << 2) | ((y & 1u) << 1) | (z & 1u);
-#endif
 }
 __host__ __device__ __forceinline__ unsigned long long leafMapSize(int N) {
     const unsigned long long nb = leafBricks(N);
@@ -579,6 +458,7 @@ struct Ray {
     int pfx, pfy, pfz;     //   and the finest-level cell it was requested for (SKIRT_LEAF_PREFETCH)
     int idx, ell;
     unsigned flags, mode;
+    unsigned id;           // queue index of the ray (a PEEL ray writes its optical depth back there)
 };
 
 // ------------------------------------------------------------------ grids
@@ -1076,7 +956,6 @@ struct LeafMapGrid {
     // requests the leaf-map entry of the estimated finest cell of the next exit point (SKIRT_LEAF_PREFETCH):
     // issued at the end of a step, it is in flight during the wave's Labs drain and the next step's segment
     __device__ static __forceinline__ void prefetch(const Args& a, Ray& r) {
-#if SKIRT_LEAF_PREFETCH && SKIRT_LEAF_CHECK_FACES
         double ds, x, y, z;
         int wall;
         exitPoint(a, r, ds, wall, x, y, z);
@@ -1085,9 +964,6 @@ struct LeafMapGrid {
         r.pfy = estimate(N, a.mapY0, a.mapInvY, y);
         r.pfz = estimate(N, a.mapZ0, a.mapInvZ, z);
         r.pre = *reinterpret_cast<const int4*>(a.leafMap + leafIndex(N, r.pfx, r.pfy, r.pfz));
-#else
-        (void)a; (void)r;
-#endif
     }
 
     template <class SegFn>
@@ -1101,24 +977,12 @@ struct LeafMapGrid {
         exitPoint(a, r, ds, wall, x, y, z);
         // the next leaf's entry is requested first; the segment's own work (optical depth, absorption)
         // runs while the load is in flight
-#if SKIRT_LEAF_CHECK_FACES
         // the entry of the estimated finest cell; its leaf is the right one when the leaf's own faces
         // (read anyway) contain the point, since T is monotone: then the exact finest cell lies in it too
         const int N = a.mapN;
-#if SKIRT_LEAF_PREFETCH
         // requested by the previous step (prefetch), for the same exit point computed the same way
         int fx = r.pfx, fy = r.pfy, fz = r.pfz;
         const int4 raw = r.pre;
-#else
-        int fx = estimate(N, a.mapX0, a.mapInvX, x);
-        int fy = estimate(N, a.mapY0, a.mapInvY, y);
-        int fz = estimate(N, a.mapZ0, a.mapInvZ, z);
-        const int4 raw = *reinterpret_cast<const int4*>(a.leafMap + leafIndex(N, fx, fy, fz));
-#endif
-#else
-        int fx, fy, fz;
-        const int4 raw = fetch(a, sh, x, y, z, fx, fy, fz);
-#endif
         if (!seg(r.cj, r.rho0, ds)) return false;
         if (!inside(a, x, y, z)) return false;  // no neighbour and no root descent contains it
         LeafEntry e = decode(raw);
@@ -1129,7 +993,6 @@ struct LeafMapGrid {
         // lies on a face, the ones ahead of the ray are the next step's exit planes
         double lox = tx[jx], loy = ty[jy], loz = tz[jz];
         double hix = tx[jx + (1 << lx)], hiy = ty[jy + (1 << ly)], hiz = tz[jz + (1 << lz)];
-#if SKIRT_LEAF_CHECK_FACES
         if (!(x >= lox && x < hix && y >= loy && y < hiy && z >= loz && z < hiz)) {
             // the estimate fell into a neighbouring leaf (or the point is on the grid's far faces): the
             // exact finest cell, its entry and its leaf's faces
@@ -1142,7 +1005,6 @@ struct LeafMapGrid {
             lox = tx[jx]; loy = ty[jy]; loz = tz[jz];
             hix = tx[jx + (1 << lx)]; hiy = ty[jy + (1 << ly)]; hiz = tz[jz + (1 << lz)];
         }
-#endif
         r.x = x; r.y = y; r.z = z;
         if (e.node == r.ci || x == lox || y == loy || z == loz) {
             // on a face, or not out of the current leaf: the reference's own search decides
@@ -1335,17 +1197,10 @@ struct Grid<SKIRT_GRID_VORONOI> {
         b.L1 = fminf(b.L1, lo);
     }
 
-    // The start of a step: the cell's header (with the first entries, loaded by the caller in the same
-    // round), the pending segment (r.ck = 1: the previous cell's segment, cell r.ci, density r.rho0, site
-    // r.bx0..bz0, ends on the bisector plane with this cell, whose exact site arrives with this load),
-    // and the bounds' operands. False: the ray ended.
-    template <class SegFn>
-    __device__ static __forceinline__ bool head(const Args& a, Ray& r, StepIn& s, SegFn seg) {
-        const double2 h0 = *reinterpret_cast<const double2*>(s.B);
-        const double2 h1 = *reinterpret_cast<const double2*>(s.B + 1);
-        const int4 h2 = *reinterpret_cast<const int4*>(s.B + 2);
-        return headFrom(a, r, s, h0, h1, h2, seg);
-    }
+    // The start of a step: the cell's header h0..h2 (loaded with the first entries in the same round), the
+    // pending segment (r.ck = 1: the previous cell's segment, cell r.ci, density r.rho0, site r.bx0..bz0,
+    // ends on the bisector plane with this cell, whose exact site arrives with this load), and the bounds'
+    // operands. False: the ray ended.
     template <class SegFn>
     __device__ static __forceinline__ bool headFrom(const Args& a, Ray& r, StepIn& s, const double2& h0, const double2& h1,
                                                     const int4& h2, SegFn seg) {
@@ -1424,7 +1279,7 @@ struct Grid<SKIRT_GRID_VORONOI> {
                 for (int u = 0; u < kVorCand; u++)
                     if (u < nc) consider(cs[u], pix[u], piy[u], piz[u]);
             } else {
-                constexpr int G = SKIRT_VOR_FALLBACK_GROUP;
+                constexpr int G = kVorFallbackGroup;
                 for (int q0 = 0; q0 < cnt; q0 += G) {
                     int nxt[G];
                     double pix[G], piy[G], piz[G];
@@ -1490,7 +1345,6 @@ struct Grid<SKIRT_GRID_VORONOI> {
         StepIn s;
         s.B = a.vorSlots + r.cj;
         Best b{FLT_MAX, FLT_MAX, FLT_MAX, 0};
-#if SKIRT_VOR_PIPE
         // kVorGroups groups of entries in flight: they load with the header, and each group's next load is
         // issued as soon as the group is consumed, so a cell with more than kVorUnroll neighbours does not
         // wait for a second round trip
@@ -1508,88 +1362,13 @@ struct Grid<SKIRT_GRID_VORONOI> {
                 for (int u = 0; u < kVorUnroll; u++) {
                     float lo, uc;
                     // (a cell's list is padded to whole groups with NaN entries: no count check per entry)
-                    bounds(s, L.g[gi][u], kVorPadNaN || qb + u < s.cnt, lo, uc);
+                    bounds(s, L.g[gi][u], true, lo, uc);
                     take(b, lo, uc, L.g[gi][u].next);
                 }
                 if (qb + NG * kVorUnroll < s.cnt) vorEntries(s.B, qb + NG * kVorUnroll, L.g[gi]);
             }
         }
-#else
-        VorEntry (&e)[kVorUnroll] = L.g[0];
-        if (!headFrom(a, r, s, L.h0, L.h1, L.h2, seg)) return false;
-        for (int q0 = 0; q0 < s.cnt; q0 += kVorUnroll) {
-            if (q0) vorEntries(s.B, q0, e);
-#pragma unroll
-            for (int u = 0; u < kVorUnroll; u++) {
-                float lo, uc;
-                bounds(s, e[u], q0 + u < s.cnt, lo, uc);
-                take(b, lo, uc, e[u].next);
-            }
-        }
-#endif
         return decide(a, r, s, b, seg);
-    }
-
-    // The same step, neighbour-parallel, for a wave with at most kVorWideMax live rays (the drain of a
-    // launch, after the queue ran out; called by every lane of the wave, live = the lanes with a ray).
-    // The wave's groups of G lanes each take one live ray: a lane bounds the entries j, j + G, ... of that
-    // ray's cell and the group reduces the bounds (U, L1, L2 are order-free; w1 is used only when L1 is
-    // unique), so the ray's lane decides exactly as step() does. A lane-serial step runs its entries in
-    // rounds of kVorUnroll loads, each a round trip, which the drain waits on with few rays in flight.
-    template <class SegFn>
-    __device__ static __forceinline__ bool stepWide(const Args& a, Ray& r, unsigned long long live, SegFn seg) {
-        const int lane = threadIdx.x & 63;
-        const bool mine = (live >> lane) & 1ull;
-        const int k = __popcll(live);
-        const int lg = k <= 4 ? 4 : k <= 8 ? 3 : 2;  // log2 of the lanes per ray
-        const int G = 1 << lg;
-        const int g = lane >> lg, j = lane & (G - 1);
-        const bool grp = g < k;
-        int owner = 0;  // the lane of the g-th live ray
-        {
-            unsigned long long m = live;
-#pragma unroll
-            for (int t = 0; t < kVorWideMax; t++) {
-                owner = t == g ? __ffsll((long long)m) - 1 : owner;
-                m &= m - 1ull;
-            }
-        }
-        const int cj = __shfl(r.cj, owner);
-        const VorEntry* Bg = a.vorSlots + cj;
-        VorEntry e{0.f, 0.f, 0.f, -1};
-        if (grp) e = vorEntry(Bg, j);  // with the header, one round (the array is padded by kVorPad slots)
-        StepIn s{};
-        s.B = a.vorSlots + r.cj;
-        bool alive = false;
-        if (mine) alive = head(a, r, s, seg);
-        if (!alive) s.cnt = 0;  // the group of a ray that ended evaluates nothing (a count, not a shuffled bool:
-                                // the lane mask of a divergently assigned bool lost its upper 32 lanes there)
-        StepIn sg{};
-        sg.Dx = __shfl(s.Dx, owner); sg.Dy = __shfl(s.Dy, owner); sg.Dz = __shfl(s.Dz, owner);
-        sg.fkx = __shfl(s.fkx, owner); sg.fky = __shfl(s.fky, owner); sg.fkz = __shfl(s.fkz, owner);
-        sg.eA = __shfl(s.eA, owner); sg.eA2 = __shfl(s.eA2, owner); sg.eB2 = __shfl(s.eB2, owner);
-        const int cnt = __shfl(s.cnt, owner);
-        const bool act = grp && cnt > 0;
-        Best b{FLT_MAX, FLT_MAX, FLT_MAX, 0};
-        for (int q0 = 0; __ballot(act && q0 < cnt); q0 += G) {
-            const bool valid = act && q0 + j < cnt;
-            if (q0 && valid) e = vorEntry(Bg, q0 + j);
-            float lo, uc;
-            bounds(sg, e, valid, lo, uc);
-            take(b, lo, uc, e.next);
-        }
-        for (int o = 1; o < G; o <<= 1) {
-            const float U2 = __shfl_xor(b.U, o), L12 = __shfl_xor(b.L1, o), L22 = __shfl_xor(b.L2, o);
-            const int w2 = __shfl_xor(b.w1, o);
-            b.U = fminf(b.U, U2);
-            b.w1 = L12 < b.L1 ? w2 : b.w1;
-            b.L2 = fminf(fmaxf(b.L1, L12), fminf(b.L2, L22));  // the second least of the two pairs
-            b.L1 = fminf(b.L1, L12);
-        }
-        const int src = (mine ? __popcll(live & ((1ull << lane) - 1ull)) : 0) << lg;  // a lane of the ray's group
-        const Best mb{__shfl(b.U, src), __shfl(b.L1, src), __shfl(b.L2, src), __shfl(b.w1, src)};
-        if (!alive) return false;
-        return decide(a, r, s, mb, seg);
     }
 
     __device__ static __forceinline__ int whichcell(const Args& a, const Shared&, double x, double y, double z) {
@@ -1618,47 +1397,7 @@ struct Grid<SKIRT_GRID_VORONOI> {
 };
 
 // ================================================================== trace kernel
-// The iteration's rays in pull order. Without sortFill every ray is in the queue: ctr[q] from its bottom
-// (event order: a packet's FILL or WALK ray beside its peel-offs), then the WALK rays ctr[8 + q] queued from
-// its top (Args::walkBack). With sortFill the FILL rays have a queue of their own, traced in key order, and
-// are spread evenly among the others: pull index v is a FILL ray when floor((v + 1) nfill / n) >
-// floor(v nfill / n), so that waves keep both kinds in flight, the absorbing FILL paths and the atomic-free
-// peel-off paths, at the same mix throughout the launch (round 2: the two kinds pulled one after the other
-// are 15 % slower on C3; alternating them 1:1 until the shorter kind runs out, 7 %).
-struct PullMap {
-    unsigned nfill, nfront, nback;
-    unsigned long long n;
-    double inv;  // 1 / n
-    __device__ __forceinline__ void init(const Args& a) {
-        nfill = a.ctr[kCtrFill + a.parity];
-        nfront = a.ctr[a.parity];
-        nback = a.ctr[8 + a.parity];
-        n = (unsigned long long)nfill + nfront + nback;
-        inv = n ? 1.0 / (double)n : 0.0;
-    }
-    // floor(v nfill / n): the quotient in double (v nfill < 2^53 is exact), corrected to the integer one
-    __device__ __forceinline__ unsigned fillsBefore(unsigned v) const {
-        const unsigned long long num = (unsigned long long)v * nfill;
-        unsigned q = (unsigned)((double)num * inv);
-        if ((unsigned long long)q * n > num) q--;
-        else if ((unsigned long long)(q + 1u) * n <= num) q++;
-        return q;
-    }
-    __device__ __forceinline__ const RayRec* rec(const Args& a, unsigned v) const {
-        unsigned k = v;  // index within its kind
-        if (nfill) {
-            const unsigned q = fillsBefore(v);
-            if ((unsigned long long)(v + 1u) * nfill >= (unsigned long long)(q + 1u) * n)
-                return a.fillRays + (a.fillPerm ? a.fillPerm[q] : q);
-            k = v - q;
-        }
-        return a.rays + (k < nfront ? k : (unsigned)a.rayCap - 1u - (k - nfront));
-    }
-};
-
-// CACHED: the Labs add of a step waits in registers (addIdx, addVal) for the workgroup's LDS line cache
-// (LabsCache, traceBodyCached) instead of the lane's LDS buffer
-template <int GRID, bool ONECOMP, bool CONT, bool CACHED = false>
+template <int GRID, bool ONECOMP, bool CONT>
 struct Tracer {
     const Args& a;
     const Shared& sh;
@@ -1677,15 +1416,9 @@ struct Tracer {
     // atomic round trip per burst instead of one per step.
     double* pendVal;    // LDS, [kLabsBuf][kBlock]
     unsigned* pendIdx;  // LDS, [kLabsBuf][kBlock]
-#if SKIRT_LABS_BUFFER_ATOMICS
-    __amdgpu_buffer_rsrc_t labsRsrc;  // the Labs table as a raw buffer of labsBytes (SKIRT_LABS_BUFFER_ATOMICS)
-#endif
+    __amdgpu_buffer_rsrc_t labsRsrc;  // the Labs table as a raw buffer of labsBytes (unless Args::labsGlobal)
     int npend = 0;
     unsigned gstep = 0;  // grid steps of the wave (drainStep's round robin)
-    // CACHED: this step's Labs add (a step adds at most one segment: kSegsPerStep == 1)
-    unsigned addIdx = 0;
-    double addVal = 0.0;
-    bool hasAdd = false;
 
     __device__ __forceinline__ void drain() {
         static_assert(kLabsBuf >= 2 && kLabsBuf <= 64 && (kLabsBuf & (kLabsBuf - 1)) == 0, "kLabsBuf: power of 2");
@@ -1693,41 +1426,6 @@ struct Tracer {
         const int lane = threadIdx.x & 63;
         const int wbase = threadIdx.x - lane;
         const int j = lane & (kLabsBuf - 1);
-#ifdef SKIRT_EXPERIMENT_LINE_COUNT
-        // tuning experiment only (the counts replace the request and lane-slot statistics): the distinct
-        // 64-byte lines and distinct addresses among the wave's buffered adds, i.e. what a perfect
-        // per-wave merge of the buffer would issue
-        {
-            unsigned mine[kLabsBuf];
-            bool dupLine[kLabsBuf], dupAddr[kLabsBuf];
-#pragma unroll
-            for (int i = 0; i < kLabsBuf; i++) {
-                mine[i] = pendIdx[i * kBlock + threadIdx.x];
-                dupLine[i] = dupAddr[i] = false;
-            }
-            for (int l2 = 0; l2 < 64; l2++) {
-                const int n2 = __shfl(npend, l2);
-                for (int s2 = 0; s2 < n2; s2++) {
-                    const unsigned o = pendIdx[s2 * kBlock + wbase + l2];
-#pragma unroll
-                    for (int i = 0; i < kLabsBuf; i++) {
-                        const bool earlier = l2 < lane || (l2 == lane && s2 < i);
-                        if (earlier && (o >> 3) == (mine[i] >> 3)) dupLine[i] = true;
-                        if (earlier && o == mine[i]) dupAddr[i] = true;
-                    }
-                }
-            }
-            unsigned nl = 0, na = 0;
-#pragma unroll
-            for (int i = 0; i < kLabsBuf; i++) {
-                if (i < npend && !dupLine[i]) nl++;
-                if (i < npend && !dupAddr[i]) na++;
-            }
-            for (int off = 32; off > 0; off >>= 1) { nl += __shfl_xor(nl, off); na += __shfl_xor(na, off); }
-            requests += nl;
-            laneSlots += na;
-        }
-#endif
 #pragma unroll
         for (int i = 0; i < kLabsBuf; i++) issue(i);
         npend = 0;
@@ -1750,18 +1448,14 @@ struct Tracer {
         const unsigned prev = __shfl(line, lane - 1);
         const unsigned long long starts = __ballot(j < n && (j == 0 || prev != line));
         absorbs += (unsigned)__popcll(__ballot(j < n));
-#ifndef SKIRT_EXPERIMENT_LINE_COUNT
         requests += (unsigned)__popcll(starts);
-#endif
-#ifdef SKIRT_EXPERIMENT_NO_LABS_ATOMICS  // tuning experiment only: the cost of the Labs atomics
-        if (j < n && pendVal[q] == -1.0) atomicAddF64(a.labs + idx, pendVal[q]);
-#elif SKIRT_LABS_BUFFER_ATOMICS
-        // every lane issues; a lane without an add adds 0 at the first byte past the table (dropped)
-        const double v = j < n ? pendVal[q] : 0.0;
-        bufferAtomicAddF64(v, labsRsrc, (int)(j < n ? idx * 8u : a.labsBytes), 0, 0);
-#else
-        if (j < n) atomicAddF64(a.labs + idx, pendVal[q]);
-#endif
+        if (a.labsGlobal) {  // a table of 4 GiB or more (wave-uniform): global atomics
+            if (j < n) atomicAddF64(a.labs + idx, pendVal[q]);
+        } else {
+            // every lane issues; a lane without an add adds 0 at the first byte past the table (dropped)
+            const double v = j < n ? pendVal[q] : 0.0;
+            bufferAtomicAddF64(v, labsRsrc, (int)(j < n ? idx * 8u : a.labsBytes), 0, 0);
+        }
     }
 
     // One drain instruction per grid step, round robin over the lane groups: every lane's buffer is
@@ -1773,17 +1467,6 @@ struct Tracer {
         const int i = (int)(gstep++ & (kLabsBuf - 1));
         issue(i);
         if (((threadIdx.x & 63) / G) == i) npend = 0;
-    }
-
-    // Two drain instructions per grid step, for walks that add up to two segments per step (Voronoi): every
-    // lane's buffer is emptied every kLabsBuf / 2 steps, which holds its at most kLabsBuf adds.
-    __device__ __forceinline__ void drainStep2() {
-        constexpr int G = 64 / kLabsBuf;
-        const int i = (int)((gstep++ & (kLabsBuf / 2 - 1)) * 2);
-        issue(i);
-        issue(i + 1);
-        const int grp = (threadIdx.x & 63) / G;
-        if (grp == i || grp == i + 1) npend = 0;
     }
 
     __device__ __forceinline__ double rho(int m, int h) const { return a.rho[(size_t)m * a.ncomp + h]; }
@@ -1820,13 +1503,7 @@ struct Tracer {
                 // optically thick segment: the deep-cell differences of the thick pan_oct_sa models. With
                 // the Labs adds leaving one instruction per step, exp fits the octree walk's registers.)
                 const double ef = -expm1(-dtau);
-#if SKIRT_EXACT_ATTENUATION
                 const double Lintm = r.param * exp(-taustart) * ef;
-#else
-                (void)taustart;
-                const double Lintm = r.param * r.f1 * ef;
-                r.f1 = r.f1 * (1.0 - ef);
-#endif
                 double albedo;
                 if (ONECOMP) albedo = sh.alb[r.ell];
                 else {
@@ -1839,15 +1516,9 @@ struct Tracer {
                     r.f2 += albedo * Lintm;
                 }
                 if (a.store) {
-                    if constexpr (CACHED) {
-                        addVal = (1.0 - albedo) * Lintm;
-                        addIdx = (unsigned)r.ell * (unsigned)a.labsStride + (unsigned)m;
-                        hasAdd = true;
-                    } else {
-                        pendVal[npend * kBlock + threadIdx.x] = (1.0 - albedo) * Lintm;
-                        pendIdx[npend * kBlock + threadIdx.x] = (unsigned)r.ell * (unsigned)a.labsStride + (unsigned)m;
-                        npend++;
-                    }
+                    pendVal[npend * kBlock + threadIdx.x] = (1.0 - albedo) * Lintm;
+                    pendIdx[npend * kBlock + threadIdx.x] = (unsigned)r.ell * (unsigned)a.labsStride + (unsigned)m;
+                    npend++;
                 }
             }
         } else if (r.mode == RAY_WALK) {
@@ -1858,12 +1529,13 @@ struct Tracer {
         return true;
     }
 
-    // load a queued ray and enter the grid: the part of the path before the grid (segments outside
+    // load queued ray `id` and enter the grid: the part of the path before the grid (segments outside
     // it, m = -1) and the first cell (DustGrid::path); an empty path finishes the ray at once
-    __device__ __forceinline__ void load(Ray& r, const RayRec* rec) {
-        const double2* c = reinterpret_cast<const double2*>(rec);
+    __device__ __forceinline__ void load(Ray& r, unsigned id) {
+        const double2* c = reinterpret_cast<const double2*>(a.rays + id);
         const double2 c0 = c[0], c1 = c[1], c2 = c[2], c3 = c[3];
         const int4 c6 = reinterpret_cast<const int4*>(c)[4];
+        r.id = id;
         r.x = c0.x; r.y = c0.y; r.z = c1.x;
         r.dx = c1.y; r.dy = c2.x; r.dz = c2.y;
         // 1/direction, 0 where |k| <= 1e-15 (that axis is never crossed), as the event kernel computed it
@@ -2199,13 +1871,6 @@ __global__ void __launch_bounds__(kBlock) buildLeafMapKernel(LeafEntry* map, con
     for (unsigned long long q = blockIdx.x * (unsigned long long)blockDim.x + threadIdx.x; q < n;
          q += (unsigned long long)gridDim.x * blockDim.x) {
         unsigned fx = 0, fy = 0, fz = 0;
-#ifdef SKIRT_LEAF_MORTON
-        for (int b = 0; b < L; b++) {  // inverse Morton
-            fx |= (unsigned)((q >> (3 * b)) & 1u) << b;
-            fy |= (unsigned)((q >> (3 * b + 1)) & 1u) << b;
-            fz |= (unsigned)((q >> (3 * b + 2)) & 1u) << b;
-        }
-#else
         {  // inverse of leafIndex
             const unsigned long long nb = leafBricks(N), br = q >> 3;
             fx = (unsigned)(2 * (br / (nb * nb)) + ((q >> 2) & 1u));
@@ -2213,7 +1878,6 @@ __global__ void __launch_bounds__(kBlock) buildLeafMapKernel(LeafEntry* map, con
             fz = (unsigned)(2 * (br % nb) + (q & 1u));
             fx = min(fx, (unsigned)N - 1u); fy = min(fy, (unsigned)N - 1u); fz = min(fz, (unsigned)N - 1u);
         }
-#endif
         int node = 0, level = 0;
         LeafEntry e;
         if (splitDir) {
@@ -2253,16 +1917,12 @@ __device__ __forceinline__ void traceBody(const Args& a) {
         a.ctr[5 + (1 - a.parity)] = 0;  // and its detection records (the last ones were detected already)
         a.ctr[2 + a.parity] = 0;  // active list just consumed by the event kernel
         a.ctr[8 + (1 - a.parity)] = 0;  // the next iteration's WALK rays
-        a.ctr[kCtrFill + (1 - a.parity)] = 0;  // and FILL rays
     }
-    // the iteration's rays (PullMap): the FILL rays among ctr[q] from the bottom of the queue, then the WALK
-    // rays ctr[8 + q] from its top (Args::walkBack), pulled last: the short WALK paths fill the lanes that the
-    // long FILL and peel-off paths free at the end of a launch, instead of idling until the launch's longest
-    // path ends
-    PullMap pm;
-    pm.init(a);
-    const unsigned int nfront = pm.nfront;
-    if (pm.n == 0) return;  // an iteration after the end of the phase
+    // the iteration's rays: ctr[q] from the bottom of the queue, then the WALK rays ctr[8 + q] from its top
+    // (Args::walkBack), pulled last: the short WALK paths fill the lanes that the long FILL and peel-off
+    // paths free at the end of a launch, instead of idling until the launch's longest path ends
+    const unsigned int nfront = a.ctr[a.parity];
+    if (nfront + a.ctr[8 + a.parity] == 0) return;  // an iteration after the end of the phase
     // the front rays (growing up from 0) and the WALK rays (growing down from rayCap - 1) must not meet:
     // the event and continuous peel-off kernels reserved them independently, so this is the first point
     // where both totals are final; an overflow fails the phase instead of tracing overwritten records
@@ -2270,30 +1930,23 @@ __device__ __forceinline__ void traceBody(const Args& a) {
         if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(a.error, ERR_QUEUE);
         return;
     }
-#ifdef SKIRT_EXPERIMENT_TIMELINE
-    const unsigned long long tlStart = __builtin_amdgcn_s_memrealtime();
-    unsigned long long tlExhausted = 0, tlRays = 0;
-#endif
     Shared sh = stageTables(a, lds, gridParts<GRID>() | STAGE_OPTICS);
 
     Tracer<GRID, ONECOMP, CONT> T{a, sh};
-#if SKIRT_LABS_BUFFER_ATOMICS
     T.labsRsrc = __builtin_amdgcn_make_buffer_rsrc(a.labs, 0, (int)a.labsBytes, 0x00020000);
-#endif
     T.pendVal = lds + a.ldsInstrOff;  // after the grid and optics tables
     T.pendIdx = reinterpret_cast<unsigned*>(lds + a.ldsInstrOff + kLabsBuf * kBlock);
     T.waveSegs = T.pendIdx + kLabsBuf * kBlock;
     if (threadIdx.x < 3 * (kBlock / 64)) T.waveSegs[threadIdx.x] = 0;
     __syncthreads();
     const int lane = threadIdx.x & 63;
-    const unsigned int nrays = (unsigned)pm.n;
+    const unsigned int nrays = nfront + a.ctr[8 + a.parity];
     Ray r;
     r.mode = RAY_NONE;
     bool done = false;
-#if SKIRT_PULL_CHUNK
     // the wave reserves queue ids kPullChunk at a time and hands them to its idle lanes; the next
     // reservation is requested while the current one still lasts, so a pull rarely waits for the atomic
-    constexpr unsigned kPullChunk = SKIRT_PULL_CHUNK;
+    constexpr unsigned kPullChunk = 64;
     unsigned cur = 0, curEnd = 0, nxt = 0;
     bool haveNext = false;
     auto reserve = [&]() {
@@ -2301,7 +1954,6 @@ __device__ __forceinline__ void traceBody(const Args& a) {
         if (lane == 0) base = atomicAdd(a.ctr + 4, kPullChunk);
         return __shfl(base, 0);
     };
-#endif
     while (true) {
         const bool idle = (r.mode == RAY_NONE) && !done;
         const unsigned long long imask = __ballot(idle);
@@ -2309,7 +1961,6 @@ __device__ __forceinline__ void traceBody(const Args& a) {
         if (imask == 0 && amask == 0) break;
         if (imask != 0 && (amask == 0 || __popcll(imask) >= a.threshold)) {
             const unsigned int rank = (unsigned int)__popcll(imask & ((1ull << lane) - 1ull));
-#if SKIRT_PULL_CHUNK
             const unsigned int k = (unsigned int)__popcll(imask);
             const unsigned int avail = curEnd - cur;
             if (avail < k && !haveNext) { nxt = reserve(); haveNext = true; }
@@ -2317,63 +1968,24 @@ __device__ __forceinline__ void traceBody(const Args& a) {
             if (avail >= k) cur += k;
             else { cur = nxt + (k - avail); curEnd = nxt + kPullChunk; haveNext = false; }
             if (!haveNext && curEnd - cur < kPullChunk / 2 && cur < nrays) { nxt = reserve(); haveNext = true; }
-#else
-            // idle lanes pull consecutive rays from the queue with one atomic per wave
-            const int leader = __ffsll((long long)imask) - 1;
-            unsigned int base = 0;
-            if (lane == leader) base = atomicAdd(a.ctr + 4, (unsigned int)__popcll(imask));
-            base = __shfl(base, leader);
-            const unsigned int id = base + rank;
-#endif
             if (idle) {
                 if (id >= nrays) done = true;
-                else T.load(r, pm.rec(a, id));  // a RAY_NONE record (empty path) leaves the lane idle
+                else T.load(r, id < nfront ? id : (unsigned)a.rayCap - 1u - (id - nfront));  // a RAY_NONE record (empty path) leaves the lane idle
             }
-#ifdef SKIRT_EXPERIMENT_TIMELINE
-            tlRays += (unsigned long long)__popcll(__ballot(idle && id < nrays));
-            if (!tlExhausted && __ballot(idle && id >= nrays)) tlExhausted = __builtin_amdgcn_s_memrealtime();
-#endif
         }
-        // the queue ran out for this wave: the Voronoi step goes neighbour-parallel when few rays remain
-        const bool draining = GRID == SKIRT_GRID_VORONOI && kVorWideMax > 0 && __ballot(done) != 0;
 #pragma unroll 1
         for (int it = 0; it < kStepsPerPull; it++) {
             const unsigned long long live = __ballot(r.mode != RAY_NONE);
             if (live == 0) break;
-#ifndef SKIRT_EXPERIMENT_LINE_COUNT
             T.laneSlots += 64;
-#endif
             auto seg = [&](int m, double rho0, double ds) { return T.segment(r, m, rho0, ds); };
-            if constexpr (GRID == SKIRT_GRID_VORONOI && kVorWideMax > 0) {
-                if (draining && __popcll(live) <= kVorWideMax) {
-                    if (!Grid<GRID>::stepWide(a, r, live, seg) && r.mode != RAY_NONE) {
-                        T.finish(r);
-                        r.mode = RAY_NONE;
-                    }
-                    if (__ballot(T.npend > kLabsBuf - kSegsPerStep<GRID>)) T.drain();
-                    continue;
-                }
-            }
-            if constexpr (GRID == SKIRT_GRID_VORONOI && kVorSplitDrain) {
-                // the step's loads, then the wave's two drain instructions, then the rest of the step: the
-                // header's wait then covers the loads only (SKIRT_VOR_SPLIT_DRAIN)
-                typename Grid<GRID>::Load L;
-                const bool act = r.mode != RAY_NONE;
-                Grid<GRID>::stepLoad(a, r, L, act);
-                T.drainStep2();
-                if (act && !Grid<GRID>::stepRest(a, sh, r, L, seg)) {
-                    T.finish(r);
-                    r.mode = RAY_NONE;
-                }
-                continue;
-            }
             if (r.mode != RAY_NONE) {
                 if (!Grid<GRID>::step(a, sh, r, seg)) {
                     T.finish(r);
                     r.mode = RAY_NONE;
                 }
             }
-            if constexpr (kLabsSmooth && kSegsPerStep<GRID> == 1) {
+            if constexpr (kSegsPerStep<GRID> == 1) {
                 T.drainStep();  // one drain instruction per step
             } else {
                 // a buffer without room for another step's adds: issue the wave's adds
@@ -2382,12 +1994,6 @@ __device__ __forceinline__ void traceBody(const Args& a) {
         }
     }
     T.drain();
-#ifdef SKIRT_EXPERIMENT_TIMELINE
-    if (unsigned long long* t = tlSlot(a, 0)) {
-        const unsigned long long tEnd = __builtin_amdgcn_s_memrealtime();
-        if (lane == 0) { t[0] = tlStart; t[1] = tlExhausted; t[2] = tEnd; t[3] = tlRays; }
-    }
-#endif
     // (wave totals: lane 0 contributes them)
     const unsigned* ws = T.waveSegs + (threadIdx.x >> 6) * 3;
     const bool l0 = lane == 0;
@@ -2407,423 +2013,11 @@ __global__ void __launch_bounds__(kBlock) SKIRT_VOR_TRACE_ATTR traceKernelVor(co
     traceBody<SKIRT_GRID_VORONOI, ONECOMP, CONT>(a);
 }
 
-// ------------------------------------------------------------------ the cached trace kernel
-// Labs adds through an LDS line cache (Args::sortFill; DESIGN.md section 4, "C3: the Labs line cache").
-// f64 atomics execute memory-side at one chip-wide rate of 64-byte requests (2.36e10/s), and a ray's
-// consecutive adds share a line only 1.85 times on C3. With the FILL rays sorted (fillSortKey) and each
-// workgroup pulling consecutive rays of that order, the rays a workgroup traces together start close
-// together and head the same way, so the workgroup's adds fall into far fewer lines than its rays cross
-// alone (tools/labs_locality.cpp models 4.2-5.1 adds per line for C3 with 2048 cached lines). The cache
-// holds whole lines of one wavelength's Labs row, kCacheWays per set, shared by the workgroup's 12 waves:
-//  * a hit pins its line (+1 on the line's word), adds into LDS, unpins;
-//  * a miss takes a free way (compare-and-swap from the free tag), or evicts the set's round-robin victim:
-//    the evicting lane locks the victim (compare-and-swap of its word with no pins to "locked"), copies its
-//    8 sums to the wave's eviction buffer, zeroes them, writes its own add and retags the way in one atomic
-//    add that also unlocks it. A lane that finds its line locked, retagged, or cannot lock a victim adds
-//    straight to Labs. No lane ever waits for another, so no wave can block the workgroup.
-//  * once per grid step a wave issues its evicted lines (8 lanes per line: one 64-byte request each) and
-//    its direct adds as buffer atomics; after the last ray the workgroup adds the cached lines to Labs.
-// LDS operations of one wave execute in program order, and the compiler is kept from reordering them
-// (signal fences), which is all the protocol relies on.
-typedef __attribute__((address_space(3))) unsigned long long LdsU64;
-typedef __attribute__((address_space(3))) double LdsF64;
-typedef __attribute__((address_space(3))) unsigned LdsU32;
-typedef unsigned long long VecU64x2 __attribute__((ext_vector_type(2)));
-typedef double VecF64x2 __attribute__((ext_vector_type(2)));
-typedef __attribute__((address_space(3))) VecU64x2 LdsU64x2;
-typedef __attribute__((address_space(3))) VecF64x2 LdsF64x2;
-typedef unsigned VecU32x4 __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(3))) VecU32x4 LdsU32x4;
-constexpr unsigned kPoolChunk = 1536;  // pull indices a workgroup reserves at once (about half FILL rays)
-constexpr int kCacheWaves = kCacheBlock / 64;
-
-__device__ __forceinline__ unsigned long long ldsAdd64(LdsU64* p, unsigned long long v) {
-    return __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-__device__ __forceinline__ bool ldsCas64(LdsU64* p, unsigned long long& expect, unsigned long long want) {
-    return __hip_atomic_compare_exchange_strong(p, &expect, want, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-__device__ __forceinline__ void ldsAddF64(LdsF64* p, double v) {
-    (void)__hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-__device__ __forceinline__ unsigned ldsAdd32(LdsU32* p, unsigned v) {
-    return __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-__device__ __forceinline__ void ldsOrder() { __atomic_signal_fence(__ATOMIC_SEQ_CST); }
-
-struct LabsCache {
-    LdsU32* tag;               // [sets][kCacheWays]: the Labs line cached in the way (kCacheEmpty: free)
-    LdsU32* pin;               // [sets][kCacheWays]: lanes adding into the way; kPinLock: being evicted
-    LdsF64* data;              // [sets][kCacheWays][8]: the line's sums
-    LdsF64* evData;            // this wave's evicted lines [kEvictLines][8]
-    LdsU32* evTag;             // [kEvictLines]: their Labs lines
-    LdsU32* rr;                // [sets]: the next victim of each set
-    unsigned setShift;         // set of a line: (line * 2654435761) >> setShift
-    __amdgpu_buffer_rsrc_t rsrc;
-    unsigned oob;              // a byte offset past Labs: the buffer range check drops the lane
-    unsigned requests = 0;     // 64-byte atomic requests issued (wave-uniform)
-    bool debugDirect = false;  // Args::cacheDebug & 1
-
-    static constexpr unsigned kPinLock = 0x80000000u;
-
-    // add into way w if it holds `line`: pinned, the way cannot be evicted meanwhile (the tag is read after
-    // the pin; a tag only changes while its way is locked, which needs no pins)
-    __device__ __forceinline__ bool tryHit(unsigned w, unsigned line, unsigned e, double v) {
-        const unsigned old = ldsAdd32(pin + w, 1u);
-        ldsOrder();
-        const unsigned t = tag[w];
-        const bool ok = !(old & kPinLock) && t == line;
-        if (ok) ldsAddF64(data + w * 8 + e, v);
-        ldsOrder();
-        (void)ldsAdd32(pin + w, ~0u);  // unpin
-        return ok;
-    }
-    // take the free way w for `line` (its sums are zero), or add into it if another lane just took it for
-    // the same line
-    __device__ __forceinline__ bool tryInsert(unsigned w, unsigned line, unsigned e, double v) {
-        const unsigned old = ldsAdd32(pin + w, 1u);
-        ldsOrder();
-        unsigned expect = kCacheEmpty;
-        const bool took = __hip_atomic_compare_exchange_strong(tag + w, &expect, line, __ATOMIC_RELAXED,
-                                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        const bool ok = !(old & kPinLock) && (took || expect == line);
-        if (ok) ldsAddF64(data + w * 8 + e, v);
-        ldsOrder();
-        (void)ldsAdd32(pin + w, ~0u);
-        return ok;
-    }
-    // lock way w (no pins), hand its line to eviction slot `slot`, take the way for `line` with the add
-    __device__ __forceinline__ bool tryEvict(unsigned w, unsigned line, unsigned e, double v, unsigned slot) {
-        unsigned expect = 0u;
-        if (!__hip_atomic_compare_exchange_strong(pin + w, &expect, kPinLock, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                  __HIP_MEMORY_SCOPE_WORKGROUP))
-            return false;
-        ldsOrder();
-        const unsigned victim = tag[w];
-        LdsF64x2* d2 = reinterpret_cast<LdsF64x2*>(data + w * 8);
-        const VecF64x2 q0 = d2[0], q1 = d2[1], q2 = d2[2], q3 = d2[3];
-        LdsF64x2* o2 = reinterpret_cast<LdsF64x2*>(evData + slot * 8);
-        o2[0] = q0; o2[1] = q1; o2[2] = q2; o2[3] = q3;
-        evTag[slot] = victim;
-        const VecF64x2 z = {0.0, 0.0};
-        d2[0] = z; d2[1] = z; d2[2] = z; d2[3] = z;
-        data[w * 8 + e] = v;
-        tag[w] = line;
-        ldsOrder();
-        (void)ldsAdd32(pin + w, 0u - kPinLock);  // unlock (pins of lanes that found it locked stay counted)
-        return true;
-    }
-
-    // the step's adds of the wave (lanes with `has`): cached, or straight to Labs
-    __device__ __forceinline__ void addStep(bool has, unsigned idx, double v) {
-        const int lane = threadIdx.x & 63;
-        const unsigned line = idx >> 3, e = idx & 7u;
-        unsigned doff = oob;
-        double dval = 0.0;
-        bool evict = false;
-        unsigned w0 = 0, vway = 0;
-#ifdef SKIRT_EXP_NOCACHE
-        if (has) {
-#else
-        if (has && debugDirect) {
-#endif
-            doff = idx * 8u;
-            dval = v;
-        } else if (has) {
-            w0 = ((line * 2654435761u) >> setShift) * kCacheWays;
-            const LdsU32x4* tp = reinterpret_cast<const LdsU32x4*>(tag + w0);
-            const VecU32x4 t0 = tp[0], t1 = tp[1];
-            int hit = -1, freeWay = -1;
-#pragma unroll
-            for (int k = kCacheWays - 1; k >= 0; k--) {
-                const unsigned t = k < 4 ? t0[k & 3] : t1[k & 3];
-                if (t == line) hit = k;
-                if (t == kCacheEmpty) freeWay = k;
-            }
-            bool done = false;
-            if (hit >= 0) done = tryHit(w0 + (unsigned)hit, line, e, v);
-            else if (freeWay >= 0) done = tryInsert(w0 + (unsigned)freeWay, line, e, v);
-            else {
-                evict = true;
-                vway = ldsAdd32(rr + w0 / kCacheWays, 1u) & (kCacheWays - 1);  // round robin (FIFO)
-            }
-            if (!done && !evict) { doff = idx * 8u; dval = v; }
-        }
-        const unsigned long long em = __ballot(evict);
-        const unsigned slot = (unsigned)__popcll(em & ((1ull << lane) - 1ull));
-        if (evict) {
-            const bool ok = slot < (unsigned)kEvictLines && tryEvict(w0 + vway, line, e, v, slot);
-            if (!ok) {
-                if (slot < (unsigned)kEvictLines) evTag[slot] = kCacheEmpty;
-                doff = idx * 8u;
-                dval = v;
-            }
-        }
-        ldsOrder();
-        // The evicted lines (lane q adds entry q & 7 of line q >> 3) and the direct adds leave as two buffer
-        // atomics that every step issues, lanes without an add at an offset past Labs (dropped): a fixed
-        // count of vector-memory operations per step, so that the next step's leaf-map load is waited for
-        // alone, not with these atomics (s_waitcnt vmcnt counts them all; an atomic under a branch makes
-        // the compiler wait with vmcnt(0))
-        const unsigned nev = min((unsigned)__popcll(em), (unsigned)kEvictLines);
-        const unsigned j = (unsigned)lane >> 3, ee = (unsigned)lane & 7u;
-        const unsigned tg = j < nev ? evTag[j] : kCacheEmpty;
-        const double ev = evData[j * 8 + ee];
-        bufferAtomicAddF64(ev, rsrc, (int)((tg != kCacheEmpty && ev != 0.0) ? tg * 64u + ee * 8u : oob), 0, 0);
-        requests += (unsigned)__popcll(__ballot(ee == 0 && tg != kCacheEmpty));
-        ldsOrder();
-        bufferAtomicAddF64(dval, rsrc, (int)doff, 0, 0);
-        requests += (unsigned)__popcll(__ballot(doff != oob));
-    }
-
-    // after the workgroup's last ray: every cached line to Labs (8 lanes per line)
-    __device__ __forceinline__ void flushAll(unsigned nlines) {
-        const unsigned ee = threadIdx.x & 7u;
-        unsigned lines = 0;
-        for (unsigned L = threadIdx.x >> 3; L < nlines; L += blockDim.x >> 3) {
-            const unsigned tg = tag[L];
-            const double dv = data[L * 8 + ee];
-            bufferAtomicAddF64(dv, rsrc, (int)((tg != kCacheEmpty && dv != 0.0) ? tg * 64u + ee * 8u : oob), 0, 0);
-            if (ee == 0 && tg != kCacheEmpty) lines++;
-        }
-        requests = lines;  // (per lane: the lines this lane's group flushed)
-    }
-};
-
-template <int GRID, bool ONECOMP>
-__device__ __forceinline__ void traceBodyCached(const Args& a) {
-    extern __shared__ __attribute__((aligned(16))) double lds[];
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        // reset the counters the next event iteration appends to (nobody else uses them now)
-        a.ctr[1 - a.parity] = 0;
-        a.ctr[5 + (1 - a.parity)] = 0;
-        a.ctr[2 + a.parity] = 0;
-        a.ctr[8 + (1 - a.parity)] = 0;
-        a.ctr[kCtrFill + (1 - a.parity)] = 0;
-    }
-    PullMap pm;
-    pm.init(a);
-    if (pm.n == 0) return;  // an iteration after the end of the phase
-    if ((unsigned long long)pm.nfront + pm.nback > (unsigned long long)a.rayCap) {
-        if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(a.error, ERR_QUEUE);
-        return;
-    }
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    // LDS: tables | cache words | cache sums | eviction buffers | pull pool | round-robin counters | eviction
-    // tags | segment counts | pool-exhausted flag
-    typedef __attribute__((address_space(3))) char LdsByte;
-    LdsByte* cb = (LdsByte*)((char*)lds) + a.ldsCacheOff;  // (a C cast: the address-space cast)
-    const unsigned sets = (unsigned)a.cacheSets, nlines = sets * kCacheWays;
-    LabsCache C;
-    C.tag = reinterpret_cast<LdsU32*>(cb); cb += nlines * 4;
-    C.pin = reinterpret_cast<LdsU32*>(cb); cb += nlines * 4;
-    C.data = reinterpret_cast<LdsF64*>(cb); cb += nlines * 64;
-    LdsF64* evAll = reinterpret_cast<LdsF64*>(cb); cb += kCacheWaves * kEvictLines * 64;
-    LdsU64* pool = reinterpret_cast<LdsU64*>(cb); cb += 8;
-    C.rr = reinterpret_cast<LdsU32*>(cb); cb += sets * 4;
-    LdsU32* evTagAll = reinterpret_cast<LdsU32*>(cb); cb += kCacheWaves * kEvictLines * 4;
-    unsigned* waveSegs = (unsigned*)(LdsU32*)cb; cb += kCacheWaves * 3 * 4;
-    volatile LdsU32* poolDone = reinterpret_cast<volatile LdsU32*>(cb);
-    const int uwave = __builtin_amdgcn_readfirstlane(wave);
-    C.evData = evAll + uwave * kEvictLines * 8;
-    C.evTag = evTagAll + uwave * kEvictLines;
-    C.setShift = 32u - (unsigned)(31 - __builtin_clz(sets));
-    C.rsrc = __builtin_amdgcn_make_buffer_rsrc(a.labs, 0, (int)a.labsBytes, 0x00020000);
-    C.oob = a.labsBytes;
-    C.debugDirect = (a.cacheDebug & 1) != 0;
-    for (unsigned q = threadIdx.x; q < nlines; q += blockDim.x) { C.tag[q] = kCacheEmpty; C.pin[q] = 0u; }
-    for (unsigned q = threadIdx.x; q < nlines * 8; q += blockDim.x) C.data[q] = 0.0;
-    for (unsigned q = threadIdx.x; q < sets; q += blockDim.x) C.rr[q] = 0u;
-    if (threadIdx.x < 3 * kCacheWaves) waveSegs[threadIdx.x] = 0u;
-    if (threadIdx.x == 0) { *pool = 0ull; *poolDone = 0u; }
-    Shared sh = stageTables(a, lds, gridParts<GRID>() | STAGE_OPTICS);  // (ends with a barrier)
-
-    Tracer<GRID, ONECOMP, false, true> T{a, sh};
-    T.waveSegs = waveSegs;
-    const unsigned nvirt = (unsigned)pm.n;
-    Ray r;
-    r.mode = RAY_NONE;
-    bool done = false;
-    while (true) {
-        const bool idle = (r.mode == RAY_NONE) && !done;
-        const unsigned long long imask = __ballot(idle);
-        const unsigned long long amask = __ballot(r.mode != RAY_NONE);
-        if (imask == 0 && amask == 0) break;
-        if (imask != 0 && (amask == 0 || __popcll(imask) >= a.threshold)) {
-#ifdef SKIRT_EXP_WAVEPULL
-            {
-                const unsigned k = (unsigned)__popcll(imask);
-                const unsigned rank = (unsigned)__popcll(imask & ((1ull << lane) - 1ull));
-                unsigned base = 0;
-                if (lane == 0) base = atomicAdd(a.ctr + 4, k);
-                base = __shfl(base, 0);
-                if (idle) {
-                    if (base + rank < nvirt) T.load(r, pm.rec(a, base + rank));
-                    else done = true;
-                }
-            }
-#else
-            // the idle lanes pull consecutive indices from the workgroup's chunk (one LDS atomic per wave);
-            // the wave that crosses the chunk's end reserves the next chunk for the workgroup
-            const unsigned k = (unsigned)__popcll(imask);
-            const unsigned rank = (unsigned)__popcll(imask & ((1ull << lane) - 1ull));
-            unsigned long long old = 0;
-            if (lane == 0) old = ldsAdd64(pool, (unsigned long long)k);
-            old = __shfl(old, 0);
-            const unsigned nxt = (unsigned)old, end = (unsigned)(old >> 32);
-            // (signed 64-bit arithmetic: with unsigned 32-bit compares the device compiler dropped the nxt <=
-            // end test of the crossing condition -- an unconditional `sub nuw` from min(k, end - nxt) -- and
-            // every wave that found the chunk used up took a chunk of its own)
-            const long long avail = (long long)end - (long long)nxt;
-            const unsigned got = avail > 0 ? (unsigned)min((long long)k, avail) : 0u;
-            unsigned base2 = 0, got2 = 0;
-            if (avail >= 0 && avail < (long long)k) {
-                unsigned b = 0;
-                if (lane == 0) b = atomicAdd(a.ctr + 4, kPoolChunk);
-                b = __shfl(b, 0);
-                if (b >= nvirt) {
-                    if (lane == 0) {
-                        (void)__hip_atomic_exchange(pool, 0x80000000ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                        *poolDone = 1u;
-                    }
-                } else {
-                    const unsigned e2 = min(b + kPoolChunk, nvirt);
-                    got2 = min(k - got, e2 - b);
-                    base2 = b;
-                    if (lane == 0)
-                        (void)__hip_atomic_exchange(pool, ((unsigned long long)e2 << 32) | (b + got2),
-                                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                }
-            }
-            // (one call site of load: the grid entry is inlined once)
-            const bool have = rank < got + got2;
-            const unsigned id = rank < got ? nxt + rank : base2 + (rank - got);
-            if (idle) {
-                if (have) T.load(r, pm.rec(a, id));
-                else if (*poolDone) done = true;
-            }
-#endif
-        }
-#pragma unroll 1
-        for (int it = 0; it < kStepsPerPull; it++) {
-            const unsigned long long live = __ballot(r.mode != RAY_NONE);
-            if (live == 0) break;
-            T.laneSlots += 64;
-            if (r.mode != RAY_NONE) {
-                if (!Grid<GRID>::step(a, sh, r, [&](int m, double rho0, double ds) { return T.segment(r, m, rho0, ds); })) {
-                    T.finish(r);
-                    r.mode = RAY_NONE;
-                }
-            }
-            T.absorbs += (unsigned)__popcll(__ballot(T.hasAdd));
-            if (!(a.cacheDebug & 4)) C.addStep(T.hasAdd, T.addIdx, T.addVal);
-            T.hasAdd = false;
-        }
-    }
-    __syncthreads();  // every wave's rays are done: the cache holds the workgroup's remaining sums
-    const unsigned stepRequests = C.requests;
-    C.flushAll(nlines);
-    unsigned flushed = C.requests;
-    for (int off = 32; off > 0; off >>= 1) flushed += __shfl_xor(flushed, off);
-    const unsigned* ws = waveSegs + wave * 3;
-    const bool l0 = lane == 0;
-    const unsigned long long vals[8] = {0, l0 ? ws[0] : 0u, l0 ? ws[1] : 0u, l0 ? ws[2] : 0u, 0,
-                                        l0 ? T.absorbs : 0u, l0 ? T.laneSlots : 0u,
-                                        l0 ? (unsigned long long)stepRequests + flushed : 0ull};
-    flushStats(a, vals);
-}
-
-template <int GRID, bool ONECOMP>
-__global__ void __launch_bounds__(kCacheBlock) traceKernelCached(const Args a) {
-    traceBodyCached<GRID, ONECOMP>(a);
-}
-
-// ------------------------------------------------------------------ FILL ray sort (Args::sortFill)
-// Between the event kernel and the trace kernel of an iteration, a counting sort of the FILL queue by
-// fillSortKey: sortRankKernel gives every ray its rank among the rays of its key (one returning atomic per
-// ray on the key's count), the scan kernels turn the counts into each key's first position, and
-// sortPlaceKernel writes fillPerm[first[key] + rank] = ray. The ray count is read on the device.
-
-// exclusive scan of one value per thread over the block; returns the thread's prefix, *total the block's sum
-template <int NT>
-__device__ __forceinline__ unsigned blockExclusiveScan(unsigned v, unsigned* part, unsigned* total) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    unsigned inc = v;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const unsigned u = __shfl_up(inc, off);
-        if (lane >= off) inc += u;
-    }
-    if (lane == 63) part[wave] = inc;
-    __syncthreads();
-    unsigned before = 0, all = 0;
-#pragma unroll
-    for (int w = 0; w < NT / 64; w++) {
-        const unsigned pw = part[w];
-        if (w < wave) before += pw;
-        all += pw;
-    }
-    __syncthreads();  // part is reused by the next call
-    *total = all;
-    return before + inc - v;
-}
-
-__global__ void __launch_bounds__(kBlock) sortRankKernel(const Args a) {
-    const unsigned n = a.ctr[kCtrFill + a.parity];
-    for (unsigned f = blockIdx.x * kBlock + threadIdx.x; f < n; f += gridDim.x * kBlock)
-        a.fillRank[f] = atomicAdd(a.sortHist + a.fillKey[f], 1u);
-}
-
-// block b: the sum of the counts of keys [b kScanChunk, (b + 1) kScanChunk)
-__global__ void __launch_bounds__(kBlock) sortScanSumsKernel(const Args a) {
-    if (a.ctr[kCtrFill + a.parity] == 0) return;
-    __shared__ unsigned part[kBlock / 64];
-    const uint4* h = reinterpret_cast<const uint4*>(a.sortHist + (size_t)blockIdx.x * kScanChunk);
-    static_assert(kScanChunk == 4 * kBlock, "one uint4 of counts per thread");
-    const uint4 c = h[threadIdx.x];
-    unsigned total;
-    (void)blockExclusiveScan<kBlock>(c.x + c.y + c.z + c.w, part, &total);
-    if (threadIdx.x == 0) a.sortBlockSums[blockIdx.x] = total;
-}
-
-// the chunk sums' exclusive scan, in place (kSortBuckets / kScanChunk sums, two per thread)
-constexpr int kScanTop = (int)(kSortBuckets / kScanChunk);
-__global__ void __launch_bounds__(kScanTop / 2) sortScanTopKernel(const Args a) {
-    if (a.ctr[kCtrFill + a.parity] == 0) return;
-    __shared__ unsigned part[kScanTop / 2 / 64];
-    uint2* s2 = reinterpret_cast<uint2*>(a.sortBlockSums);
-    const uint2 v = s2[threadIdx.x];
-    unsigned total;
-    const unsigned pre = blockExclusiveScan<kScanTop / 2>(v.x + v.y, part, &total);
-    s2[threadIdx.x] = make_uint2(pre, pre + v.x);
-}
-
-// the counts of chunk b become first positions: the chunk's exclusive scan plus the sums before the chunk
-__global__ void __launch_bounds__(kBlock) sortScanApplyKernel(const Args a) {
-    if (a.ctr[kCtrFill + a.parity] == 0) return;
-    __shared__ unsigned part[kBlock / 64];
-    uint4* h = reinterpret_cast<uint4*>(a.sortHist + (size_t)blockIdx.x * kScanChunk);
-    const uint4 c = h[threadIdx.x];
-    unsigned total;
-    const unsigned pre = blockExclusiveScan<kBlock>(c.x + c.y + c.z + c.w, part, &total) + a.sortBlockSums[blockIdx.x];
-    h[threadIdx.x] = make_uint4(pre, pre + c.x, pre + c.x + c.y, pre + c.x + c.y + c.z);
-}
-
-__global__ void __launch_bounds__(kBlock) sortPlaceKernel(const Args a) {
-    const unsigned n = a.ctr[kCtrFill + a.parity];
-    for (unsigned f = blockIdx.x * kBlock + threadIdx.x; f < n; f += gridDim.x * kBlock)
-        a.fillPerm[a.sortHist[a.fillKey[f]] + a.fillRank[f]] = f;
-}
-
 // the detections of this iteration's peel-off rays (their optical depths are in the queue now)
 __global__ void __launch_bounds__(kBlock) detectKernel(const Args a) {
     extern __shared__ __attribute__((aligned(16))) double lds[];
     const unsigned int nrays = a.ctr[5 + a.parity];  // this iteration's detection records
     if (nrays == 0) return;
-#ifdef SKIRT_EXPERIMENT_TIMELINE
-    const unsigned long long tlStart = __builtin_amdgcn_s_memrealtime();
-#endif
     Shared sh = stageTables(a, lds, STAGE_INSTR);
     const int copies = a.detCopies;
     for (int q = threadIdx.x; q < copies * a.nsed; q += blockDim.x) sh.sed[q] = 0.0;
@@ -2868,12 +2062,6 @@ __global__ void __launch_bounds__(kBlock) detectKernel(const Args a) {
             atomicAddF64(a.tally + sh.instr[ii].sedBase + (q - sh.instr[ii].sedOff), v);
         }
     }
-#ifdef SKIRT_EXPERIMENT_TIMELINE
-    if (unsigned long long* t = tlSlot(a, 2)) {
-        const unsigned long long tEnd = __builtin_amdgcn_s_memrealtime();
-        if (lane == 0) { t[0] = tlStart; t[1] = 0; t[2] = tEnd; t[3] = nrays; }
-    }
-#endif
     const unsigned long long vals[8] = {0, 0, 0, 0, detects, 0, 0, 0};
     flushStats(a, vals);
 }
@@ -2896,8 +2084,8 @@ struct Events {
     // queues ray `pos`. The trace kernel enters the grid, except for Voronoi grids (kEnterInEvent): their
     // cellIndex loops over a block's site list, which costs the trace kernel more than it costs here. A
     // path found empty here (no dust system, or a Voronoi ray missing the grid) is finished here.
-    __device__ __forceinline__ void emitRay(RayRec* queue, unsigned pos, const Packet& p, double dx, double dy, double dz,
-                                            double prm, int idx, unsigned flags, int& vcell) {
+    __device__ __forceinline__ void emitRay(unsigned pos, const Packet& p, double dx, double dy, double dz, double prm,
+                                            int idx, unsigned flags, int& vcell) {
         Ray r;
         r.x = p.rx; r.y = p.ry; r.z = p.rz;
         r.dx = dx; r.dy = dy; r.dz = dz;
@@ -2907,7 +2095,7 @@ struct Events {
         r.s = 0;
         r.ci = r.cj = 0;
         const unsigned mode = rayMode(flags);
-        int4* dst = reinterpret_cast<int4*>(queue + pos);
+        int4* dst = reinterpret_cast<int4*>(a.rays + pos);
         bool entered = a.hasDust;
         unsigned nseg = 0;
         if constexpr (kEnterInEvent<GRID>) {
@@ -3360,75 +2548,47 @@ __device__ __forceinline__ void blockReserve3(unsigned* ctr0, unsigned c0, unsig
     __syncthreads();  // the scratch words are reused by the next call
 }
 
-// N counters at once (scratch: N * (kBlock / 64) + N words); counter q's atomic is issued by lane q / W of
-// wave q % W (W waves per block)
-template <int N>
-__device__ __forceinline__ void blockReserveN(unsigned* const (&ctr)[N], const unsigned (&c)[N], unsigned (&r)[N],
+// four counters at once (scratch: 4 * (kBlock / 64) + 4 words); the first lane of wave q issues counter q's atomic
+static_assert(kBlock >= 256, "blockReserve4 needs four waves per block");
+__device__ __forceinline__ void blockReserve4(unsigned* const (&ctr)[4], const unsigned (&c)[4], unsigned (&r)[4],
                                               unsigned long long* scratch) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     constexpr int W = kBlock / 64;
-    unsigned in[N];
+    unsigned in[4];
 #pragma unroll
-    for (int q = 0; q < N; q++) in[q] = c[q];
+    for (int q = 0; q < 4; q++) in[q] = c[q];
 #pragma unroll
     for (int off = 1; off < 64; off <<= 1) {
-        unsigned v[N];
+        unsigned v[4];
 #pragma unroll
-        for (int q = 0; q < N; q++) v[q] = __shfl_up(in[q], off);
+        for (int q = 0; q < 4; q++) v[q] = __shfl_up(in[q], off);
         if (lane >= off) {
 #pragma unroll
-            for (int q = 0; q < N; q++) in[q] += v[q];
+            for (int q = 0; q < 4; q++) in[q] += v[q];
         }
     }
     if (lane == 63) {
 #pragma unroll
-        for (int q = 0; q < N; q++) scratch[q * W + wave] = in[q];
+        for (int q = 0; q < 4; q++) scratch[q * W + wave] = in[q];
     }
     __syncthreads();
-    unsigned w[N], t[N];
-#pragma unroll
-    for (int q = 0; q < N; q++) w[q] = t[q] = 0;
+    unsigned w[4] = {0, 0, 0, 0}, t[4] = {0, 0, 0, 0};
 #pragma unroll
     for (int ww = 0; ww < W; ww++) {
 #pragma unroll
-        for (int q = 0; q < N; q++) {
+        for (int q = 0; q < 4; q++) {
             const unsigned sv = (unsigned)scratch[q * W + ww];
             if (ww < wave) w[q] += sv;
             t[q] += sv;
         }
     }
 #pragma unroll
-    for (int q = 0; q < N; q++)
-        if (threadIdx.x == 64 * (q % W) + q / W) scratch[N * W + q] = t[q] ? atomicAdd(ctr[q], t[q]) : 0u;
+    for (int q = 0; q < 4; q++)
+        if (threadIdx.x == 64 * q) scratch[4 * W + q] = t[q] ? atomicAdd(ctr[q], t[q]) : 0u;
     __syncthreads();
 #pragma unroll
-    for (int q = 0; q < N; q++) r[q] = (unsigned)scratch[N * W + q] + w[q] + in[q] - c[q];
+    for (int q = 0; q < 4; q++) r[q] = (unsigned)scratch[4 * W + q] + w[q] + in[q] - c[q];
     __syncthreads();  // the scratch words are reused by the next call
-}
-
-// The sort key of a FILL ray (Args::sortFill): wavelength (2 bits), direction bin (cube-map face x 4 x 4)
-// and the 16^3 region of the start point in Morton order. Rays of one key start close together and head
-// the same way, so their paths cross the same cells for a while.
-__device__ __forceinline__ unsigned fillSortKey(const Args& a, double x, double y, double z, double kx, double ky,
-                                                double kz, int ell) {
-    const float fx = (float)kx, fy = (float)ky, fz = (float)kz;
-    const float ax = fabsf(fx), ay = fabsf(fy), az = fabsf(fz);
-    unsigned face;
-    float u, v, m;
-    if (ax >= ay && ax >= az) { face = fx > 0.f ? 0u : 1u; m = ax; u = fy; v = fz; }
-    else if (ay >= az) { face = fy > 0.f ? 2u : 3u; m = ay; u = fx; v = fz; }
-    else { face = fz > 0.f ? 4u : 5u; m = az; u = fx; v = fy; }
-    const float im = m > 0.f ? 1.f / m : 0.f;
-    const unsigned iu = (unsigned)min(3, max(0, (int)((u * im * 0.5f + 0.5f) * 4.f)));
-    const unsigned iv = (unsigned)min(3, max(0, (int)((v * im * 0.5f + 0.5f) * 4.f)));
-    const unsigned dir = (face * 4u + iu) * 4u + iv;
-    constexpr int R = 1 << kSortRegionBits;
-    auto cell = [](double t, double lo, double hi) {
-        return (unsigned)min(R - 1, max(0, (int)((float)((t - lo) / (hi - lo)) * (float)R)));
-    };
-    const unsigned mort = spread3(cell(x, a.gx0, a.gx1)) | (spread3(cell(y, a.gy0, a.gy1)) << 1) |
-                          (spread3(cell(z, a.gz0, a.gz1)) << 2);
-    return ((unsigned)(ell & 3) << (7 + 3 * kSortRegionBits)) | (dir << (3 * kSortRegionBits)) | mort;
 }
 
 // Global packet index of the j-th packet of this call. A sharded call (IdenticalAssigner,
@@ -3443,23 +2603,10 @@ __device__ __forceinline__ unsigned long long globalPacket(const Args& a, unsign
 
 template <int GRID, bool ONECOMP>
 __global__ void __launch_bounds__(kBlock) SKIRT_EVENT_ATTR eventKernel(const Args a) {
-    __shared__ unsigned long long resv[5 * (kBlock / 64) + 5];
+    __shared__ unsigned long long resv[4 * (kBlock / 64) + 4];
     extern __shared__ __attribute__((aligned(16))) double lds[];
     if (blockIdx.x == 0 && threadIdx.x == 0) a.ctr[4] = 0;  // the trace kernel's pull counter
     if (!a.init && a.ctr[2 + a.parity] == 0) return;  // an iteration after the end of the phase
-#ifdef SKIRT_EXPERIMENT_TIMELINE
-    const unsigned long long tlStart = __builtin_amdgcn_s_memrealtime();
-    // shader-clock cycles per part of a round: state loads + the FILL/WALK events, packet claims and launches,
-    // the block reservations, the ray and state writes
-    unsigned long long tlPart[4] = {0, 0, 0, 0};
-    auto stamp = [] {
-        unsigned long long t;
-        __builtin_amdgcn_sched_barrier(0);
-        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-        __builtin_amdgcn_sched_barrier(0);
-        return t;
-    };
-#endif
     Shared sh = stageTables(a, lds, gridParts<GRID>() | STAGE_OPTICS | STAGE_INSTR);
     Events<GRID, ONECOMP> E{a, sh};
     const int lane = threadIdx.x & 63;
@@ -3477,9 +2624,6 @@ __global__ void __launch_bounds__(kBlock) SKIRT_EVENT_ATTR eventKernel(const Arg
     for (unsigned int round = 0; round < rounds; round++) {
         const unsigned int w = round * stride + w0;
         const bool valid = w < nwork;
-#ifdef SKIRT_EXPERIMENT_TIMELINE
-        unsigned long long ts0 = stamp();
-#endif
         const int slot = slotNext;
         const unsigned int wn = w + stride;
         if (round + 1 < rounds) slotNext = (wn < nwork) ? (a.init ? (int)wn : actIn[wn]) : 0;
@@ -3537,11 +2681,6 @@ __global__ void __launch_bounds__(kBlock) SKIRT_EVENT_ATTR eventKernel(const Arg
         }
         // slots without a packet claim the next global packet indices (one atomic per block)
         bool need = valid && p.state == S_NEW && mainMode == RAY_NONE;
-#ifdef SKIRT_EXPERIMENT_TIMELINE
-        { const bool any = __ballot(need) != 0; (void)any; }
-        unsigned long long ts1 = stamp();
-        tlPart[0] += ts1 - ts0;
-#endif
         while (__syncthreads_or(need)) {
             unsigned long long idx = 0;
             unsigned int unused = 0;
@@ -3573,10 +2712,6 @@ __global__ void __launch_bounds__(kBlock) SKIRT_EVENT_ATTR eventKernel(const Arg
                 }
             }
         }
-#ifdef SKIRT_EXPERIMENT_TIMELINE
-        unsigned long long ts2 = stamp();
-        tlPart[1] += ts2 - ts1;
-#endif
         // rays this lane queues: its peel-offs and its next FILL/WALK ray
         int nray = 0;
         if (peel != PEEL_NONE) {
@@ -3591,28 +2726,21 @@ __global__ void __launch_bounds__(kBlock) SKIRT_EVENT_ATTR eventKernel(const Arg
         // the peel-offs: one atomic each per block
         const bool active = mainMode != RAY_NONE;
         const int npeel = nray - (mainMode != RAY_NONE ? 1 : 0);
-        // a WALK ray goes to the top of the queue (Args::walkBack), a FILL ray to the FILL queue
+        // a WALK ray goes to the top of the queue (Args::walkBack)
         const bool back = a.walkBack && mainMode == RAY_WALK;
-        const bool fill = mainMode == RAY_FILL && a.sortFill;  // (sortFill: the FILL queue)
-        unsigned int pos, apos, dpos, wpos, fpos;
+        unsigned int pos, apos, dpos, wpos;
         {
-            unsigned* const ctrs[5] = {a.ctr + a.parity, a.ctr + 2 + (1 - a.parity), a.ctr + 5 + a.parity,
-                                       a.ctr + 8 + a.parity, a.ctr + kCtrFill + a.parity};
-            const unsigned cnt[5] = {(unsigned)nray - ((back || fill) ? 1u : 0u), active ? 1u : 0u, (unsigned)npeel,
-                                     back ? 1u : 0u, fill ? 1u : 0u};
-            unsigned res[5];
-            blockReserveN<5>(ctrs, cnt, res, resv);
-            pos = res[0]; apos = res[1]; dpos = res[2]; wpos = res[3]; fpos = res[4];
+            unsigned* const ctrs[4] = {a.ctr + a.parity, a.ctr + 2 + (1 - a.parity), a.ctr + 5 + a.parity, a.ctr + 8 + a.parity};
+            const unsigned cnt[4] = {(unsigned)nray - (back ? 1u : 0u), active ? 1u : 0u, (unsigned)npeel, back ? 1u : 0u};
+            unsigned res[4];
+            blockReserve4(ctrs, cnt, res, resv);
+            pos = res[0]; apos = res[1]; dpos = res[2]; wpos = res[3];
         }
-#ifdef SKIRT_EXPERIMENT_TIMELINE
-        unsigned long long ts3 = stamp();
-        tlPart[2] += ts3 - ts2;
-#endif
         // the queue holds rayCap records (ensurePool sizes it for the slots' most rays per iteration): a
         // lane whose records would fall outside it writes none and fails the phase (ERR_QUEUE); the trace
         // kernel checks that the front and the WALK region do not meet
-        if ((unsigned long long)pos + (unsigned)(nray - ((back || fill) ? 1 : 0)) > (unsigned long long)a.rayCap ||
-            (back && wpos >= (unsigned)a.rayCap) || (fill && fpos >= (unsigned)a.nslots) ||
+        if ((unsigned long long)pos + (unsigned)(nray - (back ? 1 : 0)) > (unsigned long long)a.rayCap ||
+            (back && wpos >= (unsigned)a.rayCap) ||
             (unsigned long long)dpos + (unsigned)npeel > (unsigned long long)(a.rayCap - a.nslots)) {
             atomicOr(a.error, ERR_QUEUE);
             nray = 0;
@@ -3656,29 +2784,15 @@ __global__ void __launch_bounds__(kBlock) SKIRT_EVENT_ATTR eventKernel(const Arg
                 prm = mainParam;
                 idx = slot;
                 flags = mainMode | ((unsigned)p.ell << 18);
-                at = fill ? fpos : back ? (unsigned)a.rayCap - 1u - wpos : pos++;
-                if (fill) a.fillKey[fpos] = fillSortKey(a, p.rx, p.ry, p.rz, dx, dy, dz, p.ell);
+                at = back ? (unsigned)a.rayCap - 1u - wpos : pos++;
             }
-            // (one call site: one inlined grid entry)
-            E.emitRay((k >= npeel && fill) ? a.fillRays : a.rays, at, p, dx, dy, dz, prm, idx, flags, vcell);
+            E.emitRay(at, p, dx, dy, dz, prm, idx, flags, vcell);  // (one call site: one inlined grid entry)
         }
         // the slot stays active while it has a FILL/WALK ray in flight
         if (active) actOut[apos] = slot;
         if (valid) E.store(slot, p);
         if (kEnterInEvent<GRID> && valid) a.svcell[slot] = vcell;
-#ifdef SKIRT_EXPERIMENT_TIMELINE
-        tlPart[3] += stamp() - ts3;
-#endif
     }
-#ifdef SKIRT_EXPERIMENT_TIMELINE
-    if (unsigned long long* t = tlSlot(a, 1)) {
-        const unsigned long long tEnd = __builtin_amdgcn_s_memrealtime();
-        if (lane == 0) {
-            t[0] = tlStart; t[1] = 0; t[2] = tEnd; t[3] = rounds;
-            for (int q = 0; q < 4; q++) t[4 + q] = tlPart[q];
-        }
-    }
-#endif
     const unsigned long long vals[8] = {E.packets, E.segFill, E.segWalk, E.segPeel, E.detects, 0, 0, 0};
     flushStats(a, vals);
 }
@@ -3775,7 +2889,7 @@ __global__ void __launch_bounds__(kBlock) contKernel(const Args a) {
                     const unsigned level = (unsigned)min(p.nscatt + 1, 255);
                     const unsigned flags = RAY_PEEL | (cat << 2) | ((unsigned)i << 4) | (level << 10) | ((unsigned)p.ell << 18);
                     a.det[dpos] = DetRec{Lp, 0.0, l, flags};
-                    E.emitRay(a.rays, pos++, q, ins.kobs[0], ins.kobs[1], ins.kobs[2], Lp, (int)dpos, flags, qcell);
+                    E.emitRay(pos++, q, ins.kobs[0], ins.kobs[1], ins.kobs[2], Lp, (int)dpos, flags, qcell);
                     dpos++;
                 }
             }
@@ -3890,10 +3004,6 @@ struct SkirtMcrt {
     // runs without the atomic-free WALK paths between the absorbing FILL paths: C3 2.16e8 -> 2.08e8, C2
     // 2.9e8 -> 2.8e8; C4 9.30e7 -> 9.38e7 (profiles/r03_walk_back_ab.txt)
     int walkBack = getenv("SKIRT_AMD_WALK_BACK") ? atoi(getenv("SKIRT_AMD_WALK_BACK")) : -1;
-    // the Labs line cache with sorted FILL rays (traceKernelCached) for absorbing phases on Cartesian grids and
-    // octree / k-d tree leaf maps: SKIRT_AMD_LABS_CACHE=0 turns it off (the per-lane buffered drain instead)
-    int labsCache = getenv("SKIRT_AMD_LABS_CACHE") ? atoi(getenv("SKIRT_AMD_LABS_CACHE")) : 0;
-    int lastCached = 0;        // the cache sets of the last phase's trace kernel (0: the per-lane drain)
     int traceBlocksPerCU = 0;  // the occupancy the last trace launch was sized for
     int lastDetCopies = 0;  // SED copies of the last run's detect kernel
     double lastMs = 0;
@@ -3944,10 +3054,8 @@ int ensurePool(SkirtMcrt* c, int nslots, bool continuous, int halves) {
     if (rays >= (size_t)INT32_MAX) return fail(c, SKIRT_ERR_UNSUPPORTED, "ray queue too large");
     const int rayCap = (int)rays;
     const size_t path = continuous ? (size_t)nslots * (kPathCap * sizeof(PathRec) + sizeof(int)) : 0;
-    // + the FILL queue with its sort keys, ranks and order, and the sort's key counts
-    const size_t fillq = (size_t)nslots * (sizeof(RayRec) + 3 * 4) + (size_t)kSortBuckets * 4 + (size_t)kScanTop * 4 + 64;
     const size_t half = (size_t)rayCap * sizeof(RayRec) + (size_t)(rayCap - nslots) * sizeof(DetRec) +
-                        (size_t)nslots * (10 * 8 + 5 * 4 + 6 * 4 + 2 * 4) + path + fillq + 4096;
+                        (size_t)nslots * (10 * 8 + 5 * 4 + 6 * 4 + 2 * 4) + path + 4096;
     if (c->dPool && c->nslots == nslots && c->rayCap == rayCap && c->poolPath == (path > 0) && c->poolHalves == halves)
         return SKIRT_OK;
     c->poolPath = path > 0;
@@ -4024,15 +3132,6 @@ void carvePool(SkirtMcrt* c, Args& a, int h) {
         p += n * kPathCap * sizeof(PathRec);
         takeI(a.pathCnt);
     }
-    p = reinterpret_cast<char*>(((uintptr_t)p + 15) & ~(uintptr_t)15);
-    a.fillRays = reinterpret_cast<RayRec*>(p);
-    p += n * sizeof(RayRec);
-    takeU(a.fillKey); takeU(a.fillRank); takeU(a.fillPerm);
-    p = reinterpret_cast<char*>(((uintptr_t)p + 15) & ~(uintptr_t)15);
-    a.sortHist = reinterpret_cast<uint32_t*>(p);
-    p += (size_t)kSortBuckets * 4;
-    a.sortBlockSums = reinterpret_cast<uint32_t*>(p);
-    p += (size_t)kScanTop * 4;
     a.nslots = c->nslots;
     a.rayCap = c->rayCap;
     a.ctr = c->dCtr + kCtrWords * h;
@@ -4496,8 +3595,8 @@ int skirt_mcrt_upload_grid(SkirtMcrt* c, const SkirtGridDesc* g) {
             const int m = refOf[d];
             const int cnt = g->cell_nbr_offset[m + 1] - g->cell_nbr_offset[m];
             if (cnt < 1) return fail(c, SKIRT_ERR_ARG, "Voronoi cell without neighbours");
-            // pairs of entries; with kVorPadNaN whole groups of kVorUnroll (even)
-            const int per = kVorPadNaN ? kVorUnroll : 2;
+            // whole groups of kVorUnroll entries (even)
+            const int per = kVorUnroll;
             start[d + 1] = start[d] + kVorHead + (cnt + per - 1) / per * per;
         }
         if ((size_t)start[N] + kVorPad >= (size_t)INT32_MAX) return fail(c, SKIRT_ERR_UNSUPPORTED, "Voronoi mesh too large");
@@ -5094,12 +4193,16 @@ static int runPhase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, uint6
     a.store = phase == SKIRT_PHASE_STELLAR ? (p->store_absorption ? 1 : 0) : (phase == SKIRT_PHASE_DUST_SELFABS ? 1 : 0);
     a.hasDust = p->has_dust ? 1 : 0;
     if (a.store && !c->dLabs) return fail(c, SKIRT_ERR_STATE, "no Labs buffer");
-    // the trace kernel addresses Labs through a buffer descriptor (32-bit byte offsets, one byte past the end
-    // for the drain's empty lanes): at most 4 GiB - 8 (e.g. 2^21 cells x 255 wavelengths)
-    if ((uint64_t)c->labsStride * (uint64_t)c->nlambda * sizeof(double) > 0xfffffff8ull)
-        return fail(c, SKIRT_ERR_UNSUPPORTED, "Labs table larger than 4 GiB");
+    // the trace kernel adds to Labs through a buffer descriptor (32-bit byte offsets, one byte past the end
+    // for the drain's empty lanes) while the table holds at most 4 GiB - 8 (e.g. 2^21 cells x 255
+    // wavelengths), with global atomics beyond (SKIRT_AMD_LABS_GLOBAL=1 forces them: tests); the buffered
+    // adds carry 32-bit element indices, so 2^32 doubles (32 GiB) at most
+    const uint64_t labsElems = (uint64_t)c->labsStride * (uint64_t)c->nlambda;
+    if (a.store && labsElems > 0xffffffffull) return fail(c, SKIRT_ERR_UNSUPPORTED, "Labs table larger than 32 GiB");
+    const bool forceGlobal = getenv("SKIRT_AMD_LABS_GLOBAL") && atoi(getenv("SKIRT_AMD_LABS_GLOBAL")) != 0;
+    a.labsGlobal = (forceGlobal || labsElems * sizeof(double) > 0xfffffff8ull) ? 1 : 0;
     a.labs = phase == SKIRT_PHASE_DUST_SELFABS ? c->dLabsDust : c->dLabs;
-    a.labsBytes = (unsigned)((size_t)c->labsStride * c->nlambda * sizeof(double));
+    a.labsBytes = a.labsGlobal ? 0u : (unsigned)(labsElems * sizeof(double));
     a.tally = c->dTally;
     a.error = c->dError; a.stats = c->dStats;
     a.crossed = c->dCrossed; a.crossedBins = c->crossedBins;
@@ -5123,28 +4226,6 @@ static int runPhase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, uint6
                             + (size_t)kLabsBuf * kBlock * (sizeof(double) + sizeof(unsigned))  // + Labs buffers
                             + (size_t)3 * (kBlock / 64) * sizeof(unsigned);               // + segment counts
     const size_t ldsEvent = (size_t)a.ldsSedOff * sizeof(double);           // + instruments
-    // the cached trace kernel (absorbing phases on the grids whose walk adds one segment per step): the
-    // largest power-of-two number of cache sets that fits next to the tables
-    const bool leafKind = c->gridKind == SKIRT_GRID_OCTREE && leafMap;
-    const bool cacheGrid = (c->gridKind == SKIRT_GRID_CARTESIAN || leafKind) && a.hasDust;
-    size_t ldsCached = 0;
-    a.sortFill = 0;
-    a.cacheSets = 0;
-    if (c->labsCache && cacheGrid && a.store && !continuous) {
-        const size_t tables = (((size_t)a.ldsInstrOff * sizeof(double)) + 15) & ~(size_t)15;
-        const size_t fixed = (size_t)kCacheWaves * kEvictLines * (64 + 4) + 8 + (size_t)kCacheWaves * 3 * 4 + 16;
-        const size_t perSet = (size_t)kCacheWays * (8 + 64) + 4;
-        int sets = 1 << 12;
-        while (sets >= 8 && tables + fixed + (size_t)sets * perSet > c->ldsMax) sets >>= 1;
-        if (sets >= 8) {
-            a.sortFill = 1;
-            a.cacheSets = sets;
-            a.ldsCacheOff = (int)tables;
-            ldsCached = tables + fixed + (size_t)sets * perSet;
-        }
-    }
-    c->lastCached = a.sortFill ? a.cacheSets : 0;
-    a.cacheDebug = getenv("SKIRT_AMD_CACHE_DEBUG") ? atoi(getenv("SKIRT_AMD_CACHE_DEBUG")) : 0;
     // budget: what one workgroup may allocate (160 KiB on gfx950). The trace and event kernels need their
     // tables; the detect kernel keeps as many SED copies as fit (8, 4, 2, 1), or none (SEDs to the tally)
     const size_t budget = c->ldsMax;
@@ -5175,19 +4256,11 @@ static int runPhase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, uint6
                                                : SKIRT_WALK_TREE_NODES;
     const bool one = a.ncomp == 1;
     const void* traceFn = nullptr;
-    if (a.sortFill) {
-        if (kind == SKIRT_GRID_CARTESIAN) traceFn = one ? (const void*)traceKernelCached<SKIRT_GRID_CARTESIAN, true>
-                                                        : (const void*)traceKernelCached<SKIRT_GRID_CARTESIAN, false>;
-        else if (kind == SKIRT_GRID_OCTREE) traceFn = one ? (const void*)traceKernelCached<SKIRT_GRID_OCTREE, true>
-                                                          : (const void*)traceKernelCached<SKIRT_GRID_OCTREE, false>;
-        else traceFn = one ? (const void*)traceKernelCached<kBinTreeMap, true> : (const void*)traceKernelCached<kBinTreeMap, false>;
-    }
     auto pick = [&](auto fn1, auto fnN, auto fn1c, auto fnNc) {
         traceFn = continuous ? (one ? (const void*)fn1c : (const void*)fnNc) : (one ? (const void*)fn1 : (const void*)fnN);
     };
 #define SKIRT_PICK(G) pick(traceKernel<G, true, false>, traceKernel<G, false, false>, traceKernel<G, true, true>, traceKernel<G, false, true>)
-    if (a.sortFill) {}
-    else if (kind == SKIRT_GRID_CARTESIAN) SKIRT_PICK(SKIRT_GRID_CARTESIAN);
+    if (kind == SKIRT_GRID_CARTESIAN) SKIRT_PICK(SKIRT_GRID_CARTESIAN);
     else if (kind == SKIRT_GRID_OCTREE) SKIRT_PICK(SKIRT_GRID_OCTREE);
     else if (kind == kBinTreeMap) SKIRT_PICK(kBinTreeMap);
     else if (kind == kOctreeBookkeeping) SKIRT_PICK(kOctreeBookkeeping);
@@ -5195,24 +4268,18 @@ static int runPhase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, uint6
         pick(traceKernelVor<true, false>, traceKernelVor<false, false>, traceKernelVor<true, true>, traceKernelVor<false, true>);
     else SKIRT_PICK(kOctreeNodes);
 #undef SKIRT_PICK
-    const size_t ldsT = a.sortFill ? ldsCached : ldsTrace;
-    const int tblock = a.sortFill ? kCacheBlock : kBlock;
-    if (ldsT > 64 * 1024)
-        HIPCHECK(c, hipFuncSetAttribute(traceFn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ldsT));
+    if (ldsTrace > 64 * 1024)
+        HIPCHECK(c, hipFuncSetAttribute(traceFn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ldsTrace));
     int tgrid = c->traceGrid;
-    if (a.sortFill) {
-        tgrid = std::max(1, c->nCusT);  // one workgroup of 12 waves per CU
-        c->traceBlocksPerCU = 1;
-    } else if (tgrid <= 0) {
+    if (tgrid <= 0) {
         int per = 0;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, traceFn, kBlock, ldsTrace) != hipSuccess || per < 1) per = 2;
         tgrid = std::max(1, c->nCusT) * per;
         c->traceBlocksPerCU = per;
     }
-    // event kernel blocks per CU (SKIRT_AMD_EVENT_BPC: tuning knob). Voronoi: 3, since its event kernel fits
-    // 3 waves/SIMD (C4 +0.6 %, profiles/r04_event_bpc_sweep.txt); the others are within the spread at 2-4
-    static const int ebpcEnv = getenv("SKIRT_AMD_EVENT_BPC") ? std::max(1, atoi(getenv("SKIRT_AMD_EVENT_BPC"))) : 0;
-    const int ebpc = ebpcEnv ? ebpcEnv : (kind == SKIRT_GRID_VORONOI ? 3 : 2);
+    // event kernel blocks per CU. Voronoi: 3, since its event kernel fits 3 waves/SIMD (C4 +0.6 %,
+    // profiles/r04_event_bpc_sweep.txt); the others are within the spread at 2-4
+    const int ebpc = kind == SKIRT_GRID_VORONOI ? 3 : 2;
     const int egrid = std::max(1, std::min((slots + kBlock - 1) / kBlock, std::max(1, c->nCusE) * ebpc));
     const int dgrid = std::max(1, std::max(1, c->nCusE) * 4);
 
@@ -5247,7 +4314,7 @@ static int runPhase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, uint6
     auto launchTrace = [&](const Args& aa, hipStream_t st) {
         // the kernel picked above (traceFn), launched through its generic entry
         void* args[] = {const_cast<Args*>(&aa)};
-        return hipLaunchKernel(traceFn, dim3(tgrid), dim3(tblock), args, ldsT, st);
+        return hipLaunchKernel(traceFn, dim3(tgrid), dim3(kBlock), args, ldsTrace, st);
     };
     if ((int)c->pollEv.size() < kMaxHalves * kPollRing) {
         while ((int)c->pollEv.size() < kMaxHalves * kPollRing) {
@@ -5268,20 +4335,6 @@ static int runPhase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, uint6
     // detect + event kernels thus run while the other half's trace kernel runs (on CUs of their own when
     // the streams are CU-masked): sE = ev0(0) ev1(0) det0(0) ev0(1) det1(0) ev1(1) ...; sT[0] = tr0(0)
     // tr0(1) ...; each kernel waits only for its own half's previous kernel on the other stream.
-#ifdef SKIRT_EXPERIMENT_TIMELINE
-    // the timeline of the phase call number SKIRT_AMD_TIMELINE_CALL (default 2: after a warm-up call)
-    static int tlCall = 0;
-    const char* tlOut = getenv("SKIRT_AMD_TIMELINE_OUT");
-    const int tlWant = getenv("SKIRT_AMD_TIMELINE_CALL") ? atoi(getenv("SKIRT_AMD_TIMELINE_CALL")) : 2;
-    unsigned long long* dTl = nullptr;
-    const size_t tlWords = (size_t)3 * kTlLaunches * kTlWaves * kTlWords;
-    if (tlOut && ++tlCall == tlWant) {
-        HIPCHECK(c, hipMalloc(&dTl, tlWords * 8));
-        HIPCHECK(c, hipMemsetAsync(dTl, 0, tlWords * 8, c->stream));
-    }
-    a.tl = dTl;
-    a.tlLaunch = 0;
-#endif
     Args ah[kMaxHalves], prev[kMaxHalves];
     int its[kMaxHalves] = {0}, polls[kMaxHalves] = {0};
     int pollIt[kMaxHalves][kPollRing] = {};  // the iteration count each copy was taken at
@@ -5289,7 +4342,6 @@ static int runPhase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, uint6
     for (int h = 0; h < halves; h++) {
         ah[h] = a;
         carvePool(c, ah[h], h);
-        if (!a.sortFill || (a.cacheDebug & 2)) ah[h].fillPerm = nullptr;  // FILL rays traced in queue order
     }
     // the detect kernel of half h's last trace launch (on sE, after that launch), then the counter copy
     auto detect = [&](int h) -> int {
@@ -5324,9 +4376,6 @@ static int runPhase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, uint6
             if (its[h] > 10000000) return fail(c, SKIRT_ERR_STATE, "photon phase did not terminate");
             aa.parity = its[h] & 1;
             aa.init = (its[h] == 0) ? 1 : 0;
-#ifdef SKIRT_EXPERIMENT_TIMELINE
-            aa.tlLaunch = its[h] * halves + h;
-#endif
             if (aa.continuous && !aa.init) {  // the continuous peel-offs of the FILL rays that just returned
                 launchCont(aa, sE);
                 HIPCHECK(c, hipGetLastError());
@@ -5334,16 +4383,6 @@ static int runPhase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, uint6
             launchEvent(aa, sE);
             HIPCHECK(c, hipGetLastError());
             if (!a.hasDust) { done[h] = true; its[h]++; continue; }  // every packet completes in the event kernel
-            if (aa.sortFill && aa.fillPerm) {  // the FILL rays in key order (their count is on the device)
-                const int sgrid = std::max(1, std::min((c->nslots + kBlock - 1) / kBlock, c->numCUs * 8));
-                HIPCHECK(c, hipMemsetAsync(aa.sortHist, 0, (size_t)kSortBuckets * 4, sE));
-                hipLaunchKernelGGL(sortRankKernel, dim3(sgrid), dim3(kBlock), 0, sE, aa);
-                hipLaunchKernelGGL(sortScanSumsKernel, dim3(kScanTop), dim3(kBlock), 0, sE, aa);
-                hipLaunchKernelGGL(sortScanTopKernel, dim3(1), dim3(kScanTop / 2), 0, sE, aa);
-                hipLaunchKernelGGL(sortScanApplyKernel, dim3(kScanTop), dim3(kBlock), 0, sE, aa);
-                hipLaunchKernelGGL(sortPlaceKernel, dim3(sgrid), dim3(kBlock), 0, sE, aa);
-                HIPCHECK(c, hipGetLastError());
-            }
             if (sE != sT[h]) {
                 HIPCHECK(c, hipEventRecord(c->evE[h], sE));
                 HIPCHECK(c, hipStreamWaitEvent(sT[h], c->evE[h], 0));
@@ -5380,20 +4419,6 @@ static int runPhase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, uint6
         }
     }
     HIPCHECK(c, hipEventRecord(c->ev1, c->stream));
-#ifdef SKIRT_EXPERIMENT_TIMELINE
-    if (dTl) {
-        std::vector<unsigned long long> h(tlWords);
-        HIPCHECK(c, hipStreamSynchronize(c->stream));
-        HIPCHECK(c, hipMemcpy(h.data(), dTl, tlWords * 8, hipMemcpyDeviceToHost));
-        (void)hipFree(dTl);
-        if (FILE* f = fopen(tlOut, "wb")) {
-            const int hdr[5] = {3, kTlLaunches, kTlWaves, it, kTlWords};
-            fwrite(hdr, sizeof hdr, 1, f);
-            fwrite(h.data(), 8, tlWords, f);
-            fclose(f);
-        }
-    }
-#endif
     return SKIRT_OK;
 }
 
@@ -5546,7 +4571,6 @@ int skirt_mcrt_stats(SkirtMcrt* c, SkirtStats* out) {
     out->device_cells = c->ndev;
     out->trace_blocks_per_cu = (uint64_t)c->traceBlocksPerCU;
     out->packages = c->packagesTotal;
-    out->labs_cache_sets = (uint64_t)c->lastCached;
     return SKIRT_OK;
 }
 

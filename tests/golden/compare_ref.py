@@ -30,10 +30,11 @@ def normalized(path):
 
 
 def differing(dir_a, dir_b, prefix=""):
-    """Names of the files of dir_a (starting with prefix) that are missing from dir_b or differ."""
+    """Names of the files of dir_a (starting with prefix) that are missing from dir_b or differ (files only: the
+    bench/ subdirectory holds fixtures of their own, make_bench_fixtures.sh)."""
     bad = []
     for name in sorted(os.listdir(dir_a)):
-        if not name.startswith(prefix):
+        if not name.startswith(prefix) or os.path.isdir(os.path.join(dir_a, name)):
             continue
         other = os.path.join(dir_b, name)
         if not os.path.exists(other) or normalized(os.path.join(dir_a, name)) != normalized(other):

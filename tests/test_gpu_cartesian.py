@@ -50,8 +50,6 @@ def test_cartesian_engine_matches_oracle_same_streams(tmp_path, name):
 @pytest.mark.parametrize("name", ["cart_odd", "pan_oct"])
 def test_aligned_cell_numbering_equals_plain_numbering(tmp_path, name, monkeypatch):
     path = os.path.join(GOLD, name + ".ski") if name == "pan_oct" else T.write(name, str(tmp_path))
-    # the request counts compare the per-lane buffered drain (the LDS line cache holds a small grid whole)
-    monkeypatch.setenv("SKIRT_AMD_LABS_CACHE", "0")
     runs = []
     for align in ("1", "0"):
         monkeypatch.setenv("SKIRT_AMD_CELL_ALIGN", align)

@@ -1,4 +1,5 @@
 """Per-wave timeline of one photon phase (SKIRT_EXPERIMENT_TIMELINE build, SKIRT_AMD_TIMELINE_OUT file):
+# (archived in round 5: the SKIRT_EXPERIMENT_TIMELINE instrumentation was removed from engine.hip; git history keeps it)
 per iteration the event, trace and detect kernels' spans, the gaps between them, and the trace kernel's
 drain tail (from the first wave that found the ray queue exhausted to the last wave's end), with the
 share of trace waves still running at 25/50/75 % of the tail.

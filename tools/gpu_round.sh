@@ -101,7 +101,7 @@ multi)
     done
   done ;;
 envs)
-  # ENV_SETS="-|SKIRT_AMD_EVENT_BPC=3|..." ("-": none): two alternating bench rounds per config over engine
+  # ENV_SETS="-|SKIRT_AMD_WALK_BACK=0|..." ("-": none): two alternating bench rounds per config over engine
   # environment settings (gpurun_out/envs.txt)
   out=gpurun_out/envs.txt; : > $out
   IFS='|' read -ra sets <<< "${ENV_SETS:?}"

@@ -345,6 +345,8 @@ int main(int argc, char** argv) {
     add("octant+region32^3", [&](const Ray& y) { return ((unsigned long long)octant(y) << 15) | cellOf(y, 5); });
     add("dir6x4^2+region16^3", [&](const Ray& y) { return ((unsigned long long)dirBin(y.k, 4) << 12) | cellOf(y, 4); });
     add("dir6x4^2+region32^3", [&](const Ray& y) { return ((unsigned long long)dirBin(y.k, 4) << 15) | cellOf(y, 5); });
+    add("dir6x4^2+region4^3", [&](const Ray& y) { return ((unsigned long long)dirBin(y.k, 4) << 6) | cellOf(y, 2); });
+    add("dir6x4^2+region2^3", [&](const Ray& y) { return ((unsigned long long)dirBin(y.k, 4) << 3) | cellOf(y, 1); });
     add("dir6x4^2+region8^3", [&](const Ray& y) { return ((unsigned long long)dirBin(y.k, 4) << 9) | cellOf(y, 3); });
     add("dir6x2^2+region16^3", [&](const Ray& y) { return ((unsigned long long)dirBin(y.k, 2) << 12) | cellOf(y, 4); });
     add("dir6x3^2+region16^3", [&](const Ray& y) { return ((unsigned long long)dirBin(y.k, 3) << 12) | cellOf(y, 4); });

@@ -11,7 +11,9 @@ atomics. The guide's halving of FETCH_SIZE holds for coalesced 16-byte-per-lane 
 scattered gather (one lane per 64-byte line, the trace kernel's leaf-map, Labs and neighbour loads)
 reports its whole 64-byte line (tools/gather_bench.hip, profiles/r02_gather_calibration.txt), so
 FETCH_SIZE is taken as it is: traffic = FETCH_SIZE + WRITE_SIZE.
-usage: python tools/pmc_traffic.py <cfg> <round>
+usage: python tools/pmc_traffic.py <cfg> <round> [<tag>]
+  a tag (a variant's gpurun_out/prof_<cfg><tag>, e.g. tools/gpu_prof.sh run with TAG=_cache1) writes
+  profiles/<round>_rocprof_<cfg><tag>.* and leaves pmc_<cfg>.json (the bench's default build) alone
 """
 import collections
 import csv
@@ -52,10 +54,11 @@ def short(name):
 
 def main():
     cfg, rnd = sys.argv[1], sys.argv[2]
-    base = os.path.join(REPO, "gpurun_out", "prof_" + cfg)
+    tag = sys.argv[3] if len(sys.argv) > 3 else ""
+    base = os.path.join(REPO, "gpurun_out", "prof_" + cfg + tag)
     prof = os.path.join(REPO, "profiles")
     stats = one(base + "/trace/**/*kernel_stats.csv")
-    shutil.copy(stats, os.path.join(prof, "%s_rocprof_%s_kernel_stats.csv" % (rnd, cfg)))
+    shutil.copy(stats, os.path.join(prof, "%s_rocprof_%s%s_kernel_stats.csv" % (rnd, cfg, tag)))
     lines = ["rocprofv3 summary, config %s (%s)" % (cfg, open(os.path.join(base, "cmd.txt")).read().strip()
                                                    if os.path.exists(os.path.join(base, "cmd.txt")) else ""), ""]
     lines.append("kernel stats (--kernel-trace --stats):")
@@ -75,17 +78,18 @@ def main():
                 m = sum(vals) / len(vals)
                 avg[(short(k), cn)] = m
                 lines.append("  %-20s %-22s %.6g  (%d dispatches)" % (short(k), cn, m, len(vals)))
-    open(os.path.join(prof, "%s_rocprof_%s.txt" % (rnd, cfg)), "w").write("\n".join(lines) + "\n")
+    open(os.path.join(prof, "%s_rocprof_%s%s.txt" % (rnd, cfg, tag)), "w").write("\n".join(lines) + "\n")
     f = avg.get(("traceKernel", "FETCH_SIZE"))
     w = avg.get(("traceKernel", "WRITE_SIZE"))
-    if f is not None and w is not None:
+    if f is not None and w is not None and not tag:
         d = {"kernel": "traceKernel", "fetch_size_kib": f, "write_size_kib": w,
              "traffic_bytes_per_launch": f * 1024 + w * 1024,
              "source": "profiles/%s_rocprof_%s.txt: FETCH_SIZE + WRITE_SIZE per traceKernel dispatch" % (rnd, cfg)}
         # the issue and atomic counters of the same dispatches, where their passes ran
         for key, cn in (("valu_insts_per_launch", "SQ_INSTS_VALU"), ("salu_insts_per_launch", "SQ_INSTS_SALU"),
                         ("atomic_requests_per_launch", "TCC_EA0_ATOMIC_sum"), ("grbm_gui_active_per_launch", "GRBM_GUI_ACTIVE"),
-                        ("sq_waves_per_launch", "SQ_WAVES")):
+                        ("sq_waves_per_launch", "SQ_WAVES"), ("valu_active_quads_per_launch", "SQ_ACTIVE_INST_VALU"),
+                        ("inst_active_quads_per_launch", "SQ_ACTIVE_INST_ANY"), ("wave_quads_per_launch", "SQ_WAVE_CYCLES")):
             v = avg.get(("traceKernel", cn))
             if v is not None:
                 d[key] = v
