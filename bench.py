@@ -82,12 +82,13 @@ def pmc_traffic(config):
     return out
 
 
-def bound_of(hbm_frac, atomic_frac):
-    """The trace kernel's limiter from the fractions of HBM bandwidth and of the f64 atomic request rate it
-    uses: the larger one if it is at least half its peak, else instruction issue / latency."""
-    if max(hbm_frac, atomic_frac) < 0.5:
-        return "issue"
-    return "hbm" if hbm_frac >= atomic_frac else "atomic"
+def bound_of(hbm_frac, atomic_frac, valu_busy=None):
+    """The trace kernel's limiter: whichever of HBM bandwidth, the f64 atomic request rate and the VALU (the
+    PMC VALU-busy fraction, where the passes exist) it uses the largest fraction of, if that is at least half;
+    else latency."""
+    fracs = {"hbm": hbm_frac, "atomic": atomic_frac, "valu": valu_busy if valu_busy is not None else 0.0}
+    best = max(fracs, key=fracs.get)
+    return best if fracs[best] >= 0.5 else "latency"
 
 
 def algorithmic_bytes(stats, geom_bytes, ncomp):
@@ -293,12 +294,12 @@ def main():
                            ("segments_fill", "segments_walk", "segments_peel", "absorb_adds", "detects")},
         },
         "roofline": {
-            # the limiter: whichever of HBM bytes and the chip's f64 atomic request rate (the Labs adds) the
-            # trace kernel uses the larger fraction of -- HBM as measured (PMC traffic) when the passes exist,
-            # since a cached working set (the C4 Voronoi mesh, 30 MB, in the MALL) makes the SURVEY bytes exceed
-            # what HBM delivers -- or "issue" when neither is above half its peak (instruction issue and
-            # latency)
-            "bound": bound_of(hbm_frac if traffic is None else traffic_frac, atomic_frac),
+            # the limiter: whichever of HBM bytes, the chip's f64 atomic request rate (the Labs adds) and the
+            # VALU (PMC VALU-busy) the trace kernel uses the largest fraction of -- HBM as measured (PMC traffic)
+            # when the passes exist, since a cached working set (the C4 Voronoi mesh, 30 MB, in the MALL) makes
+            # the SURVEY bytes exceed what HBM delivers -- or "latency" when none is above half its peak
+            # 
+            "bound": bound_of(hbm_frac if traffic is None else traffic_frac, atomic_frac, valu_busy),
             # SURVEY 8(d)'s bytes over the launch time; where they exceed the HBM peak (a cache-resident
             # working set: the C4 mesh lives in the MALL) they are no roofline, and frac is the measured
             # HBM traffic's fraction instead

@@ -91,6 +91,17 @@ GpuPhotonEngine::~GpuPhotonEngine()
 {
     if (_ctx) skirt_mcrt_destroy(_ctx);
     if (_voronoi) skirt_host_voronoi_free(_voronoi);
+    if (_rccl) skirt_rccl_destroy(_rccl);  // (a wrapped communicator stays the caller's)
+}
+
+////////////////////////////////////////////////////////////////////
+
+void GpuPhotonEngine::sumOnDevices(void* ncclComm, int rank)
+{
+    if (skirt_rccl_wrap(ncclComm, &_rccl) != SKIRT_OK)
+        throw FATALERROR("MI355X engine: cannot wrap the RCCL communicator");
+    _sumRank = rank;
+    check(skirt_mcrt_set_reducer(_ctx, skirt_rccl_reducer(), skirt_rccl_rank(_rccl, 0)));
 }
 
 ////////////////////////////////////////////////////////////////////
@@ -367,7 +378,7 @@ void GpuPhotonEngine::runPhase(int phase, uint32_t cycle, uint64_t Npp, uint64_t
 void GpuPhotonEngine::runStellar(uint64_t Npp, uint64_t seed, int rank, int size)
 {
     runPhase(SKIRT_PHASE_STELLAR, 0, Npp, seed, rank, size);
-    if (_params.store_absorption)
+    if (_params.store_absorption && handsTallies())
     {
         // DustSystem::absorb, as simulateescapeandabsorption calls it (MonteCarloSimulation.cpp:438-515)
         std::vector<double> labs(static_cast<size_t>(_Ncells) * _Nlambda);
@@ -422,6 +433,7 @@ void GpuPhotonEngine::runSelfAbsorptionCycle(uint32_t cycle, const Array& Labsbo
     runPhase(SKIRT_PHASE_DUST_SELFABS, cycle, Npp, seed, rank, size);
     std::vector<double> labs(static_cast<size_t>(_Ncells) * _Nlambda);
     check(skirt_mcrt_download_dust_labs(_ctx, labs.data()));
+    if (!handsTallies()) return;  // rank 0 holds the device-summed tallies (sumOnDevices)
     for (int m = 0; m < _Ncells; m++)
         for (int ell = 0; ell < _Nlambda; ell++)
         {
@@ -447,6 +459,7 @@ void GpuPhotonEngine::finish()
     check(skirt_mcrt_tally_sizes(_ctx, &Nlabs, &Ninstr));
     std::vector<double> tallies(Ninstr);
     check(skirt_mcrt_download(_ctx, nullptr, tallies.data()));
+    if (!handsTallies()) return;  // rank 0 holds the device-summed tallies (sumOnDevices)
     // per instrument [slot][ell][pixel] frames, then [slot][ell] SEDs (skirt_mcrt.h); the FullInstrument
     // slots are trav, strdir, strsca, dusdir, dussca and the scattering levels (FullInstrument.cpp:107-174)
     const double* t = tallies.data();

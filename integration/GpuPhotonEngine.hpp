@@ -63,6 +63,12 @@ public:
     // After the last phase: the instrument tallies of all phases into the instruments' detector arrays
     // (summed over the processes later by Instrument::sumResults, in InstrumentSystem::write)
     void finish();
+    // Optional, before the first phase: the cross-process sums on the GPUs instead of in MPI. ncclComm is
+    // this process's RCCL communicator over the job's ranks (an ncclComm_t, e.g. from ncclCommInitRank with
+    // the unique id broadcast over the reference's own ProcessCommunicator). Every phase's tallies are then
+    // all-reduced over xGMI at the phase end (skirt_rccl_reducer, include/skirt_host.h), and only rank 0
+    // hands them to the items: the reference's sumResults still runs and adds the other ranks' zeros.
+    void sumOnDevices(void* ncclComm, int rank);
 
 private:
     void check(int rc) const;
@@ -72,6 +78,7 @@ private:
     void describeInstruments();
     void uploadCellSources(const Array& Labsbolv);
     void runPhase(int phase, uint32_t cycle, uint64_t Npp, uint64_t seed, int rank, int size);
+    bool handsTallies() const { return !_rccl || _sumRank == 0; }
 
     WavelengthGrid* _lambdagrid;
     StellarSystem* _ss;
@@ -79,6 +86,8 @@ private:
     InstrumentSystem* _is;
     SkirtMcrt* _ctx{nullptr};
     SkirtVoronoi* _voronoi{nullptr};
+    struct SkirtRccl* _rccl{nullptr};  // sumOnDevices
+    int _sumRank{0};
     SkirtPhaseParams _params{};
     int _Nlambda{0};
     int _Ncells{0};

@@ -31,7 +31,7 @@ g++ -std=c++14 -fPIC -O1 -Wall -Wno-deprecated-declarations -DQT_CORE_LIB -DQT_N
     -I"$QT" -I"$QT/QtCore" \
     -c "$HERE/GpuPhotonEngine.cpp" -o "$WORK/GpuPhotonEngine.o"
 echo "compiled $WORK/GpuPhotonEngine.o"
-nm -u "$WORK/GpuPhotonEngine.o" | awk '{print $2}' | grep -E '^skirt_(mcrt|host|sim)_' | sort -u > "$WORK/needed.txt"
+nm -u "$WORK/GpuPhotonEngine.o" | awk '{print $2}' | grep -E '^skirt_(mcrt|host|sim|rccl)_' | sort -u > "$WORK/needed.txt"
 nm -D --defined-only "$REPO/skirt_amd/libskirt_amd.so" | awk '{print $3}' | sort -u > "$WORK/exported.txt"
 missing=$(comm -23 "$WORK/needed.txt" "$WORK/exported.txt")
 if [ -n "$missing" ]; then echo "symbols missing from libskirt_amd.so: $missing"; exit 1; fi
