@@ -319,24 +319,9 @@ constexpr int kBinCellBits = 23;
 constexpr unsigned kBinCellMask = (1u << kBinCellBits) - 1u;
 constexpr int kMaxBinMapLevel = 7;
 
-// Morton index of finest-level cell (x, y, z), 10 bits per axis: a ray's consecutive lookups mostly
-// hit the same or a neighbouring 2x2x2 block, i.e. the same 128-byte line
-__host__ __device__ __forceinline__ unsigned spread3(unsigned v) {
-    v &= 0x3ffu;
-    v = (v | (v << 16)) & 0x030000FFu;
-    v = (v | (v << 8)) & 0x0300F00Fu;
-    v = (v | (v << 4)) & 0x030C30C3u;
-    v = (v | (v << 2)) & 0x09249249u;
-    return v;
-}
-__host__ __device__ __forceinline__ unsigned morton3(unsigned x, unsigned y, unsigned z) {
-    return spread3(x) | (spread3(y) << 1) | (spread3(z) << 2);
-}
-
 // Leaf map order of the finest-level cells of an N^3 map (N = 2^L): 2x2x2 bricks of 8 consecutive
 // 16-byte entries (one 128-byte line), the bricks in (x, y, z) row-major order. Per line the same
 // neighbourhood as Morton order, at a few integer operations instead of three bit spreads per step.
-// (SKIRT_LEAF_MORTON: full Morton order.)
 __host__ __device__ __forceinline__ unsigned leafBricks(int N) { return (unsigned)((N + 1) >> 1); }
 __host__ __device__ __forceinline__ unsigned leafIndex(int N, unsigned x, unsigned y, unsigned z) {
     const unsigned nb = leafBricks(N);
@@ -455,7 +440,7 @@ struct Ray {
     int ci, cj, ck;        // Cartesian cell indices | octree: node, cell number, leaf size in finest cells
     int jx, jy, jz;        // octree leaf map: finest-level index of the current leaf's lower corner
     int4 pre;              // octree leaf map: the next step's leaf-map entry, requested at the end of this step
-    int pfx, pfy, pfz;     //   and the finest-level cell it was requested for (SKIRT_LEAF_PREFETCH)
+    int pfx, pfy, pfz;     //   and the finest-level cell it was requested for (LeafMapGrid::prefetch)
     int idx, ell;
     unsigned flags, mode;
     unsigned id;           // queue index of the ray (a PEEL ray writes its optical depth back there)
@@ -953,8 +938,11 @@ struct LeafMapGrid {
         z = r.z + (ds + a.eps) * r.dz;
     }
 
-    // requests the leaf-map entry of the estimated finest cell of the next exit point (SKIRT_LEAF_PREFETCH):
-    // issued at the end of a step, it is in flight during the wave's Labs drain and the next step's segment
+    // requests the leaf-map entry of the estimated finest cell of the next exit point: issued at the end of a
+    // step, before the wave's Labs drain, it is in flight during the drain and the next step's segment. A load
+    // waits for every older vector-memory operation of its wave (vmcnt counts in issue order, atomics
+    // included, and a no-return f64 atomic stays counted for thousands of cycles under load): requested
+    // after the drain, each step's entry would wait for the previous step's Labs atomic too.
     __device__ static __forceinline__ void prefetch(const Args& a, Ray& r) {
         double ds, x, y, z;
         int wall;
