@@ -15,6 +15,10 @@
 
 #include "../../../include/skirt_host.h"
 
+namespace skirt {
+void setSimError(const std::string& msg);  // sim.cpp
+}
+
 struct SkirtRccl {
     std::vector<ncclComm_t> comms;
     bool owned = true;
@@ -75,7 +79,10 @@ int skirt_sim_run_devices(const char* ski, const char* datadir, int ndev, double
     for (int d = 0; d < ndev; d++) devs[d] = d;
     SkirtRccl* rccl = nullptr;
     int rc = skirt_rccl_create(ndev, devs.data(), &rccl);
-    if (rc) return rc;
+    if (rc) {
+        skirt::setSimError("ncclCommInitAll over " + std::to_string(ndev) + " devices failed");
+        return rc;
+    }
     // one model per device: the setup draws are the reference's, so every rank builds the same grid
     std::vector<SkirtSim*> sims(ndev, nullptr);
     std::vector<int> rcs(ndev, SKIRT_OK);
@@ -90,7 +97,8 @@ int skirt_sim_run_devices(const char* ski, const char* datadir, int ndev, double
         for (auto& t : th) t.join();
     }
     const auto t0 = std::chrono::steady_clock::now();
-    for (int d = 0; d < ndev && rc == SKIRT_OK; d++) rc = rcs[d];
+    for (int d = 0; d < ndev && rc == SKIRT_OK; d++)
+        if ((rc = rcs[d])) skirt::setSimError("device " + std::to_string(d) + ": " + errs[d]);
     if (rc == SKIRT_OK) {
         // one host thread per device: the engine's phase loop runs on its thread, and the ranks' all-reduces
         // meet on the devices
@@ -107,7 +115,8 @@ int skirt_sim_run_devices(const char* ski, const char* datadir, int ndev, double
                 if (r) errs[d] = skirt_sim_error();
             });
         for (auto& t : th) t.join();
-        for (int d = 0; d < ndev && rc == SKIRT_OK; d++) rc = rcs[d];
+        for (int d = 0; d < ndev && rc == SKIRT_OK; d++)
+            if ((rc = rcs[d])) skirt::setSimError("device " + std::to_string(d) + ": " + errs[d]);
     }
     if (seconds) *seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     if (rc == SKIRT_OK && stats) rc = skirt_mcrt_stats(skirt_sim_engine(sims[0]), stats);

@@ -69,9 +69,16 @@ int check(SkirtSim* s, int rc) {
 }
 }  // namespace
 
+namespace skirt {
+// the calling thread's skirt_sim_error message (rccl_reducer.cpp: a device thread's failure, reported on
+// the caller's thread)
+void setSimError(const std::string& msg) { g_err = msg; }
+}  // namespace skirt
+
 extern "C" {
 
 const char* skirt_sim_error(void) { return g_err.c_str(); }
+
 
 namespace {
 // SkirtGeometry parameters as SkirtSourceDesc::geom_param lays them out; returns the SKIRT_GEOM_* kind
