@@ -1164,16 +1164,18 @@ struct Grid<SKIRT_GRID_VORONOI> {
         const float inv = __builtin_amdgcn_rcpf(den);
         const float sa = num * inv;
         const float err = fmaf(fmaf(fabsf(sa), s.eA2, s.eB2), inv, fabsf(sa) * kVorEpsF);
-        // den > 2 eA: the sign of n.k and the interval [sa - err, sa + err] are certain (an interval at or
-        // below 0: no exit); den <= -eA: moving away for certain; otherwise (den = 0 included: m = 0 is a
+        // den > 2 eA: the sign of n.k and the interval [sa - err, sa + err] are certain; den <= -eA: moving away for certain; otherwise (den = 0 included: m = 0 is a
         // degenerate wall) the sign is uncertain: lo = -FLT_MAX. Entries past the count (`valid`), and the
         // NaN padding after a cell's list (den NaN, so neither sure nor maybe): no exit. ucand: the upper
         // bound of a certain exit (lo > 0), else FLT_MAX. Selected as floats, no bool temporaries.
         const float lov = sa - err, hiv = sa + err;
         const bool sure = valid && den > s.eA2;
         const bool maybe = valid && den > -s.eA;
-        const float loSure = hiv > 0.f ? lov : FLT_MAX;
-        lo = sure ? loSure : (maybe ? -FLT_MAX : FLT_MAX);
+        // (a sure interval wholly behind the ray, hiv <= 0, stays a possible exit, which the exact evaluation
+        // would drop: inside the cell no plane the ray moves towards lies behind it, so this happens at
+        // rounding level only -- tools/vor_compact_check.cpp, mode r: the same 297 exact re-evaluations in
+        // 1,004,001 steps with and without the check; C4 +0.7 %, profiles/r05_vor_behind_ab.txt)
+        lo = sure ? lov : (maybe ? -FLT_MAX : FLT_MAX);
         ucand = (sure && lov > 0.f) ? hiv : FLT_MAX;
     }
 

@@ -179,8 +179,9 @@ static int compactStepF(const Mesh& M, int m, const double r[3], const double k[
             const float lov = sa - err, hiv = sa + err;
             const bool sure = den > 2.0f * eA;
             const bool maybe = den > -eA;  // (den = 0 for a degenerate wall's m = 0: uncertain)
-            const float loSure = hiv > 0.f ? lov : FLT_MAX;
-            const float lo = sure ? loSure : (maybe ? -FLT_MAX : FLT_MAX);
+            // (an interval wholly behind the ray, hiv <= 0, stays a possible exit: the exact evaluation drops it;
+            // inside the cell a plane ahead of the ray is never behind it, so it happens only at rounding level)
+            const float lo = sure ? lov : (maybe ? -FLT_MAX : FLT_MAX);
             const float ucand = (sure && lov > 0.f) ? hiv : FLT_MAX;
             gLo[q - g.cell_nbr_offset[m]] = lo;
             U = fminf(U, ucand);
