@@ -4295,9 +4295,10 @@ static int runPhase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, uint6
         tgrid = std::max(1, c->nCusT) * per;
         c->traceBlocksPerCU = per;
     }
-    // event kernel blocks per CU. Voronoi: 3, since its event kernel fits 3 waves/SIMD (C4 +0.6 %,
-    // profiles/r04_event_bpc_sweep.txt); the others are within the spread at 2-4
-    const int ebpc = kind == SKIRT_GRID_VORONOI ? 3 : 2;
+    // event kernel blocks per CU: 3 (3 waves/SIMD, the registers allow it). Voronoi: C4 +0.6 % against 2
+    // (profiles/r04_event_bpc_sweep.txt); the other grids, once the block reservations no longer serialize on
+    // one counter line: C3 +0.7 %, C2 +2.3 % against 2, 4 the same as 3 (profiles/r05_event_bpc_ab.txt)
+    const int ebpc = 3;
     const int egrid = std::max(1, std::min((slots + kBlock - 1) / kBlock, std::max(1, c->nCusE) * ebpc));
     const int dgrid = std::max(1, std::max(1, c->nCusE) * 4);
 
