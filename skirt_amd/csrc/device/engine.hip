@@ -4168,8 +4168,8 @@ static int runPhase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, uint6
     const bool forked = c->halves > 1 || c->cusT || c->cusE;  // the pipeline runs on the owned streams
     // the detect kernel of an iteration beside the next iteration's event kernel (one pipeline on the
     // caller's stream, peel-offs at the interaction points): C3 +1.9 %, C2 within the spread; beside the
-    // next trace kernel as well, C3 +1.6 %, C2 -1.5 %. Not for Voronoi grids, whose event kernel runs 3
-    // waves per SIMD: C4 -2.2 % (profiles/r05_detect_aside_ab.txt)
+    // next trace kernel as well, C3 +1.6 %, C2 -1.5 %. Not for Voronoi grids: C4 -2.2 %, and -2.6 % again
+    // after the counter-line and event-grid changes (profiles/r05_detect_aside_ab.txt)
     const bool detAside = !forked && !continuous && !c->instr.empty() && p->has_dust &&
                           c->gridKind != SKIRT_GRID_VORONOI;
     if ((rc = ensurePool(c, slots, continuous, halves, detAside))) return rc;
