@@ -447,6 +447,8 @@ struct Ray {
     int jx, jy, jz;        // octree leaf map: finest-level index of the current leaf's lower corner
     int4 pre;              // octree leaf map: the next step's leaf-map entry, requested at the end of this step
     int pfx, pfy, pfz;     //   and the finest-level cell it was requested for (LeafMapGrid::prefetch)
+    double ex, ey, ez, eds;  // octree leaf map: the current leaf's exit point and distance, and its wall,
+    int ewall;               //   computed once by prefetch for the next step
     int idx, ell;
     unsigned flags, mode;
     unsigned id;           // queue index of the ray (a PEEL ray writes its optical depth back there)
@@ -950,13 +952,11 @@ struct LeafMapGrid {
     // included, and a no-return f64 atomic stays counted for thousands of cycles under load): requested
     // after the drain, each step's entry would wait for the previous step's Labs atomic too.
     __device__ static __forceinline__ void prefetch(const Args& a, Ray& r) {
-        double ds, x, y, z;
-        int wall;
-        exitPoint(a, r, ds, wall, x, y, z);
+        exitPoint(a, r, r.eds, r.ewall, r.ex, r.ey, r.ez);  // (kept for the step: the ray does not move before it)
         const int N = a.mapN;
-        r.pfx = estimate(N, a.mapX0, a.mapInvX, x);
-        r.pfy = estimate(N, a.mapY0, a.mapInvY, y);
-        r.pfz = estimate(N, a.mapZ0, a.mapInvZ, z);
+        r.pfx = estimate(N, a.mapX0, a.mapInvX, r.ex);
+        r.pfy = estimate(N, a.mapY0, a.mapInvY, r.ey);
+        r.pfz = estimate(N, a.mapZ0, a.mapInvZ, r.ez);
         r.pre = *reinterpret_cast<const int4*>(a.leafMap + leafIndex(N, r.pfx, r.pfy, r.pfz));
     }
 
@@ -966,9 +966,11 @@ struct LeafMapGrid {
         const double* tx = sh.mesh;
         const double* ty = tx + N1;
         const double* tz = ty + N1;
-        double ds, x, y, z;
-        int wall;
-        exitPoint(a, r, ds, wall, x, y, z);
+        // the exit point prefetch computed at the end of the last step (or at the grid entry): 139 -> 129 VGPRs,
+        // C3 within the spread, C5 +0.5 % (profiles/r05_exit_reuse_ab.txt)
+        const double ds = r.eds;
+        double x = r.ex, y = r.ey, z = r.ez;
+        const int wall = r.ewall;
         // the next leaf's entry is requested first; the segment's own work (optical depth, absorption)
         // runs while the load is in flight
         // the entry of the estimated finest cell; its leaf is the right one when the leaf's own faces
