@@ -3014,6 +3014,7 @@ struct SkirtMcrt {
     int traceBlocksPerCU = 0;  // the occupancy the last trace launch was sized for
     int lastDetCopies = 0;  // SED copies of the last run's detect kernel
     double lastMs = 0;
+    bool phaseTimed = false;  // ev0/ev1 recorded by the last phase (an empty slice records nothing)
     std::vector<hipEvent_t> traceEv;  // pairs around the trace launches not yet timed
     int traceLaunches = 0;
     uint64_t packagesTotal = 0;       // packet indices of the phases run since the last zero_tallies (SkirtStats::packages)
@@ -4128,6 +4129,7 @@ static int runPhase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, uint6
     if (rc) return rc;
     if (phase == SKIRT_PHASE_DUST_SELFABS && (rc = ensureDustLabs(c))) return rc;
     c->lastMs = 0;
+    c->phaseTimed = false;
     c->lastIterations = 0;
     if (c->traceLaunches) {  // time the previous call's launches before their events are reused
         HIPCHECK(c, hipStreamSynchronize(c->stream));
@@ -4473,6 +4475,7 @@ static int runPhase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, uint6
         }
     }
     HIPCHECK(c, hipEventRecord(c->ev1, c->stream));
+    c->phaseTimed = true;
     return SKIRT_OK;
 }
 
@@ -4481,7 +4484,9 @@ int skirt_mcrt_synchronize(SkirtMcrt* c) {
     HIPCHECK(c, hipSetDevice(c->device));
     HIPCHECK(c, hipStreamSynchronize(c->stream));
     float ms = 0;
-    if (hipEventElapsedTime(&ms, c->ev0, c->ev1) == hipSuccess) c->lastMs = ms;
+    // only events this phase recorded: an elapsed time over unrecorded ones fails, and the failure would stay
+    // behind as the thread's last error for the next launch check of any engine on this thread
+    if (c->phaseTimed && hipEventElapsedTime(&ms, c->ev0, c->ev1) == hipSuccess) c->lastMs = ms;
     for (int k = 0; k < c->traceLaunches; k++)
         if (hipEventElapsedTime(&ms, c->traceEv[2 * k], c->traceEv[2 * k + 1]) == hipSuccess) c->traceMs += ms;
     c->traceLaunchesTotal += (uint64_t)c->traceLaunches;

@@ -11,6 +11,7 @@
    from several engine runs with independent seeds (sqrt(N) Monte Carlo tolerance).
 """
 import os
+import re
 
 import numpy as np
 import pytest
@@ -197,6 +198,54 @@ def test_sharded_packet_ranges_sum_to_the_whole():
     ff, sf = full.instrument(0)
     np.testing.assert_allclose(sa + sb, sf, rtol=1e-12)
     np.testing.assert_allclose(fa + fb, ff, rtol=1e-12, atol=1e-300)
+
+
+@pytest.mark.parametrize("name,mix", [("c1_oligo16", "OligoDustSystem"), ("pan_cart16", "PanDustSystem")])
+def test_dust_free_models_match_oracle_same_streams(tmp_path, name, mix):
+    """A simulation without a dust system (MonteCarloSimulation.cpp:265-301 with _ds null): every packet is
+    launched, detected unattenuated by every instrument and ends in the event kernel (no trace kernel, no
+    Labs). Engine = oracle on the same Philox streams."""
+    text = open(ski(name)).read()
+    text, n = re.subn(r'\s*<dustSystem type="%s">.*?</dustSystem>' % mix, "", text, flags=re.S)
+    assert n == 1
+    path = str(tmp_path / (name + "_nodust.ski"))
+    with open(path, "w") as f:
+        f.write(text)
+    packages = 2000
+    sim = S.Simulation(path, packages=packages)
+    assert sim.info.has_dust == 0
+    sim.attach(0)
+    sim.run_stellar()
+    sim.run_dust()
+    sim.fetch()
+    orc = O.run(path, rng=O.RNG_PHILOX, threads=16, packages=packages, phases=O.PHASES_ALL)
+    st = sim.stats()
+    assert st["packets"] == orc.packets > 0
+    assert st["segments_fill"] == st["segments_walk"] == st["segments_peel"] == 0
+    frames, seds = sim.instrument(0)
+    np.testing.assert_allclose(seds, orc.seds[0], rtol=1e-12, atol=1e-300)
+    if frames is not None:
+        np.testing.assert_allclose(frames, orc.frames[0], rtol=1e-12, atol=1e-300)
+
+
+def test_more_ranks_than_packets_per_wavelength():
+    """Ragged shards: 7 ranks over 3 packets per wavelength, so four ranks shoot nothing. Every rank runs its
+    (possibly empty) slice of every wavelength without error, and the slices add up to the whole."""
+    name = "pan_oct"
+    full = run_gpu(name, packages=3)
+    parts = []
+    for rank in range(7):
+        sim = S.Simulation(ski(name), packages=3)
+        sim.attach(0)
+        sim.set_reducer(lambda tally, ptr, n, stream: None)  # one process: the test sums
+        sim.run_stellar_shard(rank, 7)
+        sim.fetch()
+        parts.append(sim)
+    counts = [p.stats()["packets"] for p in parts]
+    assert sum(counts) == full.stats()["packets"] and counts.count(0) >= 4, counts
+    np.testing.assert_allclose(sum(p.labs() for p in parts), full.labs(), rtol=1e-12, atol=1e-300)
+    np.testing.assert_allclose(sum(p.instrument(0)[1] for p in parts), full.instrument(0)[1], rtol=1e-12,
+                               atol=1e-300)
 
 
 def test_wavelength_shards_sum_to_the_whole():
