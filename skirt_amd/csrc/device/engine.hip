@@ -191,6 +191,8 @@ __device__ __forceinline__ void vorEntries(const VorEntry* B, int q0, VorEntry (
 }
 // Voronoi walk: entries per load group, even (pairs); with exp(-tau) per FILL segment 4 is best (C4 7.30e7;
 // 6: 7.26e7 with 28 B/lane spilled; one group of 8: 7.25e7; profiles/r03_vor_pipe.txt, r03_exact_attenuation.txt)
+// FILL segments: exp(-tau) carried as a product while the segments' optical depths stay below this
+constexpr double kCarryTau = 0.5;
 constexpr int kVorUnroll = 4;
 // groups of entries in flight per step: loaded with the header, each reloaded once consumed. 3: C4 trace
 // launch 23.64 -> 23.19 ms, 9.64e7 -> 9.89e7 pkt/s, profiles/r04_ktrace_groups_nolicm.txt; 4 with each
@@ -1489,19 +1491,21 @@ struct Tracer {
                 atomicOr(a.error, ERR_PATH_CAP);
             }
         }
-        const double taustart = r.tau;
         r.s += ds;
         r.tau += dtau;
         nseg++;
         if (r.mode == RAY_FILL) {
             if (m >= 0 && (!ONECOMP || a.store)) {
-                // L_abs = (1-albedo) L exp(-tau_{n-1}) (1 - exp(-dtau_n)) (MonteCarloSimulation.cpp:458-462),
-                // in the reference's operation order. (Rounds 1-3 carried exp(-tau_{n-1}) as the running
-                // product of 1 - (1 - exp(-dtau)), exact only to about 1e-16 / exp(-dtau) relative behind an
-                // optically thick segment: the deep-cell differences of the thick pan_oct_sa models. With
-                // the Labs adds leaving one instruction per step, exp fits the octree walk's registers.)
+                // L_abs = (1-albedo) L exp(-tau_{n-1}) (1 - exp(-dtau_n)) (MonteCarloSimulation.cpp:458-462).
+                // exp(-tau) is carried in f1 as the running product of exp(-dtau) = 1 - ef, which is exact to
+                // about an ulp per segment while ef <= 1 - exp(-kCarryTau); behind a thicker segment (where
+                // 1 - ef loses digits: rounds 1-3 carried it unconditionally and the thick pan_oct_sa models'
+                // deep cells drifted) it is evaluated anew. One f64 exp less per segment: C2 +0.6 %, C5 +0.5 %,
+                // C3 within the spread (profiles/r05_exp_carry_ab.txt)
                 const double ef = -expm1(-dtau);
-                const double Lintm = r.param * exp(-taustart) * ef;
+                const double Lintm = r.param * r.f1 * ef;
+                if (dtau < kCarryTau) r.f1 -= r.f1 * ef;
+                else r.f1 = exp(-r.tau);
                 double albedo;
                 if (ONECOMP) albedo = sh.alb[r.ell];
                 else {
