@@ -94,6 +94,13 @@ void skirt_sim_free(SkirtSim* sim);
  * of a SkirtGridDesc, valid while the SkirtVoronoi lives. */
 typedef struct SkirtVoronoi SkirtVoronoi;
 SkirtVoronoi* skirt_host_voronoi_build(const double* sites, int nsites, const double extent[6]);
+/* As skirt_host_voronoi_build, with the cells computed on HIP device `device` (skirt_mcrt_voronoi_cells) and
+ * the ones outgrowing its capacities on the host (*host_cells of them, if host_cells is not NULL); device < 0:
+ * every cell on the host. The tessellation is the host build's, bit for bit, either way. */
+SkirtVoronoi* skirt_host_voronoi_build_ex(const double* sites, int nsites, const double extent[6], int device,
+                                          int* host_cells);
+/* copies the cells' volumes (ncells) and centroids (3 per cell); either pointer may be NULL */
+int skirt_host_voronoi_cells(const SkirtVoronoi* v, double* volume, double* centroid);
 int skirt_host_voronoi_describe(const SkirtVoronoi* v, SkirtGridDesc* grid);
 void skirt_host_voronoi_free(SkirtVoronoi* v);
 

@@ -34,7 +34,8 @@
 extern "C" {
 #endif
 
-#define SKIRT_MCRT_ABI_VERSION 13  /* 11: SkirtStats::packages; 12: SkirtStats::labs_cache_sets; 13: without it */
+#define SKIRT_MCRT_ABI_VERSION 14  /* 11: SkirtStats::packages; 12: SkirtStats::labs_cache_sets; 13: without it;
+                                     14: skirt_mcrt_voronoi_cells */
 
 enum {
     SKIRT_OK = 0,
@@ -292,6 +293,23 @@ typedef struct {
 } SkirtDensityDesc;
 int skirt_mcrt_sample_density(int device, const SkirtDensityDesc* dens, const double* boxes, size_t n,
                               const uint32_t* words, int nsample, int mode, double* out);
+
+/* The cells of a Voronoi tessellation on HIP device `device` (setup, §8(f)2; the reference computes them with
+ * Voro++, VoronoiMesh.cpp:310-376): the host construction of skirt_host_voronoi_build (the domain box clipped
+ * by the bisector planes of the nearest sites, nearest first, until no farther site can cut it), one cell per
+ * thread in the same f64 operations, so every output equals the host's bit for bit. `extent` = {xmin, ymin,
+ * zmin, xmax, ymax, zmax}; `nodes`/`perm`: the k-d tree over the sites whose nearest-site queries the cells
+ * use (leaves hold perm[lo..hi), children after their parent). Outputs per site i: its sorted distinct
+ * neighbour ids (walls -1..-6) at ids[i * max_ids], their count nids[i] (-1: the cell outgrew the device's
+ * fixed capacities; the caller builds it), bbox[6 i ..] (min xyz, max xyz of its vertices), volume[i],
+ * centroid[3 i ..]. Synchronous. */
+typedef struct {
+    int lo, hi, left, right, dim; /* left < 0: a leaf */
+    double split, bmin[3], bmax[3];
+} SkirtKdNode;
+int skirt_mcrt_voronoi_cells(int device, const double* sites, int nsites, const double extent[6],
+                             const SkirtKdNode* nodes, int nnodes, const int* perm, int max_ids, int* ids, int* nids,
+                             double* bbox, double* volume, double* centroid);
 
 /* Copies tallies to host (Labs converted to row-major cell x wavelength); either pointer may be NULL.
  * With a reducer set, the instrument tallies are summed over the processes first. */

@@ -18,7 +18,7 @@ import os
 import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
-ABI_VERSION = 13  # SKIRT_MCRT_ABI_VERSION of include/skirt_mcrt.h
+ABI_VERSION = 14  # SKIRT_MCRT_ABI_VERSION of include/skirt_mcrt.h
 # SKIRT_AMD_LIB selects another build of the same library (e.g. a tuning variant built by
 # tools/build_variant.sh next to the default one)
 LIB_PATH = os.path.join(PKG_DIR, os.environ.get("SKIRT_AMD_LIB", "libskirt_amd.so"))
@@ -71,7 +71,7 @@ ABI_SYMBOLS = [
     "skirt_sim_load_ex", "skirt_mcrt_sample_density", "skirt_sim_density",
     "skirt_mcrt_set_crossed", "skirt_mcrt_download_crossed", "skirt_mcrt_column_densities",
     "skirt_rccl_create", "skirt_rccl_wrap", "skirt_rccl_rank", "skirt_rccl_reducer", "skirt_rccl_destroy",
-    "skirt_sim_run_devices",
+    "skirt_sim_run_devices", "skirt_mcrt_voronoi_cells", "skirt_host_voronoi_build_ex", "skirt_host_voronoi_cells",
 ]
 
 _lib = None

@@ -1342,7 +1342,7 @@ static void buildVoronoiGrid(const Ctx& c, const XmlElement* ge, Model& m, Unifo
         throw std::runtime_error("unsupported Voronoi particle distribution " + dist);
     }
     StageTimer st("tessellation");
-    buildVoronoi(m.grid.vor, sites, xmin, xmax, ymin, ymax, zmin, zmax);
+    buildVoronoi(m.grid.vor, sites, xmin, xmax, ymin, ymax, zmin, zmax, c.sampler ? c.sampler->voronoiCells() : nullptr);
 }
 
 Model loadSki(const std::string& path, UniformSource& rng, const std::string& datadir, DensitySampler* sampler) {

@@ -248,6 +248,8 @@ struct DensitySampler {
     virtual ~DensitySampler() = default;
     virtual void sample(const std::vector<DustComp>& dust, const double* boxes, size_t n, const uint32_t* words,
                         int nsample, int mode, double* out) = 0;
+    // the Voronoi tessellation's cells on the same device (null: on the host)
+    virtual const VoronoiCellsFn* voronoiCells() const { return nullptr; }
 };
 
 // Builds the model from a .ski file; `rng` supplies the setup random numbers (octree subdivision

@@ -1,6 +1,7 @@
 // Host driver: .ski -> Model -> device engine -> outputs (include/skirt_host.h).
 #include <algorithm>
 #include <chrono>
+#include <cstddef>
 #include <cstdio>
 #include <cstdlib>
 #include <cmath>
@@ -99,10 +100,31 @@ int packGeometry(const Geometry& g, double* p) {
 static_assert((int)kDensComponents == (int)SKIRT_DENS_COMPONENTS && (int)kDensNode == (int)SKIRT_DENS_NODE,
               "density sampling modes");
 
-// the setup's density sampling on a HIP device through skirt_mcrt_sample_density
+static_assert(sizeof(KdNode) == sizeof(SkirtKdNode) && offsetof(KdNode, split) == offsetof(SkirtKdNode, split) &&
+                  offsetof(KdNode, bmax) == offsetof(SkirtKdNode, bmax),
+              "the host k-d tree node is the C ABI's SkirtKdNode");
+
+// a Voronoi tessellation's cells on a HIP device through skirt_mcrt_voronoi_cells
+VoronoiCellsFn deviceVoronoiCells(int device) {
+    return [device](const std::vector<double>& sites, const double box[6], const std::vector<KdNode>& nodes,
+                    const std::vector<int>& perm, int maxIds, int* ids, int* nids, double* bbox, double* volume,
+                    double* centroid) {
+        const int rc = skirt_mcrt_voronoi_cells(device, sites.data(), (int)(sites.size() / 3), box,
+                                                reinterpret_cast<const SkirtKdNode*>(nodes.data()), (int)nodes.size(),
+                                                perm.data(), maxIds, ids, nids, bbox, volume, centroid);
+        if (rc)
+            throw std::runtime_error("Voronoi cells on device " + std::to_string(device) + " failed (error " +
+                                     std::to_string(rc) + ")");
+    };
+}
+
+// the setup's density sampling (and a Voronoi grid's cells) on a HIP device through
+// skirt_mcrt_sample_density (skirt_mcrt_voronoi_cells)
 struct DeviceDensitySampler final : DensitySampler {
     int device;
-    explicit DeviceDensitySampler(int d) : device(d) {}
+    VoronoiCellsFn cells;
+    explicit DeviceDensitySampler(int d) : device(d), cells(deviceVoronoiCells(d)) {}
+    const VoronoiCellsFn* voronoiCells() const override { return &cells; }
     void sample(const std::vector<DustComp>& dust, const double* boxes, size_t n, const uint32_t* words, int nsample,
                 int mode, double* out) override {
         const int nc = (int)dust.size();
@@ -511,6 +533,11 @@ struct SkirtVoronoi {
 };
 
 SkirtVoronoi* skirt_host_voronoi_build(const double* sites, int nsites, const double extent[6]) {
+    return skirt_host_voronoi_build_ex(sites, nsites, extent, -1, nullptr);
+}
+
+SkirtVoronoi* skirt_host_voronoi_build_ex(const double* sites, int nsites, const double extent[6], int device,
+                                          int* host_cells) {
     if (!sites || nsites < 1 || !extent) {
         g_err = "skirt_host_voronoi_build: no sites or no extent";
         return nullptr;
@@ -518,12 +545,21 @@ SkirtVoronoi* skirt_host_voronoi_build(const double* sites, int nsites, const do
     try {
         auto v = std::make_unique<SkirtVoronoi>();
         std::vector<double> sv(sites, sites + 3 * (size_t)nsites);
-        buildVoronoi(v->g, sv, extent[0], extent[3], extent[1], extent[4], extent[2], extent[5]);
+        const VoronoiCellsFn dev = device >= 0 ? deviceVoronoiCells(device) : VoronoiCellsFn();
+        buildVoronoi(v->g, sv, extent[0], extent[3], extent[1], extent[4], extent[2], extent[5],
+                     device >= 0 ? &dev : nullptr, host_cells);
         return v.release();
     } catch (std::exception& e) {
         g_err = e.what();
         return nullptr;
     }
+}
+
+int skirt_host_voronoi_cells(const SkirtVoronoi* v, double* volume, double* centroid) {
+    if (!v) return SKIRT_ERR_ARG;
+    if (volume) std::copy(v->g.volume.begin(), v->g.volume.end(), volume);
+    if (centroid) std::copy(v->g.centroid.begin(), v->g.centroid.end(), centroid);
+    return SKIRT_OK;
 }
 
 int skirt_host_voronoi_describe(const SkirtVoronoi* v, SkirtGridDesc* g) {

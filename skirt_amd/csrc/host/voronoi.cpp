@@ -7,6 +7,9 @@
 #include <cmath>
 #include <cstdint>
 #include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <stdexcept>
 #include <string>
 #include <thread>
@@ -154,11 +157,11 @@ public:
         std::sort_heap(out.begin(), out.end(), worse);
     }
 
+    const std::vector<KdNode>& nodes() const { return nodes_; }
+    const std::vector<int>& perm() const { return idx_; }
+
 private:
-    struct Node {
-        int lo, hi, left = -1, right = -1, dim = 0;
-        double split = 0, bmin[3], bmax[3];
-    };
+    using Node = KdNode;
     const std::vector<double>& site_;
     std::vector<int> idx_;
     std::vector<Node> nodes_;
@@ -174,8 +177,8 @@ private:
 
     int build(int lo, int hi) {
         const int me = (int)nodes_.size();
-        nodes_.push_back(Node{lo, hi});
-        Node nd{lo, hi};
+        nodes_.push_back(Node{lo, hi, -1, -1, 0, 0.0, {}, {}});
+        Node nd{lo, hi, -1, -1, 0, 0.0, {}, {}};
         for (int q = 0; q < 3; q++) { nd.bmin[q] = DBL_MAX; nd.bmax[q] = -DBL_MAX; }
         for (int t = lo; t < hi; t++)
             for (int q = 0; q < 3; q++) {
@@ -239,7 +242,7 @@ bool VoronoiGrid::isPointClosestTo(double x, double y, double z, int m) const {
 }
 
 void buildVoronoi(VoronoiGrid& g, const std::vector<double>& sites, double xmin, double xmax, double ymin, double ymax,
-                  double zmin, double zmax) {
+                  double zmin, double zmax, const VoronoiCellsFn* cells, int* hostCells) {
     g.xmin = xmin; g.xmax = xmax; g.ymin = ymin; g.ymax = ymax; g.zmin = zmin; g.zmax = zmax;
     const double wx = xmax - xmin, wy = ymax - ymin, wz = zmax - zmin;
     const double L = std::sqrt(wx * wx + wy * wy + wz * wz);
@@ -248,9 +251,19 @@ void buildVoronoi(VoronoiGrid& g, const std::vector<double>& sites, double xmin,
     const int N = g.ncells();
     if (N < 1) throw std::runtime_error("a Voronoi grid needs sites");
 
+    // SKIRT_AMD_SETUP_TIMES: the stages' wall times
+    static const bool timing = std::getenv("SKIRT_AMD_SETUP_TIMES") != nullptr;
+    auto t0 = std::chrono::steady_clock::now();
+    auto stage = [&](const char* what) {
+        if (!timing) return;
+        const auto t1 = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "[setup] voronoi %-18s %.3f s\n", what, std::chrono::duration<double>(t1 - t0).count());
+        t0 = t1;
+    };
     // candidate neighbours come nearest first from a k-d tree over the sites (the sites of a
     // DustDensity grid cluster by orders of magnitude, which a uniform bucket grid cannot follow)
     const SiteTree tree(sites);
+    stage("k-d tree");
     g.bbox.assign(6 * (size_t)N, 0);
     g.volume.assign(N, 0);
     g.centroid.assign(3 * (size_t)N, 0);
@@ -309,8 +322,30 @@ void buildVoronoi(VoronoiGrid& g, const std::vector<double>& sites, double xmin,
         g.centroid[3 * (size_t)i + 1] = vol > 0 ? cy / vol : s[1];
         g.centroid[3 * (size_t)i + 2] = vol > 0 ? cz / vol : s[2];
     };
+    // the cells on the device first (where they fit its capacities); the host builds the rest
+    std::vector<int> todo;
+    if (cells) {
+        constexpr int kIds = 96;  // neighbour ids per cell the device returns
+        std::vector<int> ids((size_t)N * kIds), nids(N);
+        const double box[6] = {xmin, ymin, zmin, xmax, ymax, zmax};
+        (*cells)(sites, box, tree.nodes(), tree.perm(), kIds, ids.data(), nids.data(), g.bbox.data(), g.volume.data(),
+                 g.centroid.data());
+        for (int i = 0; i < N; i++) {
+            if (nids[i] < 0 || nids[i] > kIds) {
+                todo.push_back(i);
+                continue;
+            }
+            cellIds[i].assign(ids.begin() + (size_t)i * kIds, ids.begin() + (size_t)i * kIds + nids[i]);
+        }
+    } else {
+        todo.resize(N);
+        for (int i = 0; i < N; i++) todo[i] = i;
+    }
+    if (cells) stage("device cells");
+    if (hostCells) *hostCells = (int)todo.size();
     {
         const int T = std::max(1, std::min(16, (int)std::thread::hardware_concurrency()));
+        const int NT = (int)todo.size();
         std::atomic<int> next{0};
         std::vector<std::thread> th;
         std::vector<std::string> errs(T);
@@ -318,8 +353,8 @@ void buildVoronoi(VoronoiGrid& g, const std::vector<double>& sites, double xmin,
             th.emplace_back([&, w] {
                 try {
                     std::vector<std::pair<double, int>> cand;
-                    for (int c0; (c0 = next.fetch_add(64)) < N;)
-                        for (int i = c0; i < std::min(N, c0 + 64); i++) buildCell(i, cand);
+                    for (int c0; (c0 = next.fetch_add(64)) < NT;)
+                        for (int q = c0; q < std::min(NT, c0 + 64); q++) buildCell(todo[q], cand);
                 } catch (std::exception& e) {
                     errs[w] = e.what();
                 }
@@ -328,6 +363,7 @@ void buildVoronoi(VoronoiGrid& g, const std::vector<double>& sites, double xmin,
         for (auto& e : errs)
             if (!e.empty()) throw std::runtime_error(e);
     }
+    stage("host cells");
     g.nbrOffset.assign(N + 1, 0);
     g.nbrList.clear();
     for (int i = 0; i < N; i++) {
@@ -370,6 +406,7 @@ void buildVoronoi(VoronoiGrid& g, const std::vector<double>& sites, double xmin,
     g.blockList.assign(count[nb3], 0);
     std::vector<int> fill(g.blockOffset.begin(), g.blockOffset.end() - 1);
     slabs([&](size_t b, int m) { g.blockList[fill[b]++] = m; });
+    stage("neighbours, blocks");
 }
 
 void voronoiRandomPosition(const VoronoiGrid& g, UniformSource& rng, int m, double& x, double& y, double& z) {

@@ -6,6 +6,7 @@
 // by the bisector planes of the sites near it, nearest first, until no farther site can cut it.
 #pragma once
 
+#include <functional>
 #include <vector>
 
 namespace skirt {
@@ -35,9 +36,26 @@ struct VoronoiGrid {
     void blockIndices(double x, double y, double z, int& i, int& j, int& k) const;
 };
 
-// builds the tessellation of `sites` (3 per site, all inside the box) in the box
+// A node of the k-d tree over the sites that the cells' nearest-site queries use (leaves of at most 8
+// sites perm[lo .. hi), split at the median of the widest axis; children after their parent)
+struct KdNode {
+    int lo, hi, left, right, dim;
+    double split, bmin[3], bmax[3];
+};
+
+// The cells on another processor (skirt_mcrt_voronoi_cells on a HIP device): from the sites, the box
+// {xmin, ymin, zmin, xmax, ymax, zmax} and the host's k-d tree, per cell its sorted neighbour ids (at most
+// maxIds, at ids[i * maxIds]; nids[i] < 0: not computed, the host builds that cell), bounding box (6),
+// volume and centroid (3), bit for bit as the host computes them. Throws on failure.
+using VoronoiCellsFn = std::function<void(const std::vector<double>& sites, const double box[6],
+                                          const std::vector<KdNode>& nodes, const std::vector<int>& perm, int maxIds,
+                                          int* ids, int* nids, double* bbox, double* volume, double* centroid)>;
+
+// builds the tessellation of `sites` (3 per site, all inside the box) in the box; with `cells`, the cells
+// are computed there (the ones it leaves undone on the host), and *hostCells counts those the host built
 void buildVoronoi(VoronoiGrid& g, const std::vector<double>& sites, double xmin, double xmax, double ymin,
-                  double ymax, double zmin, double zmax);
+                  double ymax, double zmin, double zmax, const VoronoiCellsFn* cells = nullptr,
+                  int* hostCells = nullptr);
 
 // VoronoiMesh::randomPosition: uniform points in the cell's bounding box until one lies in the cell
 void voronoiRandomPosition(const VoronoiGrid& g, UniformSource& rng, int m, double& x, double& y, double& z);

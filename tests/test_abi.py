@@ -32,7 +32,7 @@ def test_library_exports_every_declared_function():
 
 
 def test_abi_version_and_stats_layout():
-    assert S.lib().skirt_mcrt_abi_version() == 13 == S.ABI_VERSION
+    assert S.lib().skirt_mcrt_abi_version() == 14 == S.ABI_VERSION
     assert "#define SKIRT_MCRT_ABI_VERSION %d" % S.ABI_VERSION in open(HEADERS[0]).read()
     text = open(HEADERS[0]).read()
     body = re.search(r"typedef struct \{([^}]*)\} SkirtStats;", text, flags=re.S).group(1)
