@@ -1351,7 +1351,9 @@ struct Grid<SKIRT_GRID_VORONOI> {
         if (!headFrom(a, r, s, L.h0, L.h1, L.h2, seg)) return false;
         // (the next groups are loaded only while the list lasts: loading them unconditionally -- past the list
         // into the next block -- let the compiler drop the register moves at the join, but made C4 24 % slower,
-        // 9.53e7 -> 7.37e7 pkt/s, profiles/r04_ab_c4_vor_uncond_loads_c3c5_prefetch.txt)
+        // 9.53e7 -> 7.37e7 pkt/s, profiles/r04_ab_c4_vor_uncond_loads_c3c5_prefetch.txt; a lane past its list
+        // reading one line that all such lanes share instead: 208 -> 170 register moves, still 5 % slower,
+        // profiles/r05_vor_uncond_shared_ab.txt)
         constexpr int NG = kVorGroups;
         for (int q0 = 0; q0 < s.cnt; q0 += NG * kVorUnroll) {
 #pragma unroll
