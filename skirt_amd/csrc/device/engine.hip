@@ -42,6 +42,7 @@ namespace {
 
 constexpr double kDblMax = 1.7976931348623157e308;
 constexpr int kBlock = 256;
+constexpr int kSegWords = 3 * (kBlock / 64) * 4 / 8;  // the trace kernel's per-wave segment counts, in doubles
 constexpr int kLabsBuf = 16;      // buffered Labs adds per trace lane (LDS)
 constexpr int kStepsPerPull = 4;  // grid steps between two ray pulls of a trace wave
 // The slot pool runs as one or two independent pipelines ("halves", SkirtMcrt::halves): with two, one
@@ -63,6 +64,7 @@ constexpr int kPollRing = 3;       // copies in flight per half (the host reads 
 // path would otherwise take the octree kernel to 175 and 2 waves; C3 1.91e8 -> 2.15e8 pkt/s at 3). The
 // Voronoi walk has its own kernel and attribute below.
 #define SKIRT_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(3)))
+#define SKIRT_NOSTORE_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(4)))
 // the Voronoi trace kernel at 2 waves per SIMD: its branch-free bounds keep several entries in flight
 // and run without spills in 256 VGPRs (C4 5.72e7 pkt/s at 3 waves, 6.08e7 at 2)
 #define SKIRT_VOR_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(2)))
@@ -1399,7 +1401,7 @@ struct Grid<SKIRT_GRID_VORONOI> {
 };
 
 // ================================================================== trace kernel
-template <int GRID, bool ONECOMP, bool CONT>
+template <int GRID, bool ONECOMP, bool CONT, bool STORE>
 struct Tracer {
     const Args& a;
     const Shared& sh;
@@ -1497,7 +1499,7 @@ struct Tracer {
         r.tau += dtau;
         nseg++;
         if (r.mode == RAY_FILL) {
-            if (m >= 0 && (!ONECOMP || a.store)) {
+            if (m >= 0 && (!ONECOMP || (STORE && a.store))) {
                 // L_abs = (1-albedo) L exp(-tau_{n-1}) (1 - exp(-dtau_n)) (MonteCarloSimulation.cpp:458-462).
                 // exp(-tau) is carried in f1 as the running product of exp(-dtau) = 1 - ef, which is exact to
                 // about an ulp per segment while ef <= 1 - exp(-kCarryTau); behind a thicker segment (where
@@ -1519,7 +1521,7 @@ struct Tracer {
                     albedo = (kext > 0.0) ? ksca / kext : 0.0;
                     r.f2 += albedo * Lintm;
                 }
-                if (a.store) {
+                if (STORE && a.store) {
                     pendVal[npend * kBlock + threadIdx.x] = (1.0 - albedo) * Lintm;
                     pendIdx[npend * kBlock + threadIdx.x] = (unsigned)r.ell * (unsigned)a.labsStride + (unsigned)m;
                     npend++;
@@ -1912,7 +1914,9 @@ __global__ void __launch_bounds__(kBlock) buildLeafMapKernel(LeafEntry* map, con
 
 // CONT: continuous scattering (the FILL rays record their dust segments); its own instantiations keep
 // the recording out of the other kernels' registers
-template <int GRID, bool ONECOMP, bool CONT>
+// STORE false: a phase that stores no absorption (a.store = 0), one dust component, no continuous
+// scattering: no Labs buffers and no drain (its own instantiation, traceKernelNoStore)
+template <int GRID, bool ONECOMP, bool CONT, bool STORE>
 __device__ __forceinline__ void traceBody(const Args& a) {
     extern __shared__ __attribute__((aligned(16))) double lds[];
     if (blockIdx.x == 0 && threadIdx.x == 0) {
@@ -1935,11 +1939,12 @@ __device__ __forceinline__ void traceBody(const Args& a) {
     }
     Shared sh = stageTables(a, lds, gridParts<GRID>() | STAGE_OPTICS);
 
-    Tracer<GRID, ONECOMP, CONT> T{a, sh};
+    Tracer<GRID, ONECOMP, CONT, STORE> T{a, sh};
     T.labsRsrc = __builtin_amdgcn_make_buffer_rsrc(a.labs, 0, (int)a.labsBytes, 0x00020000);
-    T.pendVal = lds + a.ldsInstrOff;  // after the grid and optics tables
-    T.pendIdx = reinterpret_cast<unsigned*>(lds + a.ldsInstrOff + kLabsBuf * kBlock);
-    T.waveSegs = T.pendIdx + kLabsBuf * kBlock;
+    // after the grid and optics tables: the segment counts, then the Labs buffers (STORE only)
+    T.waveSegs = reinterpret_cast<unsigned*>(lds + a.ldsInstrOff);
+    T.pendVal = lds + a.ldsInstrOff + kSegWords;
+    T.pendIdx = reinterpret_cast<unsigned*>(T.pendVal + kLabsBuf * kBlock);
     if (threadIdx.x < 3 * (kBlock / 64)) T.waveSegs[threadIdx.x] = 0;
     __syncthreads();
     const int lane = threadIdx.x & 63;
@@ -1990,7 +1995,8 @@ __device__ __forceinline__ void traceBody(const Args& a) {
                     r.mode = RAY_NONE;
                 }
             }
-            if constexpr (kSegsPerStep<GRID> == 1) {
+            if constexpr (!STORE) {
+            } else if constexpr (kSegsPerStep<GRID> == 1) {
                 T.drainStep();  // one drain instruction per step
             } else {
                 // a buffer without room for another step's adds: issue the wave's adds
@@ -1998,7 +2004,7 @@ __device__ __forceinline__ void traceBody(const Args& a) {
             }
         }
     }
-    T.drain();
+    if constexpr (STORE) T.drain();
     // (wave totals: lane 0 contributes them)
     const unsigned* ws = T.waveSegs + (threadIdx.x >> 6) * 3;
     const bool l0 = lane == 0;
@@ -2009,13 +2015,20 @@ __device__ __forceinline__ void traceBody(const Args& a) {
 
 template <int GRID, bool ONECOMP, bool CONT>
 __global__ void __launch_bounds__(kBlock) SKIRT_TRACE_ATTR traceKernel(const Args a) {
-    traceBody<GRID, ONECOMP, CONT>(a);
+    traceBody<GRID, ONECOMP, CONT, true>(a);
+}
+
+// a phase that stores no absorption (the dust emission phase), one component, no continuous scattering:
+// without the Labs buffers' LDS and registers, at 4 waves per SIMD
+template <int GRID>
+__global__ void __launch_bounds__(kBlock) SKIRT_NOSTORE_TRACE_ATTR traceKernelNoStore(const Args a) {
+    traceBody<GRID, true, false, false>(a);
 }
 
 // the Voronoi walk at its own occupancy (SKIRT_VOR_TRACE_ATTR)
 template <bool ONECOMP, bool CONT>
 __global__ void __launch_bounds__(kBlock) SKIRT_VOR_TRACE_ATTR traceKernelVor(const Args a) {
-    traceBody<SKIRT_GRID_VORONOI, ONECOMP, CONT>(a);
+    traceBody<SKIRT_GRID_VORONOI, ONECOMP, CONT, true>(a);
 }
 
 // the detections of this iteration's peel-off rays (their optical depths are in the queue now)
@@ -4252,9 +4265,12 @@ static int runPhase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, uint6
     off += a.ninstr * (int)(sizeof(DevInstr) / sizeof(double));
     a.ldsSedOff = off;
     off += c->nsed;
+    // a phase storing no absorption with one component runs traceKernelNoStore (no Labs buffers)
+    const bool noStore = !a.store && a.ncomp == 1 && !continuous && c->gridKind != SKIRT_GRID_VORONOI &&
+                         !getenv("SKIRT_AMD_NO_NOSTORE");
     const size_t ldsTrace = (size_t)a.ldsInstrOff * sizeof(double)          // grid tables + optics
-                            + (size_t)kLabsBuf * kBlock * (sizeof(double) + sizeof(unsigned))  // + Labs buffers
-                            + (size_t)3 * (kBlock / 64) * sizeof(unsigned);               // + segment counts
+                            + (size_t)kSegWords * sizeof(double)                          // + segment counts
+                            + (noStore ? 0 : (size_t)kLabsBuf * kBlock * (sizeof(double) + sizeof(unsigned)));  // + Labs buffers
     const size_t ldsEvent = (size_t)a.ldsSedOff * sizeof(double);           // + instruments
     // budget: what one workgroup may allocate (160 KiB on gfx950). The trace and event kernels need their
     // tables; the detect kernel keeps as many SED copies as fit (8, 4, 2, 1), or none (SEDs to the tally)
@@ -4286,16 +4302,19 @@ static int runPhase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, uint6
                                                : SKIRT_WALK_TREE_NODES;
     const bool one = a.ncomp == 1;
     const void* traceFn = nullptr;
-    auto pick = [&](auto fn1, auto fnN, auto fn1c, auto fnNc) {
+    auto pick = [&](auto fn1, auto fnN, auto fn1c, auto fnNc, const void* fnNoStore) {
         traceFn = continuous ? (one ? (const void*)fn1c : (const void*)fnNc) : (one ? (const void*)fn1 : (const void*)fnN);
+        if (noStore) traceFn = fnNoStore;
     };
-#define SKIRT_PICK(G) pick(traceKernel<G, true, false>, traceKernel<G, false, false>, traceKernel<G, true, true>, traceKernel<G, false, true>)
+#define SKIRT_PICK(G) pick(traceKernel<G, true, false>, traceKernel<G, false, false>, traceKernel<G, true, true>, \
+                           traceKernel<G, false, true>, (const void*)traceKernelNoStore<G>)
     if (kind == SKIRT_GRID_CARTESIAN) SKIRT_PICK(SKIRT_GRID_CARTESIAN);
     else if (kind == SKIRT_GRID_OCTREE) SKIRT_PICK(SKIRT_GRID_OCTREE);
     else if (kind == kBinTreeMap) SKIRT_PICK(kBinTreeMap);
     else if (kind == kOctreeBookkeeping) SKIRT_PICK(kOctreeBookkeeping);
     else if (kind == SKIRT_GRID_VORONOI)
-        pick(traceKernelVor<true, false>, traceKernelVor<false, false>, traceKernelVor<true, true>, traceKernelVor<false, true>);
+        pick(traceKernelVor<true, false>, traceKernelVor<false, false>, traceKernelVor<true, true>, traceKernelVor<false, true>,
+             nullptr);
     else SKIRT_PICK(kOctreeNodes);
 #undef SKIRT_PICK
     if (ldsTrace > 64 * 1024)

@@ -122,6 +122,23 @@ def test_two_pipeline_halves_do_not_change_results(name, packages, dust, monkeyp
     _assert_same_packets(*runs)
 
 
+@pytest.mark.parametrize("name,packages", [("pan_oct_sa", 1000), ("pan_cart16", 2000), ("bin_pan", 1000)])
+def test_no_store_trace_kernel_does_not_change_results(name, packages, monkeypatch):
+    """The dust emission phase stores no absorption; with one component it runs traceKernelNoStore (no Labs
+    buffers, 4 waves per SIMD). SKIRT_AMD_NO_NOSTORE=1 runs it on the storing kernel instead: the same
+    packets, the same paths, tallies equal up to the order of the atomic additions."""
+    runs = []
+    for off in ("0", "1"):
+        if off == "1":
+            monkeypatch.setenv("SKIRT_AMD_NO_NOSTORE", "1")
+        else:
+            monkeypatch.delenv("SKIRT_AMD_NO_NOSTORE", raising=False)
+        runs.append(run_gpu(name, packages=packages, dust=True))
+    # the last phase (dust emission) ran at the no-store kernel's occupancy: more trace blocks per CU
+    assert runs[0].stats()["trace_blocks_per_cu"] > runs[1].stats()["trace_blocks_per_cu"]
+    _assert_same_packets(*runs)
+
+
 def _assert_same_packets(a, b):
     sa, sb = a.stats(), b.stats()
     for k in ("packets", "segments_fill", "segments_walk", "segments_peel", "detects", "absorb_adds"):
