@@ -1355,7 +1355,8 @@ struct Grid<SKIRT_GRID_VORONOI> {
         // into the next block -- let the compiler drop the register moves at the join, but made C4 24 % slower,
         // 9.53e7 -> 7.37e7 pkt/s, profiles/r04_ab_c4_vor_uncond_loads_c3c5_prefetch.txt; a lane past its list
         // reading one line that all such lanes share instead: 208 -> 170 register moves, still 5 % slower,
-        // profiles/r05_vor_uncond_shared_ab.txt)
+        // profiles/r05_vor_uncond_shared_ab.txt; round 0 peeled and round 1 loaded into registers of its
+        // own: 208 -> 146 moves, 245 VGPRs, C4 -0.4 %, the same file)
         constexpr int NG = kVorGroups;
         for (int q0 = 0; q0 < s.cnt; q0 += NG * kVorUnroll) {
 #pragma unroll
