@@ -73,11 +73,17 @@ def main():
             continue
         lines.append("")
         lines.append("PMC pass %s (per-dispatch averages):" % os.path.basename(d.rstrip("/")))
-        for k, cs in sorted(counters(path).items()):
+        # every dispatch of a kernel family (traceKernel<...>, traceKernelNoStore<...>, traceKernelVor<...>:
+        # one average per trace launch, as bench.py times them) pooled
+        pooled = collections.defaultdict(lambda: collections.defaultdict(list))
+        for k, cs in counters(path).items():
+            for cn, vals in cs.items():
+                pooled[short(k)][cn].extend(vals)
+        for k, cs in sorted(pooled.items()):
             for cn, vals in sorted(cs.items()):
                 m = sum(vals) / len(vals)
-                avg[(short(k), cn)] = m
-                lines.append("  %-20s %-22s %.6g  (%d dispatches)" % (short(k), cn, m, len(vals)))
+                avg[(k, cn)] = m
+                lines.append("  %-20s %-22s %.6g  (%d dispatches)" % (k, cn, m, len(vals)))
     open(os.path.join(prof, "%s_rocprof_%s%s.txt" % (rnd, cfg, tag)), "w").write("\n".join(lines) + "\n")
     f = avg.get(("traceKernel", "FETCH_SIZE"))
     w = avg.get(("traceKernel", "WRITE_SIZE"))
