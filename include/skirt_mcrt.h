@@ -226,7 +226,9 @@ int skirt_mcrt_run_stellar(SkirtMcrt* ctx, uint64_t npp, uint64_t first, uint64_
  *                             uploaded cell sources with the emission bias, peel-off on, no absorption stored
  *   SKIRT_PHASE_DUST_SELFABS  dodustselfabsorptionchunk (:187-240): natural cell choice, no peel-off,
  *                             absorption into the dust Labs tally; `cycle` numbers the self-absorption
- *                             cycles of the simulation (0, 1, ...) */
+ *                             cycles of the simulation (0, 1, ...)
+ * npp = 0 (a simulation of zero packages, which the reference runs: no chunks, zero tallies) is an empty
+ * phase; its phase-end sums still run, so every rank of a sharded run makes the same collective calls. */
 int skirt_mcrt_run_phase(SkirtMcrt* ctx, int phase, uint32_t cycle, uint64_t npp, uint64_t first, uint64_t count,
                          uint64_t seed, const SkirtPhaseParams* params);
 /* Multi-GPU (one process per GPU): rank `rank` of `world` shoots packets [lo, lo + count) of EVERY

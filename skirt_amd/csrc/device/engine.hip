@@ -4069,7 +4069,6 @@ static int phaseEndReduce(SkirtMcrt* c, int phase, const SkirtPhaseParams* p);
 int skirt_mcrt_run_phase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, uint64_t first, uint64_t count,
                          uint64_t seed, const SkirtPhaseParams* p) {
     if (!c || !p) return SKIRT_ERR_ARG;
-    if (npp == 0) return fail(c, SKIRT_ERR_ARG, "npp must be positive");
     if (first + count > npp * (uint64_t)c->nlambda) return fail(c, SKIRT_ERR_ARG, "packet range exceeds npp*nlambda");
     if (c->instrReduced) return fail(c, SKIRT_ERR_STATE, kSummedTwice);
     int rc = runPhase(c, phase, cycle, npp, first, count, 0, npp, seed, p);
@@ -4079,7 +4078,6 @@ int skirt_mcrt_run_phase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, 
 int skirt_mcrt_run_phase_shard(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, int rank, int world,
                                uint64_t seed, const SkirtPhaseParams* p) {
     if (!c || !p) return SKIRT_ERR_ARG;
-    if (npp == 0) return fail(c, SKIRT_ERR_ARG, "npp must be positive");
     if (world < 1 || rank < 0 || rank >= world) return fail(c, SKIRT_ERR_ARG, "bad shard (rank, world)");
     if (world > 1 && !c->reduce) return fail(c, SKIRT_ERR_STATE, "a sharded phase needs a reducer (skirt_mcrt_set_reducer)");
     if (c->instrReduced) return fail(c, SKIRT_ERR_STATE, kSummedTwice);
@@ -4141,7 +4139,6 @@ static int runPhase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, uint6
     if (c->gridKind < 0 && p->has_dust) return fail(c, SKIRT_ERR_STATE, "no grid uploaded");
     if (!cellPhase && !c->dLumtot) return fail(c, SKIRT_ERR_STATE, "no sources uploaded");
     if (p->has_dust && !c->dRho) return fail(c, SKIRT_ERR_STATE, "no media uploaded");
-    if (npp == 0) return fail(c, SKIRT_ERR_ARG, "npp must be positive");
     if (first + count > npp * (uint64_t)c->nlambda) return fail(c, SKIRT_ERR_ARG, "packet range exceeds npp*nlambda");
     if (p->min_weight_reduction <= 0 || p->scatt_bias < 0 || p->scatt_bias > 1) return fail(c, SKIRT_ERR_ARG, "bad phase parameters");
     HIPCHECK(c, hipSetDevice(c->device));

@@ -245,6 +245,34 @@ def test_dust_free_models_match_oracle_same_streams(tmp_path, name, mix):
         np.testing.assert_allclose(frames, orc.frames[0], rtol=1e-12, atol=1e-300)
 
 
+@pytest.mark.parametrize("name", ["c1_oligo16", "pan_oct", "pan_oct_sac"])
+def test_zero_packages_give_zero_tallies(tmp_path, name):
+    """A .ski with packages="0": the reference runs no chunk in any phase and writes zeros (the oracle
+    restates it); the engine runs every phase empty, the self-absorption cycles and the dust emission
+    included, and its tallies are zero, not NaN."""
+    text = open(ski(name)).read()
+    text, n = re.subn(r'packages="[^"]*"', 'packages="0"', text)
+    assert n >= 1
+    path = str(tmp_path / (name + "_p0.ski"))
+    with open(path, "w") as f:
+        f.write(text)
+    sim = S.Simulation(path)
+    assert sim.info.npp == 0
+    sim.attach(0)
+    sim.run_stellar()
+    sim.run_dust()
+    sim.fetch()
+    orc = O.run(path, rng=O.RNG_PHILOX, threads=4, phases=O.PHASES_ALL)
+    assert sim.stats()["packets"] == orc.packets == 0
+    if sim.info.store_absorption:
+        assert np.all(sim.labs() == 0)
+    for i in range(sim.info.ninstruments):
+        frames, seds = sim.instrument(i)
+        for got, want in ((seds, orc.seds[i]), (frames, orc.frames[i])):
+            if got is not None:
+                assert np.all(got == 0) and np.all(np.asarray(want) == 0)
+
+
 def test_more_ranks_than_packets_per_wavelength():
     """Ragged shards: 7 ranks over 3 packets per wavelength, so four ranks shoot nothing. Every rank runs its
     (possibly empty) slice of every wavelength without error, and the slices add up to the whole."""
