@@ -282,6 +282,8 @@ struct Args {
     double* labs;                // [nlambda][labsStride], device cell order
     unsigned labsBytes;          // its size (< 4 GiB: the trace kernel addresses it through a buffer descriptor)
     int labsGlobal;              // 1: a table of 4 GiB or more, added to with global atomics (no descriptor)
+    int labsCopies;              // > 1: `labs` holds that many replicas labsCopyStride bytes apart, wave w adding
+    unsigned labsCopyStride;     //   into replica w % labsCopies (folded into the table at the phase end)
     double* tally;
     unsigned int* error;
     unsigned long long* stats;   // packets, seg_fill, seg_walk, seg_peel, detects, absorbs, lane slots
@@ -1422,6 +1424,8 @@ struct Tracer {
     double* pendVal;    // LDS, [kLabsBuf][kBlock]
     unsigned* pendIdx;  // LDS, [kLabsBuf][kBlock]
     __amdgpu_buffer_rsrc_t labsRsrc;  // the Labs table as a raw buffer of labsBytes (unless Args::labsGlobal)
+    unsigned copyOff = 0;             // this wave's replica (Args::labsCopies), in bytes
+    unsigned labsOob = 0;             // a byte offset past every replica: the empty lanes' adds are dropped
     int npend = 0;
     unsigned gstep = 0;  // grid steps of the wave (drainStep's round robin)
 
@@ -1459,7 +1463,7 @@ struct Tracer {
         } else {
             // every lane issues; a lane without an add adds 0 at the first byte past the table (dropped)
             const double v = j < n ? pendVal[q] : 0.0;
-            bufferAtomicAddF64(v, labsRsrc, (int)(j < n ? idx * 8u : a.labsBytes), 0, 0);
+            bufferAtomicAddF64(v, labsRsrc, (int)(j < n ? idx * 8u + copyOff : labsOob), 0, 0);
         }
     }
 
@@ -1941,7 +1945,10 @@ __device__ __forceinline__ void traceBody(const Args& a) {
     Shared sh = stageTables(a, lds, gridParts<GRID>() | STAGE_OPTICS);
 
     Tracer<GRID, ONECOMP, CONT, STORE> T{a, sh};
-    T.labsRsrc = __builtin_amdgcn_make_buffer_rsrc(a.labs, 0, (int)a.labsBytes, 0x00020000);
+    T.labsOob = a.labsCopies > 1 ? (unsigned)a.labsCopies * a.labsCopyStride : a.labsBytes;
+    T.labsRsrc = __builtin_amdgcn_make_buffer_rsrc(a.labs, 0, (int)T.labsOob, 0x00020000);
+    if (a.labsCopies > 1)
+        T.copyOff = (unsigned)((blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) % (unsigned)a.labsCopies) * a.labsCopyStride;
     // after the grid and optics tables: the segment counts, then the Labs buffers (STORE only)
     T.waveSegs = reinterpret_cast<unsigned*>(lds + a.ldsInstrOff);
     T.pendVal = lds + a.ldsInstrOff + kSegWords;
@@ -2987,6 +2994,9 @@ struct SkirtMcrt {
     int* dCellNode = nullptr;
     double* dLabsDust = nullptr;
     bool ownLabsDust = true;
+    // Labs replicas (SKIRT_AMD_LABS_COPIES > 1): the absorbing phases add into them, folded at the phase end
+    double* dLabsRep = nullptr;
+    size_t labsRepBytes = 0;
     // grey-body emissivity tables for the device-side dust emission sources
     int emisNtemp = 0;
     double *dEmisVolume = nullptr, *dEmisKabs = nullptr, *dEmisSigma = nullptr, *dEmisMu = nullptr, *dEmisTv = nullptr,
@@ -4030,6 +4040,7 @@ static int ensureDustLabs(SkirtMcrt* c) {
 int skirt_mcrt_bind_dust_labs(SkirtMcrt* c, double* d) {
     if (!c || !d) return SKIRT_ERR_ARG;
     if (c->ownLabsDust && c->dLabsDust) (void)hipFree(c->dLabsDust);
+    if (c->dLabsRep) (void)hipFree(c->dLabsRep);
     c->dLabsDust = d;
     c->ownLabsDust = false;
     return SKIRT_OK;
@@ -4113,6 +4124,19 @@ int skirt_mcrt_reduce_instruments(SkirtMcrt* c) {
         return fail(c, SKIRT_ERR_STATE, "the instrument reduction failed");
     c->instrReduced = true;
     return SKIRT_OK;
+}
+
+// the Labs replicas of an absorbing phase (Args::labsCopies) added into the table, in replica order, and
+// zeroed for the next phase
+__global__ void labsFoldKernel(double* dst, double* rep, size_t n, int copies, size_t strideElems) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        double sum = 0.0;
+        for (int k = 0; k < copies; k++) {
+            sum += rep[k * strideElems + i];
+            rep[k * strideElems + i] = 0.0;
+        }
+        dst[i] += sum;
+    }
 }
 
 // PanDustSystem::sumResults at the end of a phase (PanDustSystem.cpp:394-403): the stellar Labs after the
@@ -4244,6 +4268,34 @@ static int runPhase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, uint6
     a.labsGlobal = (forceGlobal || labsElems * sizeof(double) > 0xfffffff8ull) ? 1 : 0;
     a.labs = phase == SKIRT_PHASE_DUST_SELFABS ? c->dLabsDust : c->dLabs;
     a.labsBytes = a.labsGlobal ? 0u : (unsigned)(labsElems * sizeof(double));
+    // The trace waves add into K replicas of the table (wave w into w % K), folded into it at the phase end:
+    // the adds to one cell spread over K lines, which the memory-side atomic unit works on side by side.
+    // The replicas pay only while they stay in the MALL (256 MB): C3 (a 129 MB table) 2: +1.1 %, 4: +0.8 %,
+    // 8: -3.4 %; C2 (21 MB) 4: +2 %, 8: +3.3 % (profiles/r05_labs_copies_ab.txt). K = 320 MiB / the table,
+    // at most 8; SKIRT_AMD_LABS_COPIES sets it (1: no replicas)
+    double* const labsTarget = a.labs;
+    a.labsCopies = 1;
+    a.labsCopyStride = 0;
+    {
+        const uint64_t tableBytes = (uint64_t)a.labsBytes > 0 ? (uint64_t)a.labsBytes : 1;
+        const int Kauto = (int)std::min<uint64_t>(8, std::max<uint64_t>(1, (320ull << 20) / tableBytes));
+        const int K = getenv("SKIRT_AMD_LABS_COPIES") ? atoi(getenv("SKIRT_AMD_LABS_COPIES")) : Kauto;
+        const uint64_t stride = ((uint64_t)a.labsBytes + 255) & ~255ull;
+        if (a.store && !a.labsGlobal && K > 1 && K <= 64 && stride * (uint64_t)K <= 0xfffffff0ull) {
+            const size_t need = (size_t)stride * K;
+            if (c->labsRepBytes < need) {
+                if (c->dLabsRep) HIPCHECK(c, hipFree(c->dLabsRep));
+                c->dLabsRep = nullptr;
+                c->labsRepBytes = 0;
+                HIPCHECK(c, hipMalloc(&c->dLabsRep, need));
+                HIPCHECK(c, hipMemsetAsync(c->dLabsRep, 0, need, c->stream));
+                c->labsRepBytes = need;
+            }
+            a.labs = c->dLabsRep;
+            a.labsCopies = K;
+            a.labsCopyStride = (unsigned)stride;
+        }
+    }
     a.tally = c->dTally;
     a.error = c->dError; a.stats = c->dStats;
     a.crossed = c->dCrossed; a.crossedBins = c->crossedBins;
@@ -4497,6 +4549,11 @@ static int runPhase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, uint6
             HIPCHECK(c, hipStreamWaitEvent(c->stream, c->evJoin[1 + h], 0));
         }
     }
+    if (a.labsCopies > 1) {
+        hipLaunchKernelGGL(labsFoldKernel, dim3(2048), dim3(kBlock), 0, c->stream, labsTarget, c->dLabsRep,
+                           (size_t)labsElems, a.labsCopies, (size_t)a.labsCopyStride / sizeof(double));
+        HIPCHECK(c, hipGetLastError());
+    }
     HIPCHECK(c, hipEventRecord(c->ev1, c->stream));
     c->phaseTimed = true;
     return SKIRT_OK;
@@ -4675,6 +4732,7 @@ void skirt_mcrt_destroy(SkirtMcrt* c) {
     if (c->ownLabs && c->dLabs) (void)hipFree(c->dLabs);
     if (c->ownTally && c->dTally) (void)hipFree(c->dTally);
     if (c->ownLabsDust && c->dLabsDust) (void)hipFree(c->dLabsDust);
+    if (c->dLabsRep) (void)hipFree(c->dLabsRep);
     for (hipEvent_t e : c->traceEv) (void)hipEventDestroy(e);
     for (hipEvent_t e : c->pollEv) (void)hipEventDestroy(e);
     if (c->evFork) (void)hipEventDestroy(c->evFork);

@@ -139,6 +139,22 @@ def test_no_store_trace_kernel_does_not_change_results(name, packages, monkeypat
     _assert_same_packets(*runs)
 
 
+@pytest.mark.parametrize("name,packages,dust", [("pan_oct_sa", 1000, True), ("c1_oligo16", 20000, False)])
+def test_labs_replicas_do_not_change_results(name, packages, dust, monkeypatch):
+    """The absorbing phases add into replicas of the Labs table, folded into it at the phase end (by default
+    as many as fit 320 MiB, at most 8); SKIRT_AMD_LABS_COPIES=1 adds into the table itself and =3 into three
+    replicas: the same packets, tallies equal up to the order of the additions."""
+    runs = []
+    for k in (None, "1", "3"):
+        if k is None:
+            monkeypatch.delenv("SKIRT_AMD_LABS_COPIES", raising=False)
+        else:
+            monkeypatch.setenv("SKIRT_AMD_LABS_COPIES", k)
+        runs.append(run_gpu(name, packages=packages, dust=dust))
+    _assert_same_packets(runs[1], runs[0])
+    _assert_same_packets(runs[1], runs[2])
+
+
 def _assert_same_packets(a, b):
     sa, sb = a.stats(), b.stats()
     for k in ("packets", "segments_fill", "segments_walk", "segments_peel", "detects", "absorb_adds"):
