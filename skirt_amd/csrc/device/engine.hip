@@ -4270,15 +4270,18 @@ static int runPhase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, uint6
     a.labsBytes = a.labsGlobal ? 0u : (unsigned)(labsElems * sizeof(double));
     // The trace waves add into K replicas of the table (wave w into w % K), folded into it at the phase end:
     // the adds to one cell spread over K lines, which the memory-side atomic unit works on side by side.
-    // The replicas pay only while they stay in the MALL (256 MB): C3 (a 129 MB table) 2: +1.1 %, 4: +0.8 %,
-    // 8: -3.4 %; C2 (21 MB) 4: +2 %, 8: +3.3 % (profiles/r05_labs_copies_ab.txt). K = 320 MiB / the table,
-    // at most 8; SKIRT_AMD_LABS_COPIES sets it (1: no replicas)
+    // In the stellar phase the replicas pay while they stay near the MALL (256 MB): C3 (a 129 MB table) 2:
+    // +1.1 %, 3: +1.2 %, 4: +0.8 %, 6: -1 %, 8: -3.4 %; C2 (21 MB) 4: +2 %, 8: +3.3 %. The self-absorption
+    // cycles' adds crowd onto fewer lines and gain up to 6: C5 with 3 in the stellar phase and 6 in the
+    // cycles +9.0 % against none, +3.6 % against 2 everywhere; C3 +1.2 % (profiles/r05_labs_copies_ab.txt).
+    // K = 400 MiB (self-absorption: 800 MiB) / the table, at most 8; SKIRT_AMD_LABS_COPIES sets it (1: none)
     double* const labsTarget = a.labs;
     a.labsCopies = 1;
     a.labsCopyStride = 0;
     {
         const uint64_t tableBytes = (uint64_t)a.labsBytes > 0 ? (uint64_t)a.labsBytes : 1;
-        const int Kauto = (int)std::min<uint64_t>(8, std::max<uint64_t>(1, (320ull << 20) / tableBytes));
+        const uint64_t budget = phase == SKIRT_PHASE_DUST_SELFABS ? (800ull << 20) : (400ull << 20);
+        const int Kauto = (int)std::min<uint64_t>(8, std::max<uint64_t>(1, budget / tableBytes));
         const int K = getenv("SKIRT_AMD_LABS_COPIES") ? atoi(getenv("SKIRT_AMD_LABS_COPIES")) : Kauto;
         const uint64_t stride = ((uint64_t)a.labsBytes + 255) & ~255ull;
         if (a.store && !a.labsGlobal && K > 1 && K <= 64 && stride * (uint64_t)K <= 0xfffffff0ull) {
