@@ -135,3 +135,47 @@ def test_eight_rank_gloo_shards_balance_the_c3_work(tmp_path):
     assert np.all(pkts == pkts[0]) and pkts[0] > 0
     print("C3 segments per rank:", segs.astype(int).tolist(), "max/mean %.4f" % (segs.max() / segs.mean()))
     assert segs.max() / segs.mean() <= 1.05, segs
+
+
+def _worker_reducer_failure(rank, world, port, outdir, mode):
+    from skirt_amd.sharding import TallyReducer
+
+    _init(rank, world, port)
+    try:
+        t = torch.ones(8, dtype=torch.float64)
+        red = TallyReducer(t)
+        res = [red(0, t.data_ptr(), 8, 0)]  # every rank healthy: summed
+        if rank == 1 and mode == "lookup":
+            res.append(red(0, t.data_ptr() + 8, 8, 0))  # a buffer that is not a bound tensor
+        elif rank == 1 and mode == "abort":
+            red.abort("rank 1: the photon phase failed")  # failed outside the reducer
+            res.append(-1)
+        else:
+            res.append(red(0, t.data_ptr(), 8, 0))
+        res.append(red(0, t.data_ptr(), 8, 0))  # after a failure: refused without a collective
+        np.save(os.path.join(outdir, "r%d.npy" % rank), np.array(res + [t.sum().item()], dtype=np.float64))
+        with open(os.path.join(outdir, "e%d.txt" % rank), "w") as f:
+            f.write(str(red.error))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(180)
+@pytest.mark.parametrize("mode", ["lookup", "abort"])
+def test_reducer_failure_reaches_every_rank_without_a_hang(tmp_path, mode):
+    """TallyReducer's failure agreement (the reference's Parallel::call: the first failure stops every worker,
+    Parallel.cpp:181-193). Rank 1 of 3 fails at the second reduction, either in the reducer (a buffer lookup)
+    or outside it (abort(), as Simulation calls it when a phase raises). Every rank's second reduction then
+    returns 1 instead of entering an all-reduce rank 1 never joins, the third is refused at once, and only the
+    first sum happened (a hang fails the test through its timeout)."""
+    world = 3
+    mp.spawn(_worker_reducer_failure, args=(world, _free_port(), str(tmp_path), mode), nprocs=world, join=True)
+    for r in range(world):
+        res = np.load(os.path.join(tmp_path, "r%d.npy" % r))
+        second = -1 if (r == 1 and mode == "abort") else 1
+        assert res.tolist() == [0, second, 1, 8 * world], (r, res)
+        err = open(os.path.join(tmp_path, "e%d.txt" % r)).read()
+        if r == 1:
+            assert ("rank 1: the photon phase failed" if mode == "abort" else "not a bound tensor") in err
+        else:
+            assert err == "another rank failed"

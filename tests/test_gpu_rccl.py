@@ -45,3 +45,17 @@ def test_rccl_one_device_equals_single_device_run(tmp_path, name):
                     np.testing.assert_allclose(float(y), float(x), rtol=1e-6, atol=0)  # 7-9 printed digits
                 except ValueError:
                     assert x == y, f
+
+
+def test_a_failing_device_thread_returns_its_error(tmp_path):
+    """The failure path of `-g N` (Parallel.cpp:181-193: the first failure stops every worker and is reported
+    by the parent): SKIRT_AMD_FAIL_DEVICE=0 makes device 0's thread fail before its first phase. The call
+    returns that error, without waiting in a collective, and writes no outputs. (The gate that keeps the
+    other ranks out of their collectives is tested on the CPU, tests/test_rank_gate.py.)"""
+    ski = os.path.join(GOLD, "pan_oct.ski")
+    env = dict(os.environ, SKIRT_AMD_FAIL_DEVICE="0")
+    r = subprocess.run([CLI, "-g", "1", "-p", "200", "-o", str(tmp_path / "f"), ski], capture_output=True,
+                       text=True, timeout=120, env=env)
+    assert r.returncode != 0
+    assert "device 0: failure injected (SKIRT_AMD_FAIL_DEVICE)" in r.stderr, r.stderr
+    assert not [f for f in os.listdir(tmp_path) if f.startswith("f_")]
