@@ -1526,6 +1526,9 @@ struct Tracer {
                     albedo = (kext > 0.0) ? ksca / kext : 0.0;
                     r.f2 += albedo * Lintm;
                 }
+#ifdef SKIRT_DEBUG_FILL  // diagnostic builds only (tools/parity_trace.py): the FILL segments, one packet per run
+                printf("E S %d %.17g %.17g %.17g\n", m, ds, dtau, (1.0 - albedo) * Lintm);
+#endif
                 if (STORE && a.store) {
                     pendVal[npend * kBlock + threadIdx.x] = (1.0 - albedo) * Lintm;
                     pendIdx[npend * kBlock + threadIdx.x] = (unsigned)r.ell * (unsigned)a.labsStride + (unsigned)m;
@@ -1560,6 +1563,10 @@ struct Tracer {
         r.ell = rayEll(r.flags);
         r.tau = 0;
         if (CONT && r.mode == RAY_FILL) a.pathCnt[r.idx] = 0;
+#ifdef SKIRT_DEBUG_FILL
+        if (r.mode == RAY_FILL)
+            printf("E L %d %.17g %.17g %.17g %.17g %.17g %.17g %.17g\n", r.ell, r.x, r.y, r.z, r.dx, r.dy, r.dz, r.param);
+#endif
         r.s = c3.x;
         r.kext = sh.kext[r.ell];
         // FILL: f1 = exp(-tau) = 1, f2 = scattered luminosity; WALK: tau and s at the last segment end
@@ -2997,6 +3004,9 @@ struct SkirtMcrt {
     // Labs replicas (SKIRT_AMD_LABS_COPIES > 1): the absorbing phases add into them, folded at the phase end
     double* dLabsRep = nullptr;
     size_t labsRepBytes = 0;
+    // trace launches have added into the replicas since their last fold: a phase that ended early (an error
+    // return after its first trace launch) left partial adds there, which the next storing phase clears
+    bool labsRepDirty = false;
     // grey-body emissivity tables for the device-side dust emission sources
     int emisNtemp = 0;
     double *dEmisVolume = nullptr, *dEmisKabs = nullptr, *dEmisSigma = nullptr, *dEmisMu = nullptr, *dEmisTv = nullptr,
@@ -4040,7 +4050,7 @@ static int ensureDustLabs(SkirtMcrt* c) {
 int skirt_mcrt_bind_dust_labs(SkirtMcrt* c, double* d) {
     if (!c || !d) return SKIRT_ERR_ARG;
     if (c->ownLabsDust && c->dLabsDust) (void)hipFree(c->dLabsDust);
-    if (c->dLabsRep) (void)hipFree(c->dLabsRep);
+    // the Labs replicas (dLabsRep) stay: they depend on the table's size only, not on where it lives
     c->dLabsDust = d;
     c->ownLabsDust = false;
     return SKIRT_OK;
@@ -4294,6 +4304,11 @@ static int runPhase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, uint6
                 HIPCHECK(c, hipMemsetAsync(c->dLabsRep, 0, need, c->stream));
                 c->labsRepBytes = need;
             }
+            if (c->labsRepDirty) {  // (the failed phase's trace launches may still run on the pipeline streams)
+                HIPCHECK(c, hipDeviceSynchronize());
+                HIPCHECK(c, hipMemsetAsync(c->dLabsRep, 0, c->labsRepBytes, c->stream));
+            }
+            c->labsRepDirty = true;  // until the fold at this phase's end
             a.labs = c->dLabsRep;
             a.labsCopies = K;
             a.labsCopyStride = (unsigned)stride;
@@ -4472,6 +4487,9 @@ static int runPhase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, uint6
         }
         return SKIRT_OK;
     };
+    // iterations per pipeline half before the phase is declared stuck; SKIRT_AMD_MAX_ITERATIONS lowers the cap
+    // (tests of the error exits)
+    const int maxIts = getenv("SKIRT_AMD_MAX_ITERATIONS") ? atoi(getenv("SKIRT_AMD_MAX_ITERATIONS")) : 10000000;
     int total = 0;
     while (true) {
         bool all = true;
@@ -4494,7 +4512,7 @@ static int runPhase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, uint6
                 pollIt[h][slot] = its[h];
                 polls[h]++;
             }
-            if (its[h] > 10000000) return fail(c, SKIRT_ERR_STATE, "photon phase did not terminate");
+            if (its[h] > maxIts) return fail(c, SKIRT_ERR_STATE, "photon phase did not terminate");
             aa.parity = its[h] & 1;
             aa.init = (its[h] == 0) ? 1 : 0;
             if (detAside) {
@@ -4556,6 +4574,7 @@ static int runPhase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, uint6
         hipLaunchKernelGGL(labsFoldKernel, dim3(2048), dim3(kBlock), 0, c->stream, labsTarget, c->dLabsRep,
                            (size_t)labsElems, a.labsCopies, (size_t)a.labsCopyStride / sizeof(double));
         HIPCHECK(c, hipGetLastError());
+        c->labsRepDirty = false;  // the fold zeroes the replicas
     }
     HIPCHECK(c, hipEventRecord(c->ev1, c->stream));
     c->phaseTimed = true;

@@ -516,6 +516,57 @@ def test_second_run_equals_a_fresh_run():
     np.testing.assert_allclose(fa.sum(axis=2), fb.sum(axis=2), rtol=1e-10, atol=1e-300)
 
 
+def _assert_equal_runs(sim, fresh):
+    np.testing.assert_allclose(sim.selfabs_totals(), fresh.selfabs_totals(), rtol=1e-10)
+    np.testing.assert_allclose(sim.labs(), fresh.labs(), rtol=1e-10, atol=1e-300)
+    np.testing.assert_allclose(sim.labs_dust(), fresh.labs_dust(), rtol=1e-10, atol=1e-300)
+    fa, sa = sim.instrument(0)
+    fb, sb = fresh.instrument(0)
+    np.testing.assert_allclose(sa, sb, rtol=1e-10, atol=1e-300)
+    np.testing.assert_allclose(fa, fb, rtol=1e-10, atol=1e-300)
+
+
+def test_a_failed_phase_leaves_no_adds_behind(monkeypatch):
+    """A phase that fails after its first trace launches (here the iteration cap, SKIRT_AMD_MAX_ITERATIONS=2,
+    'photon phase did not terminate') has added into the Labs replicas, which only the phase-end fold used to
+    zero. The next storing phase clears them first: zero_tallies and a good run on the same
+    engine equal a fresh engine's run."""
+    name = "pan_oct_sa"
+    sim = S.Simulation(ski(name), packages=1000)
+    sim.attach(0)
+    monkeypatch.setenv("SKIRT_AMD_MAX_ITERATIONS", "2")
+    with pytest.raises(S.SkirtError, match="did not terminate"):
+        sim.run_stellar()
+        sim.fetch()
+    monkeypatch.delenv("SKIRT_AMD_MAX_ITERATIONS")
+    sim.zero_tallies()
+    sim.run_stellar()
+    sim.run_dust()
+    sim.fetch()
+    _assert_equal_runs(sim, run_gpu(name, packages=1000, dust=True))
+
+
+def test_dust_labs_bound_after_a_stellar_phase():
+    """Binding caller memory for the dust Labs after a stellar phase that added into Labs replicas (ADVICE r5,
+    high): the replicas survive the binding (they used to be freed and then reused and freed again), and the
+    self-absorption cycles and dust emission equal a fresh engine's."""
+    import torch
+
+    name = "pan_oct_sa"
+    sim = S.Simulation(ski(name), packages=1000)
+    sim.attach(0)
+    sim.run_stellar()
+    n_labs, _ = sim.tally_sizes()
+    dust = torch.zeros(n_labs, dtype=torch.float64, device="cuda:0")
+    sim.bind_dust_labs(dust.data_ptr())
+    sim.run_dust()
+    sim.fetch()
+    assert float(dust.sum()) > 0  # the cycles added into the bound memory
+    _assert_equal_runs(sim, run_gpu(name, packages=1000, dust=True))
+    del sim
+    torch.cuda.synchronize()
+
+
 def test_transparent_flux_is_deterministic():
     """F_trav = L/(4 pi d^2) for any seed (invariant 4): 2.41996378e-12 W/m2."""
     sim = run_gpu("c1_oligo16", packages=30000, seed=5)
