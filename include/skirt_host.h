@@ -104,6 +104,16 @@ int skirt_host_voronoi_cells(const SkirtVoronoi* v, double* volume, double* cent
 int skirt_host_voronoi_describe(const SkirtVoronoi* v, SkirtGridDesc* grid);
 void skirt_host_voronoi_free(SkirtVoronoi* v);
 
+/* The engine's input descriptors without a device (tests of the maintainer binding's extraction,
+ * INTEGRATION.md): skirt_sim_describe writes the SkirtGridDesc, SkirtMediaDesc, SkirtSourceDesc and
+ * SkirtInstrDesc that skirt_sim_attach would upload for this model to `path` (truncated first);
+ * skirt_host_write_descriptors appends the given descriptors in the same canonical form (NULL pointers
+ * and ninstr < 0 are skipped): one record per field, "<name> <type> <count>\n" followed by count raw
+ * values (type d double, i int32, b int8), array lengths as skirt_mcrt.h states them. */
+int skirt_sim_describe(SkirtSim* sim, const char* path);
+int skirt_host_write_descriptors(const char* path, const SkirtGridDesc* grid, const SkirtMediaDesc* media,
+                                 const SkirtSourceDesc* sources, const SkirtInstrDesc* instr, int ninstr);
+
 /* The cross-GPU sums in C++: RCCL (NCCL API) all-reduces over xGMI, the MI355X counterpart of the
  * reference's MPI_Allreduce of the absorption tables and instrument arrays (PanDustSystem.cpp:394-404,
  * Instrument.cpp:57-66, MPIsupport/ProcessManager.cpp:133-137).
@@ -120,10 +130,20 @@ int skirt_rccl_create(int ndev, const int* devices, SkirtRccl** out);
 int skirt_rccl_wrap(void* nccl_comm, SkirtRccl** out);
 void* skirt_rccl_rank(SkirtRccl* r, int rank);
 SkirtReduceTallyFn skirt_rccl_reducer(void);
+/* The reference's Parallel::call stops every worker at the first exception and rethrows it in the parent
+ * (SKIRTcore/Parallel.cpp:181-193). Across devices: skirt_rccl_abort marks the job failed (`why` is kept as the
+ * first failure's message), after which no rank of `r` enqueues another all-reduce (the reducer returns
+ * non-zero, also to ranks waiting for the others before one), and aborts owned communicators
+ * (ncclCommAbort), which returns ranks already waiting in an all-reduce on the device. Idempotent.
+ * The reducer of several ranks in one process waits, before each all-reduce, until every rank has arrived
+ * or one has failed, so a rank that fails between two collectives leaves none of its peers waiting. */
+int skirt_rccl_abort(SkirtRccl* r, const char* why);
 void skirt_rccl_destroy(SkirtRccl* r);
 /* The driver of `skirt-mi355x -g N`: loads the ski once per device, runs every phase of the simulation
  * with each device shooting its rank's slice of every wavelength (one host thread per device) and the
- * tallies summed by skirt_rccl at each phase end, then writes the outputs from rank 0. packages > 0 and
+ * tallies summed by skirt_rccl at each phase end, then writes the outputs from rank 0. The first device
+ * thread that fails stops the others (skirt_rccl_abort) and its error is returned; SKIRT_AMD_FAIL_DEVICE=d
+ * makes device d's thread fail before its first phase (tests). packages > 0 and
  * seed != 0 override the ski's. stats (may be NULL) receives rank 0's statistics; seconds (may be NULL)
  * the wall time of the photon phases. */
 int skirt_sim_run_devices(const char* ski, const char* datadir, int ndev, double packages, uint64_t seed,

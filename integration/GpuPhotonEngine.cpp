@@ -46,6 +46,24 @@ namespace
         return 0;
     }
 
+    // the engine's upload of the descriptors (the default sink)
+    class UploadSink : public GpuDescriptorSink
+    {
+    public:
+        explicit UploadSink(SkirtMcrt* ctx) : _ctx(ctx) {}
+        void grid(const SkirtGridDesc& g) override { check(skirt_mcrt_upload_grid(_ctx, &g)); }
+        void media(const SkirtMediaDesc& m) override { check(skirt_mcrt_upload_media(_ctx, &m)); }
+        void sources(const SkirtSourceDesc& s) override { check(skirt_mcrt_upload_sources(_ctx, &s)); }
+        void instruments(const SkirtInstrDesc* d, int n) override { check(skirt_mcrt_set_instruments(_ctx, d, n)); }
+
+    private:
+        void check(int rc) const
+        {
+            if (rc != SKIRT_OK) throw FATALERROR(QString("MI355X engine: ") + skirt_mcrt_last_error(_ctx));
+        }
+        SkirtMcrt* _ctx;
+    };
+
     // adds an engine tally to a detector array; an array the reference left unsized (e.g. the dust slots
     // of a FullInstrument without dust emission, FullInstrument.cpp:61-78) must receive nothing
     void addTally(Array& target, const double* src, size_t n, const char* what)
@@ -72,6 +90,35 @@ GpuPhotonEngine::GpuPhotonEngine(WavelengthGrid* lambdagrid, StellarSystem* ss, 
         throw FATALERROR("MI355X engine: cannot create a context on device " + QString::number(device));
     _Nlambda = _lambdagrid->Nlambda();
     _Ncells = _ds ? _ds->Ncells() : 0;
+    UploadSink upload(_ctx);
+    _sink = &upload;
+    describeAll();
+    _sink = nullptr;
+    check(skirt_mcrt_set_reducer(_ctx, keepLocal, nullptr));
+    check(skirt_mcrt_zero_tallies(_ctx));
+    _params.store_absorption = _ds && _ds->storeabsorptionrates() ? 1 : 0;
+    _params.has_dust = _ds ? 1 : 0;
+}
+
+////////////////////////////////////////////////////////////////////
+
+GpuPhotonEngine::GpuPhotonEngine(WavelengthGrid* lambdagrid, StellarSystem* ss, DustSystem* ds, InstrumentSystem* is,
+                                 GpuDescriptorSink* sink)
+    : _lambdagrid(lambdagrid), _ss(ss), _ds(ds), _is(is), _sink(sink)
+{
+    _Nlambda = _lambdagrid->Nlambda();
+    _Ncells = _ds ? _ds->Ncells() : 0;
+}
+
+void GpuPhotonEngine::describe(WavelengthGrid* lambdagrid, StellarSystem* ss, DustSystem* ds, InstrumentSystem* is,
+                               GpuDescriptorSink& sink)
+{
+    GpuPhotonEngine items(lambdagrid, ss, ds, is, &sink);
+    items.describeAll();
+}
+
+void GpuPhotonEngine::describeAll()
+{
     if (_ds)
     {
         describeGrid();
@@ -79,10 +126,6 @@ GpuPhotonEngine::GpuPhotonEngine(WavelengthGrid* lambdagrid, StellarSystem* ss, 
     }
     describeSources();
     describeInstruments();
-    check(skirt_mcrt_set_reducer(_ctx, keepLocal, nullptr));
-    check(skirt_mcrt_zero_tallies(_ctx));
-    _params.store_absorption = _ds && _ds->storeabsorptionrates() ? 1 : 0;
-    _params.has_dust = _ds ? 1 : 0;
 }
 
 ////////////////////////////////////////////////////////////////////
@@ -161,7 +204,7 @@ void GpuPhotonEngine::describeGrid()
         box.resize(6 * static_cast<size_t>(Nnodes));
         firstChild.assign(Nnodes, -1);
         cellnumber.assign(Nnodes, -1);
-        splitDir.assign(Nnodes, 0);
+        splitDir.assign(Nnodes, -1);  // (leaves: -1, as the .ski driver stores them)
         nbrOffset.assign(6 * static_cast<size_t>(Nnodes) + 1, 0);
         for (int l = 0; l < Nnodes; l++)
         {
@@ -219,13 +262,14 @@ void GpuPhotonEngine::describeGrid()
         const double extent[6] = {e.xmin(), e.ymin(), e.zmin(), e.xmax(), e.ymax(), e.zmax()};
         _voronoi = skirt_host_voronoi_build(sites.data(), _Ncells, extent);
         if (!_voronoi) throw FATALERROR(QString("MI355X engine: ") + skirt_sim_error());
-        check(skirt_host_voronoi_describe(_voronoi, &g));
+        if (skirt_host_voronoi_describe(_voronoi, &g) != SKIRT_OK)
+            throw FATALERROR("MI355X engine: cannot describe the Voronoi tessellation");
     }
     else
     {
         throw FATALERROR("MI355X engine: dust grid type " + QString(grid->metaObject()->className()) + " is not supported");
     }
-    check(skirt_mcrt_upload_grid(_ctx, &g));
+    _sink->grid(g);
 }
 
 ////////////////////////////////////////////////////////////////////
@@ -251,7 +295,7 @@ void GpuPhotonEngine::describeMedia()
         }
     }
     SkirtMediaDesc md = {_Ncells, Ncomp, _Nlambda, rho.data(), kext.data(), ksca.data(), alb.data(), g.data()};
-    check(skirt_mcrt_upload_media(_ctx, &md));
+    _sink->media(md);
 }
 
 ////////////////////////////////////////////////////////////////////
@@ -274,6 +318,7 @@ void GpuPhotonEngine::describeSources()
         if (PlummerGeometry* pg = dynamic_cast<PlummerGeometry*>(geo))
         {
             p[0] = pg->scale();
+            p[1] = pg->_rho0;  // PlummerGeometry.cpp:30 (no public getter)
         }
         else if (ExpDiskGeometry* eg = dynamic_cast<ExpDiskGeometry*>(geo))
         {
@@ -283,12 +328,14 @@ void GpuPhotonEngine::describeSources()
             p[2] = eg->radialTrunc();
             p[3] = eg->axialTrunc();
             p[4] = eg->innerRadius();
+            p[5] = eg->_rho0;  // ExpDiskGeometry.cpp:42
         }
         else if (SersicGeometry* sg = dynamic_cast<SersicGeometry*>(geo))
         {
             kind[h] = SKIRT_GEOM_SERSIC;
             p[0] = sg->radius();
             p[1] = sg->index();
+            p[2] = sg->_rho0;  // SersicGeometry.cpp (setupSelfBefore)
             const SersicFunction* sf = sg->_sersicfunction;
             if (sf->_sv.size() != 101 || sf->_Mv.size() != 101)
                 throw FATALERROR("MI355X engine: unexpected SersicFunction table size");
@@ -319,7 +366,7 @@ void GpuPhotonEngine::describeSources()
     }
     SkirtSourceDesc sd = {Ncomp, _Nlambda, kind.data(), param.data(), lum.data(), lumtot.data(), cdf.data(),
                           _ss->emissionBias(), table.empty() ? nullptr : table.data()};
-    check(skirt_mcrt_upload_sources(_ctx, &sd));
+    _sink->sources(sd);
 }
 
 ////////////////////////////////////////////////////////////////////
@@ -363,7 +410,7 @@ void GpuPhotonEngine::describeInstruments()
         }
         descs.push_back(d);
     }
-    check(skirt_mcrt_set_instruments(_ctx, descs.data(), static_cast<int>(descs.size())));
+    _sink->instruments(descs.data(), static_cast<int>(descs.size()));
 }
 
 ////////////////////////////////////////////////////////////////////

@@ -13,9 +13,9 @@
 //
 // Needs `friend class GpuPhotonEngine;` in the classes whose state it reads or fills (the patch that
 // check_binding.sh applies to a scratch copy of the headers): DustMix (_asymmparv), TreeDustGrid (_tree,
-// _cellnumberv, _eps), TreeNode (_neighbors), VoronoiDustGrid (_mesh), SersicGeometry (_sersicfunction),
-// SersicFunction (_sv, _Mv), FullInstrument, SimpleInstrument, FrameInstrument, SEDInstrument (detector
-// arrays).
+// _cellnumberv, _eps), TreeNode (_neighbors), VoronoiDustGrid (_mesh), SersicGeometry (_sersicfunction,
+// _rho0), SersicFunction (_sv, _Mv), PlummerGeometry and ExpDiskGeometry (_rho0), FullInstrument,
+// SimpleInstrument, FrameInstrument, SEDInstrument (detector arrays).
 #ifndef GPUPHOTONENGINE_HPP
 #define GPUPHOTONENGINE_HPP
 
@@ -31,9 +31,26 @@ class StellarSystem;
 class WavelengthGrid;
 struct SkirtVoronoi;
 
+// Receives the engine's input descriptors as the binding extracts them from the set-up simulation items; the
+// engine's upload is one such sink, a file dump (skirt_host_write_descriptors) another, which lets a test
+// compare the binding's extraction with the .ski driver's without a device (tests/test_binding_describe.py)
+class GpuDescriptorSink
+{
+public:
+    virtual ~GpuDescriptorSink() = default;
+    virtual void grid(const SkirtGridDesc& g) = 0;
+    virtual void media(const SkirtMediaDesc& m) = 0;
+    virtual void sources(const SkirtSourceDesc& s) = 0;
+    virtual void instruments(const SkirtInstrDesc* d, int n) = 0;
+};
+
 class GpuPhotonEngine
 {
 public:
+    // The descriptors the constructor would upload, handed to `sink` instead; needs no device
+    static void describe(WavelengthGrid* lambdagrid, StellarSystem* ss, DustSystem* ds, InstrumentSystem* is,
+                         GpuDescriptorSink& sink);
+
     // Describes the set-up simulation items to the engine on HIP device `device` (one engine per process;
     // the MPI rank picks its GPU). ds may be null (no dust system).
     GpuPhotonEngine(WavelengthGrid* lambdagrid, StellarSystem* ss, DustSystem* ds, InstrumentSystem* is,
@@ -71,6 +88,10 @@ public:
     void sumOnDevices(void* ncclComm, int rank);
 
 private:
+    // describe(): the items only, no engine context
+    GpuPhotonEngine(WavelengthGrid* lambdagrid, StellarSystem* ss, DustSystem* ds, InstrumentSystem* is,
+                    GpuDescriptorSink* sink);
+    void describeAll();
     void check(int rc) const;
     void describeGrid();
     void describeMedia();
@@ -85,6 +106,7 @@ private:
     DustSystem* _ds;
     InstrumentSystem* _is;
     SkirtMcrt* _ctx{nullptr};
+    GpuDescriptorSink* _sink{nullptr};  // where describeAll() sends the descriptors (the engine upload by default)
     SkirtVoronoi* _voronoi{nullptr};
     struct SkirtRccl* _rccl{nullptr};  // sumOnDevices
     int _sumRank{0};

@@ -17,7 +17,7 @@ REF=${SKIRT_REFERENCE:-/root/reference}
 QT=${QT_INCLUDE:-/opt/conda/include/qt}
 WORK=${1:-$(mktemp -d)}
 mkdir -p "$WORK/overlay"
-FRIENDS="DustMix TreeDustGrid TreeNode VoronoiDustGrid SersicGeometry SersicFunction FullInstrument SimpleInstrument FrameInstrument SEDInstrument"
+FRIENDS="DustMix TreeDustGrid TreeNode VoronoiDustGrid SersicGeometry SersicFunction PlummerGeometry ExpDiskGeometry FullInstrument SimpleInstrument FrameInstrument SEDInstrument"
 for cls in $FRIENDS; do
   src="$REF/SKIRTcore/$cls.hpp"
   [ -f "$src" ] || { echo "missing $src"; exit 1; }

@@ -70,7 +70,7 @@ ABI_SYMBOLS = [
     "skirt_host_voronoi_build", "skirt_host_voronoi_describe", "skirt_host_voronoi_free",
     "skirt_sim_load_ex", "skirt_mcrt_sample_density", "skirt_sim_density",
     "skirt_mcrt_set_crossed", "skirt_mcrt_download_crossed", "skirt_mcrt_column_densities",
-    "skirt_rccl_create", "skirt_rccl_wrap", "skirt_rccl_rank", "skirt_rccl_reducer", "skirt_rccl_destroy",
+    "skirt_rccl_create", "skirt_rccl_wrap", "skirt_rccl_rank", "skirt_rccl_reducer", "skirt_rccl_abort", "skirt_rccl_destroy", "skirt_sim_describe", "skirt_host_write_descriptors",
     "skirt_sim_run_devices", "skirt_mcrt_voronoi_cells", "skirt_host_voronoi_build_ex", "skirt_host_voronoi_cells",
 ]
 
@@ -126,6 +126,7 @@ def lib():
         L.skirt_sim_instrument.argtypes = [vp, c_int] + [ctypes.POINTER(c_int)] * 4
         L.skirt_sim_set_tallies.argtypes = [vp, ctypes.POINTER(c_dbl), ctypes.POINTER(c_dbl)]
         L.skirt_sim_write.argtypes = [vp, ctypes.c_char_p]
+        L.skirt_sim_describe.argtypes = [vp, ctypes.c_char_p]
         L.skirt_sim_error.restype = ctypes.c_char_p
         L.skirt_sim_free.argtypes = [vp]
         L.skirt_mcrt_stats.argtypes = [vp, ctypes.POINTER(SkirtStats)]
@@ -205,16 +206,28 @@ class Simulation:
     def run_stellar(self, first=0, count=0):
         self._check(lib().skirt_sim_run_stellar(self._h, first, count))
 
+    def _collective(self, check, rc):
+        """check(rc) for a call that may reach the reducer: when it fails on this rank, a reducer with an
+        abort() (TallyReducer) tells the other ranks at their next reduction, so that none waits for this
+        one in a collective (the reference's Parallel::call: the first failure stops every worker)"""
+        try:
+            check(rc)
+        except SkirtError as e:
+            fn = getattr(self, "_reducer_fn", None)
+            if fn is not None and hasattr(fn, "abort"):
+                fn.abort(str(e))
+            raise
+
     def run_stellar_shard(self, rank, world):
         """This rank's slice of every wavelength of the stellar phase (IdenticalAssigner); with world > 1
         the reducer (set_reducer) sums the stellar Labs at the phase end."""
-        self._check(lib().skirt_sim_run_stellar_shard(self._h, rank, world))
+        self._collective(self._check, lib().skirt_sim_run_stellar_shard(self._h, rank, world))
 
     def run_dust(self, rank=0, world=1):
         """Self-absorption cycles (if enabled) and the dust emission phase (PanMonteCarloSimulation::runSelf).
         With world > 1 this rank shoots its slice of every wavelength of every phase, and the reducer
         (set_reducer) sums the dust Labs after every self-absorption cycle."""
-        self._check(lib().skirt_sim_run_dust_shard(self._h, rank, world))
+        self._collective(self._check, lib().skirt_sim_run_dust_shard(self._h, rank, world))
 
     def set_reducer(self, fn):
         """fn(tally, device_ptr, n, hip_stream) sums the engine's device buffer over all processes in place
@@ -227,18 +240,18 @@ class Simulation:
 
         def cb(_user, tally, ptr, n, stream):
             try:
-                fn(tally, ptr, n, stream)
-                return 0
+                return 1 if fn(tally, ptr, n, stream) else 0  # a callable may return non-zero for a failure
             except Exception as e:  # noqa: BLE001 -- reported to the C side as a failed reduction
                 self.reducer_error = e
                 return 1
 
         self._reducer = REDUCE_FN(cb)  # kept alive as long as the engine may call it
+        self._reducer_fn = fn
         self._check_engine(lib().skirt_mcrt_set_reducer(self.engine, self._reducer, None))
 
     def reduce_instruments(self):
         """Instrument::sumResults: sums the instrument tallies over the processes (once per simulation)."""
-        self._check_engine(lib().skirt_mcrt_reduce_instruments(self.engine))
+        self._collective(self._check_engine, lib().skirt_mcrt_reduce_instruments(self.engine))
 
     def bind_dust_labs(self, ptr):
         """Make the engine accumulate the dust Labs in caller device memory (tally_sizes()[0] doubles)."""
@@ -258,8 +271,14 @@ class Simulation:
     def synchronize(self):
         self._check_engine(lib().skirt_mcrt_synchronize(self.engine))
 
+    def describe(self, path):
+        """Writes the descriptors attach() would upload (grid, media, sources, instruments) to `path` in the
+        canonical form of skirt_host_write_descriptors; no device needed (tests of the maintainer binding)."""
+        self._check(lib().skirt_sim_describe(self._h, os.fspath(path).encode()))
+
     def fetch(self):
-        self._check(lib().skirt_sim_fetch(self._h))
+        """waits and copies the tallies to the host (summing the instruments over the ranks first)"""
+        self._collective(self._check, lib().skirt_sim_fetch(self._h))
 
     def set_crossed(self, bins=16384):
         """Turn on DustSystem's cells-crossed histogram (writeCellsCrossed) for the following phases:

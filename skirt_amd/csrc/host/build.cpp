@@ -1179,10 +1179,11 @@ void buildOctree(const Ctx& c, const XmlElement* e, const Model& model, OctreeGr
             t.cellnumber[l] = (int)t.idv.size();
             t.idv.push_back(l);
         }
-    // neighbor lists (always built: the device engine uses them whatever the search method)
+    // neighbor lists, for the Neighbor search only, as the reference builds them (TreeDustGrid.cpp:158-163):
+    // the TopDown and Bookkeeping walks (engine and oracle) never read them; empty lists otherwise
     tb.hasLists.assign(Nnodes, 0);
     tb.nb.assign(6 * (size_t)Nnodes, {});
-    for (int l = 0; l < Nnodes; l++) {
+    for (int l = 0; l < Nnodes && t.search == 1; l++) {
         if (binary) tb.addneighborsBin(l);
         else tb.addneighbors(l);
     }
@@ -1267,6 +1268,8 @@ Instrument parseInstrument(const Ctx& c, const XmlElement* e) {
         ins.ypmin = ins.yc - 0.5 * ins.fovy;
         ins.ypmax = ins.yc + 0.5 * ins.fovy;
         ins.ypsiz = ins.fovy / ins.Ny;
+    } else {
+        ins.Nx = ins.Ny = 0;  // an SEDInstrument has no frame (SEDInstrument.cpp)
     }
     if (ins.kind == InstrumentKind::Full) ins.scatteringLevels = attrInt(e, "scatteringLevels", 0);
     return ins;

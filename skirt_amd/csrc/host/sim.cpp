@@ -208,15 +208,25 @@ int skirt_sim_set_photon_seed(SkirtSim* s, uint64_t seed) {
     return SKIRT_OK;
 }
 
-int skirt_sim_attach(SkirtSim* s, int device) {
-    if (!s) return SKIRT_ERR_ARG;
-    if (s->eng) { skirt_mcrt_destroy(s->eng); s->eng = nullptr; }
-    int rc = skirt_mcrt_create(device, &s->eng);
-    if (rc) { g_err = "cannot create the engine on device " + std::to_string(device); return rc; }
-    const Model& m = s->m;
-    int Nl = m.wl.n();
+}  // extern "C"
+
+namespace {
+// The descriptors skirt_sim_attach uploads (and skirt_sim_describe writes), over the model's arrays
+struct Descs {
+    bool hasGrid = false;
+    SkirtGridDesc g{};
+    SkirtMediaDesc md{};
+    SkirtSourceDesc sd{};
+    std::vector<SkirtInstrDesc> ids;
+    std::vector<double> kext, ksca, alb, gg, gp, lum, cdf, gt;
+    std::vector<int> gk;
+};
+
+void buildDescs(const Model& m, Descs& d) {
+    const int Nl = m.wl.n();
     if (m.hasDust) {
-        SkirtGridDesc g{};
+        d.hasGrid = true;
+        SkirtGridDesc& g = d.g;
         g.ncells = m.ncells();
         if (m.grid.kind == GridKind::Voronoi) {
             const VoronoiGrid& v = m.grid.vor;
@@ -248,52 +258,68 @@ int skirt_sim_attach(SkirtSim* s, int device) {
             g.eps = t.eps;
             g.search = t.search == 0 ? SKIRT_TREE_TOPDOWN : t.search == 2 ? SKIRT_TREE_BOOKKEEPING : SKIRT_TREE_NEIGHBOR;
         }
-        if ((rc = check(s, skirt_mcrt_upload_grid(s->eng, &g)))) return rc;
-        int nc = m.ncomp();
-        std::vector<double> kext(nc * Nl), ksca(nc * Nl), alb(nc * Nl), gg(nc * Nl);
+        const int nc = m.ncomp();
+        d.kext.resize(nc * Nl); d.ksca.resize(nc * Nl); d.alb.resize(nc * Nl); d.gg.resize(nc * Nl);
         for (int h = 0; h < nc; h++)
             for (int ell = 0; ell < Nl; ell++) {
-                kext[h * Nl + ell] = m.dust[h].mix.kext[ell];
-                ksca[h * Nl + ell] = m.dust[h].mix.ksca[ell];
-                alb[h * Nl + ell] = m.dust[h].mix.albedo[ell];
-                gg[h * Nl + ell] = m.dust[h].mix.g[ell];
+                d.kext[h * Nl + ell] = m.dust[h].mix.kext[ell];
+                d.ksca[h * Nl + ell] = m.dust[h].mix.ksca[ell];
+                d.alb[h * Nl + ell] = m.dust[h].mix.albedo[ell];
+                d.gg[h * Nl + ell] = m.dust[h].mix.g[ell];
             }
-        SkirtMediaDesc md{m.ncells(), nc, Nl, m.rho.data(), kext.data(), ksca.data(), alb.data(), gg.data()};
-        if ((rc = check(s, skirt_mcrt_upload_media(s->eng, &md)))) return rc;
+        d.md = SkirtMediaDesc{m.ncells(), nc, Nl, m.rho.data(), d.kext.data(), d.ksca.data(), d.alb.data(), d.gg.data()};
     }
-    int ns = (int)m.starL.size();
-    std::vector<int> gk(ns, SKIRT_GEOM_PLUMMER);
-    std::vector<double> gp(8 * ns, 0.0), lum(ns * Nl), cdf(Nl * (ns + 1)), gt;
+    const int ns = (int)m.starL.size();
+    d.gk.assign(ns, SKIRT_GEOM_PLUMMER);
+    d.gp.assign(8 * ns, 0.0);
+    d.lum.resize(ns * Nl);
+    d.cdf.resize(Nl * (ns + 1));
     for (int h = 0; h < ns; h++) {
         const Geometry& g = m.starGeom[h];
-        gk[h] = packGeometry(g, &gp[8 * h]);
+        d.gk[h] = packGeometry(g, &d.gp[8 * h]);
         if (g.kind == GeometryKind::Sersic) {
-            gt.resize(202 * (size_t)ns, 0.0);
+            d.gt.resize(202 * (size_t)ns, 0.0);
             for (int q = 0; q < 101; q++) {
-                gt[202 * (size_t)h + q] = g.sv[q];
-                gt[202 * (size_t)h + 101 + q] = g.Mv[q];
+                d.gt[202 * (size_t)h + q] = g.sv[q];
+                d.gt[202 * (size_t)h + 101 + q] = g.Mv[q];
             }
         }
-        for (int ell = 0; ell < Nl; ell++) lum[h * Nl + ell] = m.starL[h][ell];
+        for (int ell = 0; ell < Nl; ell++) d.lum[h * Nl + ell] = m.starL[h][ell];
     }
     for (int ell = 0; ell < Nl; ell++)
-        for (int q = 0; q <= ns; q++) cdf[ell * (ns + 1) + q] = m.starX[ell][q];
-    SkirtSourceDesc sd{ns, Nl, gk.data(), gp.data(), lum.data(), m.starLtot.data(), cdf.data(), m.starEmissionBias,
-                       gt.empty() ? nullptr : gt.data()};
-    if ((rc = check(s, skirt_mcrt_upload_sources(s->eng, &sd)))) return rc;
-    std::vector<SkirtInstrDesc> ids;
+        for (int q = 0; q <= ns; q++) d.cdf[ell * (ns + 1) + q] = m.starX[ell][q];
+    d.sd = SkirtSourceDesc{ns, Nl, d.gk.data(), d.gp.data(), d.lum.data(), m.starLtot.data(), d.cdf.data(),
+                           m.starEmissionBias, d.gt.empty() ? nullptr : d.gt.data()};
     for (const Instrument& ins : m.instruments) {
-        SkirtInstrDesc d{};
-        d.kind = (int)ins.kind;
-        d.nx = ins.Nx; d.ny = ins.Ny;
-        d.scattering_levels = ins.scatteringLevels;
-        for (int q = 0; q < 3; q++) d.kobs[q] = ins.kobs[q];
-        d.sinphi = ins.sinphi; d.cosphi = ins.cosphi; d.sintheta = ins.sintheta; d.costheta = ins.costheta;
-        d.sinpa = ins.sinpa; d.cospa = ins.cospa;
-        d.xpmin = ins.xpmin; d.xpsiz = ins.xpsiz; d.ypmin = ins.ypmin; d.ypsiz = ins.ypsiz;
-        ids.push_back(d);
+        SkirtInstrDesc x{};
+        x.kind = (int)ins.kind;
+        x.nx = ins.Nx; x.ny = ins.Ny;
+        x.scattering_levels = ins.scatteringLevels;
+        for (int q = 0; q < 3; q++) x.kobs[q] = ins.kobs[q];
+        x.sinphi = ins.sinphi; x.cosphi = ins.cosphi; x.sintheta = ins.sintheta; x.costheta = ins.costheta;
+        x.sinpa = ins.sinpa; x.cospa = ins.cospa;
+        x.xpmin = ins.xpmin; x.xpsiz = ins.xpsiz; x.ypmin = ins.ypmin; x.ypsiz = ins.ypsiz;
+        d.ids.push_back(x);
     }
-    if ((rc = check(s, skirt_mcrt_set_instruments(s->eng, ids.data(), (int)ids.size())))) return rc;
+}
+}  // namespace
+
+extern "C" {
+
+int skirt_sim_attach(SkirtSim* s, int device) {
+    if (!s) return SKIRT_ERR_ARG;
+    if (s->eng) { skirt_mcrt_destroy(s->eng); s->eng = nullptr; }
+    int rc = skirt_mcrt_create(device, &s->eng);
+    if (rc) { g_err = "cannot create the engine on device " + std::to_string(device); return rc; }
+    const Model& m = s->m;
+    Descs d;
+    buildDescs(m, d);
+    if (d.hasGrid) {
+        if ((rc = check(s, skirt_mcrt_upload_grid(s->eng, &d.g)))) return rc;
+        if ((rc = check(s, skirt_mcrt_upload_media(s->eng, &d.md)))) return rc;
+    }
+    if ((rc = check(s, skirt_mcrt_upload_sources(s->eng, &d.sd)))) return rc;
+    if ((rc = check(s, skirt_mcrt_set_instruments(s->eng, d.ids.data(), (int)d.ids.size())))) return rc;
     size_t nl = 0, ni = 0;
     skirt_mcrt_tally_sizes(s->eng, &nl, &ni);
     // the device tally pads each frame pixel's slots to a 64-byte line; downloads restore this layout
@@ -301,6 +327,18 @@ int skirt_sim_attach(SkirtSim* s, int device) {
     // DustSystem writeCellsCrossed: the engine keeps the cells-crossed histogram for ds_crossed
     if (m.hasDust && m.writeCellsCrossed && (rc = check(s, skirt_mcrt_set_crossed(s->eng, kCrossedBins + 1)))) return rc;
     return check(s, skirt_mcrt_zero_tallies(s->eng));
+}
+
+int skirt_sim_describe(SkirtSim* s, const char* path) {
+    if (!s || !path) return SKIRT_ERR_ARG;
+    Descs d;
+    buildDescs(s->m, d);
+    if (FILE* f = std::fopen(path, "wb")) std::fclose(f);  // the writer appends
+    else { g_err = std::string("cannot write ") + path; return SKIRT_ERR_ARG; }
+    int rc = skirt_host_write_descriptors(path, d.hasGrid ? &d.g : nullptr, d.hasGrid ? &d.md : nullptr, &d.sd,
+                                          d.ids.data(), (int)d.ids.size());
+    if (rc) g_err = std::string("cannot write ") + path;
+    return rc;
 }
 
 SkirtMcrt* skirt_sim_engine(SkirtSim* s) { return s ? s->eng : nullptr; }
