@@ -482,6 +482,13 @@ constexpr size_t kCrossedBins = 1 << 16;
 static std::atomic<bool> g_engineAttenuation{false};
 static bool engineAttenuation() { return g_engineAttenuation.load(std::memory_order_relaxed); }
 
+// diagnostic (tools/parity_trace.py): ORACLE_DEBUG_FILL=1 prints every storing one-component FILL path (start,
+// direction, luminosity) and its dust segments (cell, ds, dtau, Labs add) to stdout; run single-threaded
+static bool debugFill() {
+    static const bool on = getenv("ORACLE_DEBUG_FILL") && atoi(getenv("ORACLE_DEBUG_FILL")) != 0;
+    return on;
+}
+
 // study hook (oracle_set_fill_hook): the cells of every storing FILL path
 static OracleFillHook g_fillHook = nullptr;
 static void* g_fillUser = nullptr;
@@ -692,6 +699,9 @@ public:
                     int N = (int)p.v.size();
                     const bool product = engineAttenuation();
                     double att = 1.0;  // (product mode) exp(-taustart) as the running product
+                    if (debugFill())
+                        printf("O L %d %.17g %.17g %.17g %.17g %.17g %.17g %.17g\n", pp.ell, pp.r.x, pp.r.y, pp.r.z,
+                               pp.k.x, pp.k.y, pp.k.z, L);
                     for (int n = 0; n < N; n++) {
                         int m = p.v[n].m;
                         if (m != -1) {
@@ -700,6 +710,7 @@ public:
                             double Lintm = L * (product ? att : exp(-taustart)) * expfactorm;
                             att = att * (1.0 - expfactorm);
                             double Labsm = (1.0 - albedo) * Lintm;
+                            if (debugFill()) printf("O S %d %.17g %.17g %.17g\n", m, p.v[n].ds, p.v[n].dtau, Labsm);
                             t.add(*labs, (size_t)m * Nl + pp.ell, Labsm);
                             counts().absorbs++;
                         }
