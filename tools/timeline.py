@@ -1,4 +1,4 @@
-"""Overlap analysis of a rocprofv3 kernel trace (tools/archive/gpu_timeline.sh): per kernel busy time, the
+"""Overlap analysis of a rocprofv3 kernel trace (a kernel trace, e.g. rocprofv3 --kernel-trace): per kernel busy time, the
 union of busy intervals, and how much of the last timed phase two kernels overlapped."""
 import csv
 import glob
