@@ -474,13 +474,22 @@ inline void lockFreeAdd(double* p, double v) {
 
 constexpr size_t kCrossedBins = 1 << 16;
 
-// Test switch (oracle_set_engine_attenuation): exp(-tau_{n-1}) of the absorption sum as the GPU engine did until round 3
-// carries it, the running product of 1 - (-expm1(-dtau)) over the path's dust segments, instead of the
-// reference's exp(-taustart) per segment (MonteCarloSimulation.cpp:458-462). The two part in the last digits
-// only behind optically thick segments, where 1 - (1 - exp(-dtau)) cancels; tests/test_gpu_parity.py uses
-// the switch to show that this is the whole of the engine's deep-cell differences on thick models.
-static std::atomic<bool> g_engineAttenuation{false};
-static bool engineAttenuation() { return g_engineAttenuation.load(std::memory_order_relaxed); }
+// Test switch (oracle_set_engine_attenuation): how exp(-tau_{n-1}) of the absorption sum is evaluated.
+//   0 the reference's exp(-taustart) per segment (MonteCarloSimulation.cpp:458-462), the default;
+//   1 the running product of 1 - (-expm1(-dtau)) over the path's dust segments, as the GPU engine carried it
+//     until round 3. It parts from 0 in the last digits only behind optically thick segments, where
+//     1 - (1 - exp(-dtau)) cancels: tests/test_attenuation.py shows that this was the whole of the engine's
+//     deep-cell differences on thick models then;
+//   2 the engine's carry since round 5 (Tracer::segment, engine.hip): f <- f - f * (-expm1(-dtau)) while
+//     dtau < 0.5 (kCarryTau), exp(-tau_n) evaluated anew after a thicker segment.
+static std::atomic<int> g_engineAttenuation{0};
+static int engineAttenuation() { return g_engineAttenuation.load(std::memory_order_relaxed); }
+constexpr double kEngineCarryTau = 0.5;  // engine.hip kCarryTau
+// the next segment's exp(-tau_{n-1}) factor after segment n (dtau, cumulative tau), in mode `mode`
+static inline double nextAttenuation(int mode, double att, double expfactorm, double dtau, double tau) {
+    if (mode == 2) return dtau < kEngineCarryTau ? att - att * expfactorm : exp(-tau);
+    return att * (1.0 - expfactorm);
+}
 
 // diagnostic (tools/parity_trace.py): ORACLE_DEBUG_FILL=1 prints every storing one-component FILL path (start,
 // direction, luminosity) and its dust segments (cell, ds, dtau, Labs add) to stdout; run single-threaded
@@ -697,8 +706,8 @@ public:
                 double expfactor = -expm1(-taupath);
                 if (store) {
                     int N = (int)p.v.size();
-                    const bool product = engineAttenuation();
-                    double att = 1.0;  // (product mode) exp(-taustart) as the running product
+                    const int mode = engineAttenuation();
+                    double att = 1.0;  // (modes 1, 2) exp(-taustart) as the engine carries it
                     if (debugFill())
                         printf("O L %d %.17g %.17g %.17g %.17g %.17g %.17g %.17g\n", pp.ell, pp.r.x, pp.r.y, pp.r.z,
                                pp.k.x, pp.k.y, pp.k.z, L);
@@ -707,8 +716,8 @@ public:
                         if (m != -1) {
                             double taustart = (n == 0) ? 0.0 : p.v[n - 1].tau;
                             double expfactorm = -expm1(-p.v[n].dtau);
-                            double Lintm = L * (product ? att : exp(-taustart)) * expfactorm;
-                            att = att * (1.0 - expfactorm);
+                            double Lintm = L * (mode ? att : exp(-taustart)) * expfactorm;
+                            att = nextAttenuation(mode, att, expfactorm, p.v[n].dtau, p.v[n].tau);
                             double Labsm = (1.0 - albedo) * Lintm;
                             if (debugFill()) printf("O S %d %.17g %.17g %.17g\n", m, p.v[n].ds, p.v[n].dtau, Labsm);
                             t.add(*labs, (size_t)m * Nl + pp.ell, Labsm);
@@ -720,7 +729,7 @@ public:
             } else {
                 double Lsca = 0.0;
                 int N = (int)p.v.size();
-                const bool product = engineAttenuation();
+                const int mode = engineAttenuation();
                 double att = 1.0;
                 for (int n = 0; n < N; n++) {
                     int m = p.v[n].m;
@@ -734,8 +743,8 @@ public:
                         double albedo = (kext > 0.0) ? ksca / kext : 0.0;
                         double taustart = (n == 0) ? 0.0 : p.v[n - 1].tau;
                         double expfactorm = -expm1(-p.v[n].dtau);
-                        double Lintm = L * (product ? att : exp(-taustart)) * expfactorm;
-                        att = att * (1.0 - expfactorm);
+                        double Lintm = L * (mode ? att : exp(-taustart)) * expfactorm;
+                        att = nextAttenuation(mode, att, expfactorm, p.v[n].dtau, p.v[n].tau);
                         Lsca += albedo * Lintm;
                         if (store) {
                             t.add(*labs, (size_t)m * Nl + pp.ell, (1.0 - albedo) * Lintm);
@@ -962,7 +971,7 @@ extern "C" {
 
 const char* oracle_last_error(void) { return g_error.c_str(); }
 
-void oracle_set_engine_attenuation(int on) { g_engineAttenuation = on != 0; }
+void oracle_set_engine_attenuation(int mode) { g_engineAttenuation = (mode == 1 || mode == 2) ? mode : 0; }
 
 void oracle_set_fill_hook(OracleFillHook hook, void* user) {
     g_fillUser = user;

@@ -106,9 +106,11 @@ void oracle_counts(OracleRun* r, uint64_t out[3]);
 int oracle_crossed(OracleRun* r, const uint64_t** hist);
 void oracle_free(OracleRun* r);
 
-/* test switch: with on != 0 the absorption sums evaluate exp(-tau_{n-1}) as the GPU engine does, as the
- * running product of 1 - (-expm1(-dtau)) along the path, instead of the reference's exp(-taustart) */
-void oracle_set_engine_attenuation(int on);
+/* test switch: how the absorption sums evaluate exp(-tau_{n-1}). 0: the reference's exp(-taustart) per segment
+ * (default); 1: the running product of 1 - (-expm1(-dtau)) along the path, as the GPU engine did until round 3;
+ * 2: the engine's carry since round 5, f - f * (-expm1(-dtau)) while dtau < 0.5, exp(-tau) anew behind a
+ * thicker segment */
+void oracle_set_engine_attenuation(int mode);
 
 /* study hook (tools/labs_locality.cpp): called, from the worker threads, for every FILL path that stores
  * absorption, with the packet's wavelength, start position and direction, and the reference cell numbers

@@ -322,26 +322,39 @@ void buildVoronoi(VoronoiGrid& g, const std::vector<double>& sites, double xmin,
         g.centroid[3 * (size_t)i + 1] = vol > 0 ? cy / vol : s[1];
         g.centroid[3 * (size_t)i + 2] = vol > 0 ? cz / vol : s[2];
     };
-    // the cells on the device first (where they fit its capacities); the host builds the rest
+    // the cells on the device first (where they fit its capacities); the host builds the rest. The device
+    // returns up to kIds neighbour ids per cell in one N x kIds table on each side (1e7 sites: 3.8 GB), so
+    // tessellations above kMaxDeviceSites stay on the host, and so does one whose device run fails (e.g. its
+    // work areas do not fit): the host's cells are the same, bit for bit
     std::vector<int> todo;
-    if (cells) {
-        constexpr int kIds = 96;  // neighbour ids per cell the device returns
-        std::vector<int> ids((size_t)N * kIds), nids(N);
-        const double box[6] = {xmin, ymin, zmin, xmax, ymax, zmax};
-        (*cells)(sites, box, tree.nodes(), tree.perm(), kIds, ids.data(), nids.data(), g.bbox.data(), g.volume.data(),
-                 g.centroid.data());
-        for (int i = 0; i < N; i++) {
-            if (nids[i] < 0 || nids[i] > kIds) {
-                todo.push_back(i);
-                continue;
+    constexpr int kIds = 96;                    // neighbour ids per cell the device returns
+    constexpr int kMaxDeviceSites = 4 << 20;    // 1.6 GB of ids on each side
+    bool onDevice = false;
+    if (cells && N <= kMaxDeviceSites) {
+        try {
+            std::vector<int> ids((size_t)N * kIds), nids(N);
+            const double box[6] = {xmin, ymin, zmin, xmax, ymax, zmax};
+            (*cells)(sites, box, tree.nodes(), tree.perm(), kIds, ids.data(), nids.data(), g.bbox.data(),
+                     g.volume.data(), g.centroid.data());
+            for (int i = 0; i < N; i++) {
+                if (nids[i] < 0 || nids[i] > kIds) {
+                    todo.push_back(i);
+                    continue;
+                }
+                cellIds[i].assign(ids.begin() + (size_t)i * kIds, ids.begin() + (size_t)i * kIds + nids[i]);
             }
-            cellIds[i].assign(ids.begin() + (size_t)i * kIds, ids.begin() + (size_t)i * kIds + nids[i]);
+            onDevice = true;
+        } catch (std::exception& e) {
+            std::fprintf(stderr, "Voronoi cells on the device failed (%s): every cell on the host\n", e.what());
+            todo.clear();
+            for (auto& c : cellIds) c.clear();
         }
-    } else {
+    }
+    if (!onDevice) {
         todo.resize(N);
         for (int i = 0; i < N; i++) todo[i] = i;
     }
-    if (cells) stage("device cells");
+    if (onDevice) stage("device cells");
     if (hostCells) *hostCells = (int)todo.size();
     {
         const int T = std::max(1, std::min(16, (int)std::thread::hardware_concurrency()));

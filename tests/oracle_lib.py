@@ -99,11 +99,16 @@ class OracleResult:
 
 
 class engine_attenuation:
-    """Context: the oracle evaluates the absorption's exp(-tau_{n-1}) as a running product (the engine's form
-    until round 3, see oracle_set_engine_attenuation), to separate that arithmetic from everything else."""
+    """Context: the oracle evaluates the absorption's exp(-tau_{n-1}) as the engine does or did, to separate
+    that arithmetic from everything else (oracle_set_engine_attenuation): mode 1 the running product of the
+    engine until round 3, mode 2 the engine's carry since round 5 (the product while dtau < 0.5, exp(-tau)
+    anew behind a thicker segment)."""
+
+    def __init__(self, mode=1):
+        self.mode = mode
 
     def __enter__(self):
-        lib().oracle_set_engine_attenuation(1)
+        lib().oracle_set_engine_attenuation(self.mode)
 
     def __exit__(self, *exc):
         lib().oracle_set_engine_attenuation(0)
