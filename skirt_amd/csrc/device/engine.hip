@@ -4218,6 +4218,13 @@ static int runPhase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, uint6
     // (the queue holds kPathCap peel-offs per instrument and slot: the slots shrink with the instruments)
     if (continuous) slots = std::min(slots, std::max(64, kContSlots / std::max(1, (int)c->instr.size())));
     if ((uint64_t)slots > count) slots = (int)count;
+    // experiment (round 6): a phase that fits the pool runs its packets in lockstep (all FILL rays in one launch,
+    // then all WALK rays ...); SKIRT_AMD_POOL_DIV = d admits them d waves at a time instead
+    if (const char* pd = getenv("SKIRT_AMD_POOL_DIV")) {
+        const int d = atoi(pd);
+        if (d > 1 && (uint64_t)slots >= count) slots = std::max(64 * 1024, (int)(count / (uint64_t)d));
+        if ((uint64_t)slots > count) slots = (int)count;
+    }
     const int halves = (continuous || !p->has_dust || slots < 2 * 64 * kMaxHalves) ? 1 : c->halves;
     slots = std::max(slots, 64 * halves) / halves;  // per half
     const bool forked = c->halves > 1 || c->cusT || c->cusE;  // the pipeline runs on the owned streams
