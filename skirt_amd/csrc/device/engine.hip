@@ -202,6 +202,13 @@ constexpr int kVorUnroll = 4;
 // (profiles/r04_vor_groups4.txt). Measured and removed (git history): the neighbour-parallel drain step
 // (profiles/r03_vor_wide.txt), the drain split around the step's loads (profiles/r04_c4_variants.txt).
 constexpr int kVorGroups = 4;
+// round 6: the entry groups past a cell's first kVorGroups shared out over the wave (Grid<VORONOI>::stepCoop);
+// -DSKIRT_VOR_SHARE=0 builds the lane-serial step for A/B runs
+#ifndef SKIRT_VOR_SHARE
+#define SKIRT_VOR_SHARE 1
+#endif
+constexpr bool kVorShare = SKIRT_VOR_SHARE != 0;
+constexpr int kVorShareWords = 64 * 5;  // per wave in LDS: 64 item -> owner entries, 64 partial Bests of 4 words
 constexpr int kVorFallbackGroup = 2;  // neighbour sites loaded together by the exact re-evaluation (<= kVorUnroll)
 constexpr int kVorCand = 4;  // possible winners the exact re-evaluation collects before it takes the whole list
 // slots after the last cell's block: a step loads whole groups of entries past its list
@@ -1378,6 +1385,117 @@ struct Grid<SKIRT_GRID_VORONOI> {
         return decide(a, r, s, b, seg);
     }
 
+    // One step with the entry groups past the first kVorGroups shared out over the wave (round 6, VERDICT r5
+    // item 4). stepRest makes a wave run as many groups of kVorUnroll entries as its lane with the most
+    // neighbours needs (C4: 6.4 groups for a mean of 3.9). Here every lane bounds its own first kVorGroups
+    // groups (the 16 entries loaded with the header), and the groups beyond them are items handed out one
+    // per lane, ray or no ray (C4: 28 items per wave on average, so one round instead of 2.4): the taker
+    // bounds the owner's kVorUnroll entries with the owner's operands, fetched lane to lane, into a partial
+    // Best in LDS, and the owner merges its partials in list order. U and the two least lower bounds do not
+    // depend on the order of the entries, and w1, the first least lower bound in list order, is kept by the
+    // merge (strict <, groups in list order), so every decision is stepRest's, bit for bit. Every lane of the
+    // wave calls it (act: the lane has a ray); share: the wave's kVorShareWords of LDS.
+    template <class SegFn>
+    __device__ static __forceinline__ bool stepCoop(const Args& a, Ray& r, bool act, int* share, SegFn seg) {
+        constexpr int U = kVorUnroll;
+        constexpr int OWN = kVorGroups * kVorUnroll;
+        const int lane = threadIdx.x & 63;
+        int* map = share;                                        // item -> owner | group << 8
+        float* part = reinterpret_cast<float*>(share + 64);      // [item][U, L1, L2, w1]
+        Load L;
+        stepLoad(a, r, L, act);
+        StepIn s{};
+        s.B = a.vorSlots + (act ? r.cj : 0);
+        Best b{FLT_MAX, FLT_MAX, FLT_MAX, 0};
+        bool alive = false;
+        if (act) alive = headFrom(a, r, s, L.h0, L.h1, L.h2, seg);
+        const int cnt = alive ? s.cnt : 0;
+        // the groups past the own ones, and their item numbers (a prefix sum over the wave)
+        const int extra = cnt > OWN ? (cnt - OWN + U - 1) / U : 0;
+        int incl = extra;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const int t = __shfl_up(incl, d);
+            if (lane >= d) incl += t;
+        }
+        const int total = __shfl(incl, 63);
+        const int start = incl - extra;
+        auto own = [&](int gi) {
+            if (alive && gi * U < cnt) {
+#pragma unroll
+                for (int u = 0; u < U; u++) {
+                    float lo, uc;
+                    bounds(s, L.g[gi][u], true, lo, uc);
+                    take(b, lo, uc, L.g[gi][u].next);
+                }
+            }
+        };
+        // a round of items [base, base + 64): owners list them, each lane takes item base + lane
+        StepIn so{};
+        VorEntry e[U];
+        bool has = false;
+        auto setup = [&](int base) {
+            for (int k = 0; k < extra; k++) {
+                const int it = start + k - base;
+                if (it >= 0 && it < 64) map[it] = lane | (k << 8);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            has = base + lane < total;
+            const int m = has ? map[lane] : 0;
+            const int o = m & 63, k = m >> 8;
+            so.Dx = __shfl(s.Dx, o); so.Dy = __shfl(s.Dy, o); so.Dz = __shfl(s.Dz, o);
+            so.fkx = __shfl(s.fkx, o); so.fky = __shfl(s.fky, o); so.fkz = __shfl(s.fkz, o);
+            so.eA = __shfl(s.eA, o); so.eB2 = __shfl(s.eB2, o);
+            so.eA2 = 2.0f * so.eA;
+            const int cj = __shfl(act ? r.cj : 0, o);
+            if (has) vorEntries(a.vorSlots + cj, OWN + k * U, e);
+        };
+        auto compute = [&](int base) {
+            Best p{FLT_MAX, FLT_MAX, FLT_MAX, 0};
+            if (has) {
+#pragma unroll
+                for (int u = 0; u < U; u++) {
+                    float lo, uc;
+                    bounds(so, e[u], true, lo, uc);
+                    take(p, lo, uc, e[u].next);
+                }
+            }
+            part[4 * lane] = p.U; part[4 * lane + 1] = p.L1; part[4 * lane + 2] = p.L2;
+            part[4 * lane + 3] = __int_as_float(p.w1);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            // the owner's partials of this round, in list order
+            for (int k = 0; k < extra; k++) {
+                const int it = start + k - base;
+                if (it < 0 || it >= 64) continue;
+                const float pU = part[4 * it], pL1 = part[4 * it + 1], pL2 = part[4 * it + 2];
+                const int pw1 = __float_as_int(part[4 * it + 3]);
+                b.U = fminf(b.U, pU);
+                const float L2 = fminf(fmaxf(b.L1, pL1), fminf(b.L2, pL2));  // the second least of both pairs
+                b.w1 = pL1 < b.L1 ? pw1 : b.w1;
+                b.L1 = fminf(b.L1, pL1);
+                b.L2 = L2;
+            }
+            // (the map and partials are rewritten by the next round only after every lane has read them)
+            __builtin_amdgcn_wave_barrier();
+        };
+        own(0);
+        own(1);
+        if (total > 0) setup(0);  // its loads arrive while the last own groups are bounded
+        own(2);
+        own(3);
+        if (total > 0) compute(0);
+        for (int base = 64; base < total; base += 64) {
+            setup(base);
+            compute(base);
+        }
+        if (!alive) return false;
+        return decide(a, r, s, b, seg);
+    }
+
     __device__ static __forceinline__ int whichcell(const Args& a, const Shared&, double x, double y, double z) {
         return cellIndex(a, x, y, z);
     }
@@ -1428,6 +1546,7 @@ struct Tracer {
     unsigned labsOob = 0;             // a byte offset past every replica: the empty lanes' adds are dropped
     int npend = 0;
     unsigned gstep = 0;  // grid steps of the wave (drainStep's round robin)
+    int* share = nullptr;  // Voronoi: the wave's LDS for the shared entry groups (stepCoop)
 
     __device__ __forceinline__ void drain() {
         static_assert(kLabsBuf >= 2 && kLabsBuf <= 64 && (kLabsBuf & (kLabsBuf - 1)) == 0, "kLabsBuf: power of 2");
@@ -1451,6 +1570,7 @@ struct Tracer {
         const int n = __shfl(npend, src);
         const int q = j * kBlock + wbase + src;
         const unsigned idx = pendIdx[q];
+#ifndef SKIRT_EXPERIMENT_NO_LABS_STATS  // (timing-only experiment, round 6: the statistics' share of the drain)
         // the requests of this instruction: a lane starts one unless the lane before it (the same
         // ray's previous add) hit the same 64-byte line
         const unsigned line = (unsigned)(reinterpret_cast<size_t>(a.labs + idx) >> 6);
@@ -1458,6 +1578,7 @@ struct Tracer {
         const unsigned long long starts = __ballot(j < n && (j == 0 || prev != line));
         absorbs += (unsigned)__popcll(__ballot(j < n));
         requests += (unsigned)__popcll(starts);
+#endif
         if (a.labsGlobal) {  // a table of 4 GiB or more (wave-uniform): global atomics
             if (j < n) atomicAddF64(a.labs + idx, pendVal[q]);
         } else {
@@ -1960,6 +2081,10 @@ __device__ __forceinline__ void traceBody(const Args& a) {
     T.waveSegs = reinterpret_cast<unsigned*>(lds + a.ldsInstrOff);
     T.pendVal = lds + a.ldsInstrOff + kSegWords;
     T.pendIdx = reinterpret_cast<unsigned*>(T.pendVal + kLabsBuf * kBlock);
+    if constexpr (GRID == SKIRT_GRID_VORONOI && kVorShare) {  // after the Labs buffers (STORE) or the counts
+        int* base = STORE ? reinterpret_cast<int*>(T.pendIdx + kLabsBuf * kBlock) : reinterpret_cast<int*>(T.pendVal);
+        T.share = base + (threadIdx.x >> 6) * kVorShareWords;
+    }
     if (threadIdx.x < 3 * (kBlock / 64)) T.waveSegs[threadIdx.x] = 0;
     __syncthreads();
     const int lane = threadIdx.x & 63;
@@ -2004,7 +2129,14 @@ __device__ __forceinline__ void traceBody(const Args& a) {
             if (live == 0) break;
             T.laneSlots += 64;
             auto seg = [&](int m, double rho0, double ds) { return T.segment(r, m, rho0, ds); };
-            if (r.mode != RAY_NONE) {
+            if constexpr (GRID == SKIRT_GRID_VORONOI && kVorShare) {
+                // every lane steps together: the lanes without a ray take shared entry groups too
+                const bool act = r.mode != RAY_NONE;
+                if (!Grid<GRID>::stepCoop(a, r, act, T.share, seg) && act) {
+                    T.finish(r);
+                    r.mode = RAY_NONE;
+                }
+            } else if (r.mode != RAY_NONE) {
                 if (!Grid<GRID>::step(a, sh, r, seg)) {
                     T.finish(r);
                     r.mode = RAY_NONE;
@@ -4345,7 +4477,9 @@ static int runPhase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, uint6
                          !getenv("SKIRT_AMD_NO_NOSTORE");
     const size_t ldsTrace = (size_t)a.ldsInstrOff * sizeof(double)          // grid tables + optics
                             + (size_t)kSegWords * sizeof(double)                          // + segment counts
-                            + (noStore ? 0 : (size_t)kLabsBuf * kBlock * (sizeof(double) + sizeof(unsigned)));  // + Labs buffers
+                            + (noStore ? 0 : (size_t)kLabsBuf * kBlock * (sizeof(double) + sizeof(unsigned)))  // + Labs buffers
+                            + ((c->gridKind == SKIRT_GRID_VORONOI && kVorShare)  // + shared entry groups
+                                   ? (size_t)(kBlock / 64) * kVorShareWords * sizeof(int) : 0);
     const size_t ldsEvent = (size_t)a.ldsSedOff * sizeof(double);           // + instruments
     // budget: what one workgroup may allocate (160 KiB on gfx950). The trace and event kernels need their
     // tables; the detect kernel keeps as many SED copies as fit (8, 4, 2, 1), or none (SEDs to the tally)

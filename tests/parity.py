@@ -52,10 +52,58 @@ def outliers(a, b, rtol, floor=1e-15, drift=100.0):
     return int(out.sum()), int(near.sum()), float(rel.max() if rel.size else 0.0), float(mass), int(cmp.sum())
 
 
-def assert_parity(a, b, rtol, budget, label, mass=1e-12, floor=1e-15, drift=100.0, drift_budget=None):
+def cartesian_neighbour_scale(table, shape):
+    """For a Labs table (cells x wavelengths) of a Cartesian grid of shape (Nx, Ny, Nz), cell m = k + Nz j +
+    Nz Ny i (CartesianDustGrid.cpp:305-308): a function (cells, ells) -> the largest |value| of each element's
+    six face neighbours at the same wavelength (see `slivers` in assert_parity)."""
+    nx, ny, nz = shape
+    t = np.asarray(table)
+
+    def scale(cells, ells):
+        i, rem = np.divmod(cells, ny * nz)
+        j, k = np.divmod(rem, nz)
+        best = np.zeros(cells.size)
+        for di, dj, dk in ((1, 0, 0), (-1, 0, 0), (0, 1, 0), (0, -1, 0), (0, 0, 1), (0, 0, -1)):
+            ii, jj, kk = i + di, j + dj, k + dk
+            ok = (ii >= 0) & (ii < nx) & (jj >= 0) & (jj < ny) & (kk >= 0) & (kk < nz)
+            m = np.where(ok, kk + nz * jj + nz * ny * ii, 0)
+            best = np.maximum(best, np.where(ok, np.abs(t[m, ells]), 0.0))
+        return best
+    return scale
+
+
+def assert_parity(a, b, rtol, budget, label, mass=1e-12, floor=1e-15, drift=100.0, drift_budget=None,
+                  slivers=None):
     """Asserts at most `budget` outliers beyond drift x rtol, at most `drift_budget` (default 0.1 % of the
     compared elements) between rtol and drift x rtol (last-digit drift of long chains of segments), and
-    that all of them together carry at most `mass` of the table's total."""
+    that all of them together carry at most `mass` of the table's total.
+
+    slivers (a function (cells, ells) -> scale, e.g. cartesian_neighbour_scale): an element beyond rtol whose
+    difference is within rtol of that scale is a sliver, counted apart (at most 0.01 % of the compared
+    elements) instead of as an outlier. A ray that passes a cell's edge within a hair's breadth crosses it
+    over a sliver whose length is the difference of two nearly equal coordinates; the last-ulp differences
+    of the position (the engine's exit distances are (x_E - x) * (1/k), the reference's (x_E - x) / k, and
+    its launch directions come from other, equivalent formulas) then change the
+    sliver's length, and a cell that only that sliver reaches, by up to ulp(x) / length relative. The same
+    segment is a full crossing of the neighbouring cells, so its error is bounded relative to them
+    (profiles/r06_parity_trace.txt traces such a cell on the 128^3 Cartesian model)."""
+    if slivers is not None:
+        a2, b2 = np.asarray(a, dtype=np.float64), np.asarray(b, dtype=np.float64)
+        scale = np.maximum(np.abs(a2), np.abs(b2))
+        top = scale.max() if scale.size else 0.0
+        diff = np.abs(a2 - b2)
+        cand = np.argwhere((scale > floor * top) & (diff > rtol * scale))
+        nsl = 0
+        if cand.size:
+            nb = slivers(cand[:, 0], cand[:, 1])
+            sl = diff[cand[:, 0], cand[:, 1]] <= rtol * nb
+            nsl = int(sl.sum())
+            # the slivers compared as equal: the oracle's value in place of the engine's
+            a2 = a2.copy()
+            a2[cand[sl, 0], cand[sl, 1]] = b2[cand[sl, 0], cand[sl, 1]]
+            print("parity %s: %d sliver element(s), difference within %g of their neighbours" % (label, nsl, rtol))
+        assert nsl <= max(1, (scale > floor * top).sum() // 10000), nsl
+        a = a2
     n, nnear, worst, m, ncmp = outliers(a, b, rtol, floor, drift)
     test = os.environ.get("PYTEST_CURRENT_TEST", "").split(" ")[0]
     rec = {"test": test, "label": label, "rtol": rtol, "outliers": n, "drift": nnear, "compared": ncmp,
