@@ -44,6 +44,7 @@ constexpr double kDblMax = 1.7976931348623157e308;
 constexpr int kBlock = 256;
 constexpr int kSegWords = 3 * (kBlock / 64) * 4 / 8;  // the trace kernel's per-wave segment counts, in doubles
 constexpr int kLabsBuf = 16;      // buffered Labs adds per trace lane (LDS)
+constexpr unsigned kRequestSample = 8;  // (SKIRT_SAMPLED_REQUESTS) one wave in 8 counts the Labs requests
 constexpr int kStepsPerPull = 4;  // grid steps between two ray pulls of a trace wave
 // The slot pool runs as one or two independent pipelines ("halves", SkirtMcrt::halves): with two, one
 // half's event and detect kernels run beside the other half's trace kernel, on CUs of their own (CU-masked
@@ -1531,6 +1532,9 @@ struct Tracer {
     // Labs adds, lane-steps and 64-byte atomic requests (lane 0's values are the wave's)
     unsigned int nseg = 0;
     unsigned int absorbs = 0, laneSlots = 0, requests = 0;
+#ifdef SKIRT_SAMPLED_REQUESTS
+    unsigned int absorbLane = 0;  // this lane's buffered adds (summed over the wave at the end)
+#endif
     unsigned* waveSegs;  // LDS, [kBlock / 64][3]: FILL, WALK, PEEL segments of the wave's finished rays
     // Labs adds of this lane not yet issued. f64 atomics execute memory-side at a fixed chip-wide rate
     // of 64-byte requests; lanes of one wave instruction that hit the same 64-byte line share a
@@ -1570,7 +1574,16 @@ struct Tracer {
         const int n = __shfl(npend, src);
         const int q = j * kBlock + wbase + src;
         const unsigned idx = pendIdx[q];
-#ifndef SKIRT_EXPERIMENT_NO_LABS_STATS  // (timing-only experiment, round 6: the statistics' share of the drain)
+#if defined(SKIRT_EXPERIMENT_NO_LABS_STATS)  // (timing-only experiment, round 6: the statistics' share of the drain)
+#elif defined(SKIRT_SAMPLED_REQUESTS)
+        // (experiment, round 6) the adds are counted per lane where they are buffered; the requests in one
+        // wave of every kRequestSample (wave-uniform), scaled at the end
+        if (((blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) & (kRequestSample - 1)) == 0) {
+            const unsigned line = (unsigned)(reinterpret_cast<size_t>(a.labs + idx) >> 6);
+            const unsigned prev = __shfl(line, lane - 1);
+            requests += (unsigned)__popcll(__ballot(j < n && (j == 0 || prev != line)));
+        }
+#else
         // the requests of this instruction: a lane starts one unless the lane before it (the same
         // ray's previous add) hit the same 64-byte line
         const unsigned line = (unsigned)(reinterpret_cast<size_t>(a.labs + idx) >> 6);
@@ -1651,6 +1664,9 @@ struct Tracer {
                 printf("E S %d %.17g %.17g %.17g\n", m, ds, dtau, (1.0 - albedo) * Lintm);
 #endif
                 if (STORE && a.store) {
+#ifdef SKIRT_SAMPLED_REQUESTS
+                    absorbLane++;
+#endif
                     pendVal[npend * kBlock + threadIdx.x] = (1.0 - albedo) * Lintm;
                     pendIdx[npend * kBlock + threadIdx.x] = (unsigned)r.ell * (unsigned)a.labsStride + (unsigned)m;
                     npend++;
@@ -2156,7 +2172,11 @@ __device__ __forceinline__ void traceBody(const Args& a) {
     const unsigned* ws = T.waveSegs + (threadIdx.x >> 6) * 3;
     const bool l0 = lane == 0;
     const unsigned long long vals[8] = {0, l0 ? ws[0] : 0u, l0 ? ws[1] : 0u, l0 ? ws[2] : 0u, 0,
+#ifdef SKIRT_SAMPLED_REQUESTS
+                                        T.absorbLane, l0 ? T.laneSlots : 0u, l0 ? T.requests * kRequestSample : 0u};
+#else
                                         l0 ? T.absorbs : 0u, l0 ? T.laneSlots : 0u, l0 ? T.requests : 0u};
+#endif
     flushStats(a, vals);
 }
 

@@ -2,6 +2,10 @@ import os
 import sys
 
 import pytest
+# torch before the engine: the ROCm wheel of torch brings its own HIP runtime, and libskirt_amd.so then binds
+# to that same runtime (one libamdhip64.so.7 per process); loaded the other way round, torch finds no GPU in a
+# process whose engine already initialized the system runtime (test_dust_labs_bound_after_a_stellar_phase)
+import torch  # noqa: F401
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)

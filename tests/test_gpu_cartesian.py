@@ -14,7 +14,7 @@ import pytest
 import oracle_lib as O
 import skirt_amd as S
 import tree_models as T
-from parity import DUST_OUTLIERS, STELLAR_OUTLIERS, assert_parity
+from parity import DUST_OUTLIERS, STELLAR_OUTLIERS, assert_parity, cartesian_neighbour_scale
 
 pytestmark = pytest.mark.gpu
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "ski")
@@ -90,10 +90,17 @@ def test_labs_table_over_4_gib_takes_global_atomics(tmp_path):
     labs = sim.labs()
     assert labs.sum() > 0
     np.testing.assert_allclose(labs.sum(axis=0), orc.labs.sum(axis=0), rtol=1e-9, atol=1e-300)
-    # paths of up to ~400 cells (128 per axis) carry the last-digit drift of the device's exp/expm1 over
-    # their segments further than the 16^3 fixtures: 28 of 960,185 compared elements beyond 1e-9 (largest
-    # 1.3e-7), hence 1e-8 here. The drift is not the global atomics': at 200 wavelengths (3.4 GB, the buffer
-    # descriptor's path) the same model gives bit-identical tallies with SKIRT_AMD_LABS_GLOBAL=0 and =1
-    # (profiles/r05_labs_over_4gib.txt)
-    assert_parity(labs, orc.labs, 1e-8, STELLAR_OUTLIERS, "labs")
+    # Round 5 ran this at 1e-8: 28 of 960,185 elements were beyond 1e-9, the largest 1.34e-7 (cell 317912,
+    # wavelength 44), profiles/r05_labs_over_4gib.txt. The packet trace (profiles/r06_parity_trace.txt,
+    # tools/parity_trace.py) found no changed decision: packet 890 alone adds to that cell, engine and oracle
+    # cross the same 115 cells of its third FILL path, and the cell is a sliver of it, 1.2e11 m against a
+    # median segment of 1.6e17 m. The path starts 1 ulp apart in position and 1-3 ulp in direction (the
+    # engine's equivalent scattering formulas), every segment agrees to 1.6e-13 of the
+    # median segment, and the sliver's length -- the difference of two coordinates equal to 7e-7 of a cell --
+    # carries that as 1.3e-7 of itself. So the comparison is at 1e-9 with no outlier again, the slivers
+    # judged against their neighbours' full crossings (parity.cartesian_neighbour_scale). The global atomics
+    # play no part: at 200 wavelengths (3.4 GB, the buffer descriptor's path) SKIRT_AMD_LABS_GLOBAL=0 and =1
+    # give bit-identical tallies (profiles/r05_labs_over_4gib.txt).
+    assert_parity(labs, orc.labs, 1e-9, STELLAR_OUTLIERS, "labs",
+                  slivers=cartesian_neighbour_scale(orc.labs, (128, 128, 128)))
     del labs, orc

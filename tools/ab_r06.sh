@@ -1,6 +1,7 @@
 #!/bin/bash
 # round-6 A/B runs on one box (tool only): C3 at 2^24 / 2^25 / 2^26 packet slots and without the drain's
-# statistics (timing only, libskirt_amd_nostats.so; C2 too), C5 with its pooled dust
+# statistics (timing only, libskirt_amd_nostats.so; C2 too) or with the requests
+# sampled in one wave of 8 (libskirt_amd_sampled.so), C5 with its pooled dust
 # phases admitted in 1, 2 or 4 waves (SKIRT_AMD_POOL_DIV). Alternating order; logs under gpurun_out/ab6/.
 set -o pipefail
 out=gpurun_out/ab6; mkdir -p $out
@@ -20,10 +21,12 @@ for rep in 1 2; do
   run c3_s25_$rep --config c3 --slots 33554432
   run c3_s26_$rep --config c3 --slots 67108864
   SKIRT_AMD_LIB=libskirt_amd_nostats.so run c3_nostats_$rep --config c3
+  SKIRT_AMD_LIB=libskirt_amd_sampled.so run c3_sampled_$rep --config c3
 done
 for rep in 1 2; do
   run c2_$rep --config c2
   SKIRT_AMD_LIB=libskirt_amd_nostats.so run c2_nostats_$rep --config c2
+  SKIRT_AMD_LIB=libskirt_amd_sampled.so run c2_sampled_$rep --config c2
 done
 for rep in 1 2; do
   SKIRT_AMD_POOL_DIV=1 run c5_d1_$rep --config c5
