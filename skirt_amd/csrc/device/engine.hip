@@ -1421,14 +1421,16 @@ struct Grid<SKIRT_GRID_VORONOI> {
         }
         const int total = __shfl(incl, 63);
         const int start = incl - extra;
+        // (branch-free: a group past the lane's list is bounded as no exit. A branch around loads or
+        // atomics makes the waitcnt pass wait for every outstanding vector-memory operation at the join,
+        // the previous steps' Labs atomics included)
         auto own = [&](int gi) {
-            if (alive && gi * U < cnt) {
+            const bool v = gi * U < cnt;
 #pragma unroll
-                for (int u = 0; u < U; u++) {
-                    float lo, uc;
-                    bounds(s, L.g[gi][u], true, lo, uc);
-                    take(b, lo, uc, L.g[gi][u].next);
-                }
+            for (int u = 0; u < U; u++) {
+                float lo, uc;
+                bounds(s, L.g[gi][u], v, lo, uc);
+                take(b, lo, uc, L.g[gi][u].next);
             }
         };
         // a round of items [base, base + 64): owners list them, each lane takes item base + lane
@@ -1451,17 +1453,15 @@ struct Grid<SKIRT_GRID_VORONOI> {
             so.eA = __shfl(s.eA, o); so.eB2 = __shfl(s.eB2, o);
             so.eA2 = 2.0f * so.eA;
             const int cj = __shfl(act ? r.cj : 0, o);
-            if (has) vorEntries(a.vorSlots + cj, OWN + k * U, e);
+            vorEntries(a.vorSlots + (has ? cj : 0), has ? OWN + k * U : 0, e);  // (unconditional: see own)
         };
         auto compute = [&](int base) {
             Best p{FLT_MAX, FLT_MAX, FLT_MAX, 0};
-            if (has) {
 #pragma unroll
-                for (int u = 0; u < U; u++) {
-                    float lo, uc;
-                    bounds(so, e[u], true, lo, uc);
-                    take(p, lo, uc, e[u].next);
-                }
+            for (int u = 0; u < U; u++) {
+                float lo, uc;
+                bounds(so, e[u], has, lo, uc);
+                take(p, lo, uc, e[u].next);
             }
             part[4 * lane] = p.U; part[4 * lane + 1] = p.L1; part[4 * lane + 2] = p.L2;
             part[4 * lane + 3] = __int_as_float(p.w1);

@@ -2,9 +2,14 @@
 # round-6 A/B runs on one box (tool only): C3 at 2^24 / 2^25 / 2^26 packet slots and without the drain's
 # statistics (timing only, libskirt_amd_nostats.so; C2 too) or with the requests
 # sampled in one wave of 8 (libskirt_amd_sampled.so), C5 with its pooled dust
-# phases admitted in 1, 2 or 4 waves (SKIRT_AMD_POOL_DIV). Alternating order; logs under gpurun_out/ab6/.
+# phases admitted in 1, 2 or 4 waves (SKIRT_AMD_POOL_DIV), C4 with the shared entry groups against the lane-serial
+# step (libskirt_amd_vshare0.so). Alternating order; logs under gpurun_out/ab6/.
 set -o pipefail
 out=gpurun_out/ab6; mkdir -p $out
+# the Voronoi same-stream tests with the default build first (its shared entry groups)
+timeout -k 10 300 python -u -m pytest -x -q --timeout 240 --timeout-method thread tests/test_gpu_parity.py tests/test_gpu_counts.py \
+    -k "vor or c4" > $out/vor_tests.log 2>&1 || { echo "vor tests failed"; tail -30 $out/vor_tests.log; exit 1; }
+tail -1 $out/vor_tests.log
 run() {  # tag, then bench args (env via the caller)
     local tag=$1; shift
     timeout -k 10 170 python -u bench.py --no-cpu-baseline --steps 5 --warmup 2 "$@" > $out/$tag.json 2> $out/$tag.err || { echo "FAIL $tag"; exit 1; }
@@ -27,6 +32,10 @@ for rep in 1 2; do
   run c2_$rep --config c2
   SKIRT_AMD_LIB=libskirt_amd_nostats.so run c2_nostats_$rep --config c2
   SKIRT_AMD_LIB=libskirt_amd_sampled.so run c2_sampled_$rep --config c2
+done
+for rep in 1 2; do
+  run c4_share_$rep --config c4
+  SKIRT_AMD_LIB=libskirt_amd_vshare0.so run c4_serial_$rep --config c4
 done
 for rep in 1 2; do
   SKIRT_AMD_POOL_DIV=1 run c5_d1_$rep --config c5
