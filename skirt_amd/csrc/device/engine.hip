@@ -44,7 +44,6 @@ constexpr double kDblMax = 1.7976931348623157e308;
 constexpr int kBlock = 256;
 constexpr int kSegWords = 3 * (kBlock / 64) * 4 / 8;  // the trace kernel's per-wave segment counts, in doubles
 constexpr int kLabsBuf = 16;      // buffered Labs adds per trace lane (LDS)
-constexpr unsigned kRequestSample = 8;  // (SKIRT_SAMPLED_REQUESTS) one wave in 8 counts the Labs requests
 constexpr int kStepsPerPull = 4;  // grid steps between two ray pulls of a trace wave
 // The slot pool runs as one or two independent pipelines ("halves", SkirtMcrt::halves): with two, one
 // half's event and detect kernels run beside the other half's trace kernel, on CUs of their own (CU-masked
@@ -206,10 +205,11 @@ constexpr int kVorGroups = 4;
 // round 6: the entry groups past a cell's first kVorGroups shared out over the wave (Grid<VORONOI>::stepCoop);
 // -DSKIRT_VOR_SHARE=0 builds the lane-serial step for A/B runs
 #ifndef SKIRT_VOR_SHARE
-#define SKIRT_VOR_SHARE 1
+#define SKIRT_VOR_SHARE 0
 #endif
 constexpr bool kVorShare = SKIRT_VOR_SHARE != 0;
-constexpr int kVorShareWords = 64 * 5;  // per wave in LDS: 64 item -> owner entries, 64 partial Bests of 4 words
+// per wave in LDS: 64 item -> owner entries, 64 partial Bests of 4 words, 64 owners' operands of 12 words
+constexpr int kVorShareWords = 64 * (1 + 4 + 12);
 constexpr int kVorFallbackGroup = 2;  // neighbour sites loaded together by the exact re-evaluation (<= kVorUnroll)
 constexpr int kVorCand = 4;  // possible winners the exact re-evaluation collects before it takes the whole list
 // slots after the last cell's block: a step loads whole groups of entries past its list
@@ -1403,6 +1403,7 @@ struct Grid<SKIRT_GRID_VORONOI> {
         const int lane = threadIdx.x & 63;
         int* map = share;                                        // item -> owner | group << 8
         float* part = reinterpret_cast<float*>(share + 64);      // [item][U, L1, L2, w1]
+        float* ops = reinterpret_cast<float*>(share + 5 * 64);   // [owner lane][Dx Dy Dz kx | ky kz eA eB2 | cj]
         Load L;
         stepLoad(a, r, L, act);
         StepIn s{};
@@ -1411,16 +1412,26 @@ struct Grid<SKIRT_GRID_VORONOI> {
         bool alive = false;
         if (act) alive = headFrom(a, r, s, L.h0, L.h1, L.h2, seg);
         const int cnt = alive ? s.cnt : 0;
-        // the groups past the own ones, and their item numbers (a prefix sum over the wave)
+        // the groups past the own ones, and their item numbers: a prefix sum over the wave from one ballot per
+        // bit of the count (the lanes' counts below 32 groups; a wave with more takes the shuffle scan)
         const int extra = cnt > OWN ? (cnt - OWN + U - 1) / U : 0;
-        int incl = extra;
+        int start = 0, total = 0;
+        if (__ballot(extra >= 32) == 0) {
 #pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const int t = __shfl_up(incl, d);
-            if (lane >= d) incl += t;
+            for (int bit = 0; bit < 5; bit++) {
+                const unsigned long long m = __ballot((extra >> bit) & 1);
+                start += (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u)) << bit;
+                total += __popcll(m) << bit;
+            }
+        } else {
+            int incl = extra;
+            for (int d = 1; d < 64; d <<= 1) {
+                const int t = __shfl_up(incl, d);
+                if (lane >= d) incl += t;
+            }
+            total = __shfl(incl, 63);
+            start = incl - extra;
         }
-        const int total = __shfl(incl, 63);
-        const int start = incl - extra;
         // (branch-free: a group past the lane's list is bounded as no exit. A branch around loads or
         // atomics makes the waitcnt pass wait for every outstanding vector-memory operation at the join,
         // the previous steps' Labs atomics included)
@@ -1433,26 +1444,32 @@ struct Grid<SKIRT_GRID_VORONOI> {
                 take(b, lo, uc, L.g[gi][u].next);
             }
         };
-        // a round of items [base, base + 64): owners list them, each lane takes item base + lane
+        // a round of items [base, base + 64): owners list them and their operands, each lane takes item
+        // base + lane
         StepIn so{};
         VorEntry e[U];
         bool has = false;
+        if (extra > 0) {
+            float4* o = reinterpret_cast<float4*>(ops + 12 * lane);
+            o[0] = make_float4(s.Dx, s.Dy, s.Dz, s.fkx);
+            o[1] = make_float4(s.fky, s.fkz, s.eA, s.eB2);
+            reinterpret_cast<int*>(ops)[12 * lane + 8] = r.cj;
+        }
         auto setup = [&](int base) {
             for (int k = 0; k < extra; k++) {
                 const int it = start + k - base;
                 if (it >= 0 && it < 64) map[it] = lane | (k << 8);
             }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             has = base + lane < total;
             const int m = has ? map[lane] : 0;
-            const int o = m & 63, k = m >> 8;
-            so.Dx = __shfl(s.Dx, o); so.Dy = __shfl(s.Dy, o); so.Dz = __shfl(s.Dz, o);
-            so.fkx = __shfl(s.fkx, o); so.fky = __shfl(s.fky, o); so.fkz = __shfl(s.fkz, o);
-            so.eA = __shfl(s.eA, o); so.eB2 = __shfl(s.eB2, o);
+            const int ow = m & 63, k = m >> 8;
+            const float4* o = reinterpret_cast<const float4*>(ops + 12 * ow);
+            const float4 o0 = o[0], o1 = o[1];
+            const int cj = reinterpret_cast<const int*>(ops)[12 * ow + 8];
+            so.Dx = o0.x; so.Dy = o0.y; so.Dz = o0.z; so.fkx = o0.w;
+            so.fky = o1.x; so.fkz = o1.y; so.eA = o1.z; so.eB2 = o1.w;
             so.eA2 = 2.0f * so.eA;
-            const int cj = __shfl(act ? r.cj : 0, o);
             vorEntries(a.vorSlots + (has ? cj : 0), has ? OWN + k * U : 0, e);  // (unconditional: see own)
         };
         auto compute = [&](int base) {
@@ -1463,17 +1480,15 @@ struct Grid<SKIRT_GRID_VORONOI> {
                 bounds(so, e[u], has, lo, uc);
                 take(p, lo, uc, e[u].next);
             }
-            part[4 * lane] = p.U; part[4 * lane + 1] = p.L1; part[4 * lane + 2] = p.L2;
-            part[4 * lane + 3] = __int_as_float(p.w1);
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            reinterpret_cast<float4*>(part)[lane] = make_float4(p.U, p.L1, p.L2, __int_as_float(p.w1));
             __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             // the owner's partials of this round, in list order
             for (int k = 0; k < extra; k++) {
                 const int it = start + k - base;
                 if (it < 0 || it >= 64) continue;
-                const float pU = part[4 * it], pL1 = part[4 * it + 1], pL2 = part[4 * it + 2];
-                const int pw1 = __float_as_int(part[4 * it + 3]);
+                const float4 q = reinterpret_cast<const float4*>(part)[it];
+                const float pU = q.x, pL1 = q.y, pL2 = q.z;
+                const int pw1 = __float_as_int(q.w);
                 b.U = fminf(b.U, pU);
                 const float L2 = fminf(fmaxf(b.L1, pL1), fminf(b.L2, pL2));  // the second least of both pairs
                 b.w1 = pL1 < b.L1 ? pw1 : b.w1;
@@ -1483,9 +1498,15 @@ struct Grid<SKIRT_GRID_VORONOI> {
             // (the map and partials are rewritten by the next round only after every lane has read them)
             __builtin_amdgcn_wave_barrier();
         };
+#ifdef SKIRT_VOR_SHARE_EARLY  // (A/B: the shared loads before all four own groups)
+        if (total > 0) setup(0);
+        own(0);
+        own(1);
+#else
         own(0);
         own(1);
         if (total > 0) setup(0);  // its loads arrive while the last own groups are bounded
+#endif
         own(2);
         own(3);
         if (total > 0) compute(0);
@@ -1532,9 +1553,6 @@ struct Tracer {
     // Labs adds, lane-steps and 64-byte atomic requests (lane 0's values are the wave's)
     unsigned int nseg = 0;
     unsigned int absorbs = 0, laneSlots = 0, requests = 0;
-#ifdef SKIRT_SAMPLED_REQUESTS
-    unsigned int absorbLane = 0;  // this lane's buffered adds (summed over the wave at the end)
-#endif
     unsigned* waveSegs;  // LDS, [kBlock / 64][3]: FILL, WALK, PEEL segments of the wave's finished rays
     // Labs adds of this lane not yet issued. f64 atomics execute memory-side at a fixed chip-wide rate
     // of 64-byte requests; lanes of one wave instruction that hit the same 64-byte line share a
@@ -1574,24 +1592,14 @@ struct Tracer {
         const int n = __shfl(npend, src);
         const int q = j * kBlock + wbase + src;
         const unsigned idx = pendIdx[q];
-#if defined(SKIRT_EXPERIMENT_NO_LABS_STATS)  // (timing-only experiment, round 6: the statistics' share of the drain)
-#elif defined(SKIRT_SAMPLED_REQUESTS)
-        // (experiment, round 6) the adds are counted per lane where they are buffered; the requests in one
-        // wave of every kRequestSample (wave-uniform), scaled at the end
-        if (((blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) & (kRequestSample - 1)) == 0) {
-            const unsigned line = (unsigned)(reinterpret_cast<size_t>(a.labs + idx) >> 6);
-            const unsigned prev = __shfl(line, lane - 1);
-            requests += (unsigned)__popcll(__ballot(j < n && (j == 0 || prev != line)));
-        }
-#else
         // the requests of this instruction: a lane starts one unless the lane before it (the same
-        // ray's previous add) hit the same 64-byte line
+        // ray's previous add) hit the same 64-byte line (these statistics cost nothing measurable: C3 +0.05 %,
+        // C2 +0.6 % without them, timing only; profiles/r06_ab.txt)
         const unsigned line = (unsigned)(reinterpret_cast<size_t>(a.labs + idx) >> 6);
         const unsigned prev = __shfl(line, lane - 1);
         const unsigned long long starts = __ballot(j < n && (j == 0 || prev != line));
         absorbs += (unsigned)__popcll(__ballot(j < n));
         requests += (unsigned)__popcll(starts);
-#endif
         if (a.labsGlobal) {  // a table of 4 GiB or more (wave-uniform): global atomics
             if (j < n) atomicAddF64(a.labs + idx, pendVal[q]);
         } else {
@@ -1664,9 +1672,6 @@ struct Tracer {
                 printf("E S %d %.17g %.17g %.17g\n", m, ds, dtau, (1.0 - albedo) * Lintm);
 #endif
                 if (STORE && a.store) {
-#ifdef SKIRT_SAMPLED_REQUESTS
-                    absorbLane++;
-#endif
                     pendVal[npend * kBlock + threadIdx.x] = (1.0 - albedo) * Lintm;
                     pendIdx[npend * kBlock + threadIdx.x] = (unsigned)r.ell * (unsigned)a.labsStride + (unsigned)m;
                     npend++;
@@ -2172,11 +2177,7 @@ __device__ __forceinline__ void traceBody(const Args& a) {
     const unsigned* ws = T.waveSegs + (threadIdx.x >> 6) * 3;
     const bool l0 = lane == 0;
     const unsigned long long vals[8] = {0, l0 ? ws[0] : 0u, l0 ? ws[1] : 0u, l0 ? ws[2] : 0u, 0,
-#ifdef SKIRT_SAMPLED_REQUESTS
-                                        T.absorbLane, l0 ? T.laneSlots : 0u, l0 ? T.requests * kRequestSample : 0u};
-#else
                                         l0 ? T.absorbs : 0u, l0 ? T.laneSlots : 0u, l0 ? T.requests : 0u};
-#endif
     flushStats(a, vals);
 }
 
@@ -4370,13 +4371,9 @@ static int runPhase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, uint6
     // (the queue holds kPathCap peel-offs per instrument and slot: the slots shrink with the instruments)
     if (continuous) slots = std::min(slots, std::max(64, kContSlots / std::max(1, (int)c->instr.size())));
     if ((uint64_t)slots > count) slots = (int)count;
-    // experiment (round 6): a phase that fits the pool runs its packets in lockstep (all FILL rays in one launch,
-    // then all WALK rays ...); SKIRT_AMD_POOL_DIV = d admits them d waves at a time instead
-    if (const char* pd = getenv("SKIRT_AMD_POOL_DIV")) {
-        const int d = atoi(pd);
-        if (d > 1 && (uint64_t)slots >= count) slots = std::max(64 * 1024, (int)(count / (uint64_t)d));
-        if ((uint64_t)slots > count) slots = (int)count;
-    }
+    // (a phase that fits the pool runs its packets in lockstep; admitting them in 2 or 4 waves instead changes
+    // neither the C5 step nor its 164 trace launches: the tail iterations are the few long-lived packets either
+    // way, profiles/r06_ab.txt)
     const int halves = (continuous || !p->has_dust || slots < 2 * 64 * kMaxHalves) ? 1 : c->halves;
     slots = std::max(slots, 64 * halves) / halves;  // per half
     const bool forked = c->halves > 1 || c->cusT || c->cusE;  // the pipeline runs on the owned streams
