@@ -202,14 +202,6 @@ constexpr int kVorUnroll = 4;
 // (profiles/r04_vor_groups4.txt). Measured and removed (git history): the neighbour-parallel drain step
 // (profiles/r03_vor_wide.txt), the drain split around the step's loads (profiles/r04_c4_variants.txt).
 constexpr int kVorGroups = 4;
-// round 6: the entry groups past a cell's first kVorGroups shared out over the wave (Grid<VORONOI>::stepCoop);
-// -DSKIRT_VOR_SHARE=0 builds the lane-serial step for A/B runs
-#ifndef SKIRT_VOR_SHARE
-#define SKIRT_VOR_SHARE 0
-#endif
-constexpr bool kVorShare = SKIRT_VOR_SHARE != 0;
-// per wave in LDS: 64 item -> owner entries, 64 partial Bests of 4 words, 64 owners' operands of 12 words
-constexpr int kVorShareWords = 64 * (1 + 4 + 12);
 constexpr int kVorFallbackGroup = 2;  // neighbour sites loaded together by the exact re-evaluation (<= kVorUnroll)
 constexpr int kVorCand = 4;  // possible winners the exact re-evaluation collects before it takes the whole list
 // slots after the last cell's block: a step loads whole groups of entries past its list
@@ -1386,138 +1378,6 @@ struct Grid<SKIRT_GRID_VORONOI> {
         return decide(a, r, s, b, seg);
     }
 
-    // One step with the entry groups past the first kVorGroups shared out over the wave (round 6, VERDICT r5
-    // item 4). stepRest makes a wave run as many groups of kVorUnroll entries as its lane with the most
-    // neighbours needs (C4: 6.4 groups for a mean of 3.9). Here every lane bounds its own first kVorGroups
-    // groups (the 16 entries loaded with the header), and the groups beyond them are items handed out one
-    // per lane, ray or no ray (C4: 28 items per wave on average, so one round instead of 2.4): the taker
-    // bounds the owner's kVorUnroll entries with the owner's operands, fetched lane to lane, into a partial
-    // Best in LDS, and the owner merges its partials in list order. U and the two least lower bounds do not
-    // depend on the order of the entries, and w1, the first least lower bound in list order, is kept by the
-    // merge (strict <, groups in list order), so every decision is stepRest's, bit for bit. Every lane of the
-    // wave calls it (act: the lane has a ray); share: the wave's kVorShareWords of LDS.
-    template <class SegFn>
-    __device__ static __forceinline__ bool stepCoop(const Args& a, Ray& r, bool act, int* share, SegFn seg) {
-        constexpr int U = kVorUnroll;
-        constexpr int OWN = kVorGroups * kVorUnroll;
-        const int lane = threadIdx.x & 63;
-        int* map = share;                                        // item -> owner | group << 8
-        float* part = reinterpret_cast<float*>(share + 64);      // [item][U, L1, L2, w1]
-        float* ops = reinterpret_cast<float*>(share + 5 * 64);   // [owner lane][Dx Dy Dz kx | ky kz eA eB2 | cj]
-        Load L;
-        stepLoad(a, r, L, act);
-        StepIn s{};
-        s.B = a.vorSlots + (act ? r.cj : 0);
-        Best b{FLT_MAX, FLT_MAX, FLT_MAX, 0};
-        bool alive = false;
-        if (act) alive = headFrom(a, r, s, L.h0, L.h1, L.h2, seg);
-        const int cnt = alive ? s.cnt : 0;
-        // the groups past the own ones, and their item numbers: a prefix sum over the wave from one ballot per
-        // bit of the count (the lanes' counts below 32 groups; a wave with more takes the shuffle scan)
-        const int extra = cnt > OWN ? (cnt - OWN + U - 1) / U : 0;
-        int start = 0, total = 0;
-        if (__ballot(extra >= 32) == 0) {
-#pragma unroll
-            for (int bit = 0; bit < 5; bit++) {
-                const unsigned long long m = __ballot((extra >> bit) & 1);
-                start += (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u)) << bit;
-                total += __popcll(m) << bit;
-            }
-        } else {
-            int incl = extra;
-            for (int d = 1; d < 64; d <<= 1) {
-                const int t = __shfl_up(incl, d);
-                if (lane >= d) incl += t;
-            }
-            total = __shfl(incl, 63);
-            start = incl - extra;
-        }
-        // (branch-free: a group past the lane's list is bounded as no exit. A branch around loads or
-        // atomics makes the waitcnt pass wait for every outstanding vector-memory operation at the join,
-        // the previous steps' Labs atomics included)
-        auto own = [&](int gi) {
-            const bool v = gi * U < cnt;
-#pragma unroll
-            for (int u = 0; u < U; u++) {
-                float lo, uc;
-                bounds(s, L.g[gi][u], v, lo, uc);
-                take(b, lo, uc, L.g[gi][u].next);
-            }
-        };
-        // a round of items [base, base + 64): owners list them and their operands, each lane takes item
-        // base + lane
-        StepIn so{};
-        VorEntry e[U];
-        bool has = false;
-        if (extra > 0) {
-            float4* o = reinterpret_cast<float4*>(ops + 12 * lane);
-            o[0] = make_float4(s.Dx, s.Dy, s.Dz, s.fkx);
-            o[1] = make_float4(s.fky, s.fkz, s.eA, s.eB2);
-            reinterpret_cast<int*>(ops)[12 * lane + 8] = r.cj;
-        }
-        auto setup = [&](int base) {
-            for (int k = 0; k < extra; k++) {
-                const int it = start + k - base;
-                if (it >= 0 && it < 64) map[it] = lane | (k << 8);
-            }
-            __builtin_amdgcn_wave_barrier();
-            has = base + lane < total;
-            const int m = has ? map[lane] : 0;
-            const int ow = m & 63, k = m >> 8;
-            const float4* o = reinterpret_cast<const float4*>(ops + 12 * ow);
-            const float4 o0 = o[0], o1 = o[1];
-            const int cj = reinterpret_cast<const int*>(ops)[12 * ow + 8];
-            so.Dx = o0.x; so.Dy = o0.y; so.Dz = o0.z; so.fkx = o0.w;
-            so.fky = o1.x; so.fkz = o1.y; so.eA = o1.z; so.eB2 = o1.w;
-            so.eA2 = 2.0f * so.eA;
-            vorEntries(a.vorSlots + (has ? cj : 0), has ? OWN + k * U : 0, e);  // (unconditional: see own)
-        };
-        auto compute = [&](int base) {
-            Best p{FLT_MAX, FLT_MAX, FLT_MAX, 0};
-#pragma unroll
-            for (int u = 0; u < U; u++) {
-                float lo, uc;
-                bounds(so, e[u], has, lo, uc);
-                take(p, lo, uc, e[u].next);
-            }
-            reinterpret_cast<float4*>(part)[lane] = make_float4(p.U, p.L1, p.L2, __int_as_float(p.w1));
-            __builtin_amdgcn_wave_barrier();
-            // the owner's partials of this round, in list order
-            for (int k = 0; k < extra; k++) {
-                const int it = start + k - base;
-                if (it < 0 || it >= 64) continue;
-                const float4 q = reinterpret_cast<const float4*>(part)[it];
-                const float pU = q.x, pL1 = q.y, pL2 = q.z;
-                const int pw1 = __float_as_int(q.w);
-                b.U = fminf(b.U, pU);
-                const float L2 = fminf(fmaxf(b.L1, pL1), fminf(b.L2, pL2));  // the second least of both pairs
-                b.w1 = pL1 < b.L1 ? pw1 : b.w1;
-                b.L1 = fminf(b.L1, pL1);
-                b.L2 = L2;
-            }
-            // (the map and partials are rewritten by the next round only after every lane has read them)
-            __builtin_amdgcn_wave_barrier();
-        };
-#ifdef SKIRT_VOR_SHARE_EARLY  // (A/B: the shared loads before all four own groups)
-        if (total > 0) setup(0);
-        own(0);
-        own(1);
-#else
-        own(0);
-        own(1);
-        if (total > 0) setup(0);  // its loads arrive while the last own groups are bounded
-#endif
-        own(2);
-        own(3);
-        if (total > 0) compute(0);
-        for (int base = 64; base < total; base += 64) {
-            setup(base);
-            compute(base);
-        }
-        if (!alive) return false;
-        return decide(a, r, s, b, seg);
-    }
-
     __device__ static __forceinline__ int whichcell(const Args& a, const Shared&, double x, double y, double z) {
         return cellIndex(a, x, y, z);
     }
@@ -1568,7 +1428,6 @@ struct Tracer {
     unsigned labsOob = 0;             // a byte offset past every replica: the empty lanes' adds are dropped
     int npend = 0;
     unsigned gstep = 0;  // grid steps of the wave (drainStep's round robin)
-    int* share = nullptr;  // Voronoi: the wave's LDS for the shared entry groups (stepCoop)
 
     __device__ __forceinline__ void drain() {
         static_assert(kLabsBuf >= 2 && kLabsBuf <= 64 && (kLabsBuf & (kLabsBuf - 1)) == 0, "kLabsBuf: power of 2");
@@ -2102,10 +1961,6 @@ __device__ __forceinline__ void traceBody(const Args& a) {
     T.waveSegs = reinterpret_cast<unsigned*>(lds + a.ldsInstrOff);
     T.pendVal = lds + a.ldsInstrOff + kSegWords;
     T.pendIdx = reinterpret_cast<unsigned*>(T.pendVal + kLabsBuf * kBlock);
-    if constexpr (GRID == SKIRT_GRID_VORONOI && kVorShare) {  // after the Labs buffers (STORE) or the counts
-        int* base = STORE ? reinterpret_cast<int*>(T.pendIdx + kLabsBuf * kBlock) : reinterpret_cast<int*>(T.pendVal);
-        T.share = base + (threadIdx.x >> 6) * kVorShareWords;
-    }
     if (threadIdx.x < 3 * (kBlock / 64)) T.waveSegs[threadIdx.x] = 0;
     __syncthreads();
     const int lane = threadIdx.x & 63;
@@ -2150,14 +2005,7 @@ __device__ __forceinline__ void traceBody(const Args& a) {
             if (live == 0) break;
             T.laneSlots += 64;
             auto seg = [&](int m, double rho0, double ds) { return T.segment(r, m, rho0, ds); };
-            if constexpr (GRID == SKIRT_GRID_VORONOI && kVorShare) {
-                // every lane steps together: the lanes without a ray take shared entry groups too
-                const bool act = r.mode != RAY_NONE;
-                if (!Grid<GRID>::stepCoop(a, r, act, T.share, seg) && act) {
-                    T.finish(r);
-                    r.mode = RAY_NONE;
-                }
-            } else if (r.mode != RAY_NONE) {
+            if (r.mode != RAY_NONE) {
                 if (!Grid<GRID>::step(a, sh, r, seg)) {
                     T.finish(r);
                     r.mode = RAY_NONE;
@@ -4494,9 +4342,7 @@ static int runPhase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, uint6
                          !getenv("SKIRT_AMD_NO_NOSTORE");
     const size_t ldsTrace = (size_t)a.ldsInstrOff * sizeof(double)          // grid tables + optics
                             + (size_t)kSegWords * sizeof(double)                          // + segment counts
-                            + (noStore ? 0 : (size_t)kLabsBuf * kBlock * (sizeof(double) + sizeof(unsigned)))  // + Labs buffers
-                            + ((c->gridKind == SKIRT_GRID_VORONOI && kVorShare)  // + shared entry groups
-                                   ? (size_t)(kBlock / 64) * kVorShareWords * sizeof(int) : 0);
+                            + (noStore ? 0 : (size_t)kLabsBuf * kBlock * (sizeof(double) + sizeof(unsigned)));  // + Labs buffers
     const size_t ldsEvent = (size_t)a.ldsSedOff * sizeof(double);           // + instruments
     // budget: what one workgroup may allocate (160 KiB on gfx950). The trace and event kernels need their
     // tables; the detect kernel keeps as many SED copies as fit (8, 4, 2, 1), or none (SEDs to the tally)
