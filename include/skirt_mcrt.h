@@ -44,7 +44,7 @@ enum {
     SKIRT_ERR_STATE = 3,     /* call order violated (e.g. run before upload) */
     SKIRT_ERR_NUMERIC = 4,   /* "optical depth along the path is not a positive number" (DustSystem.cpp:976-979) */
     SKIRT_ERR_UNSUPPORTED = 5  /* a model outside the engine's limits, e.g. a Labs table (cells x wavelengths,
-                                  f64) above 4 GiB, a Voronoi mesh above 2^31 slots, tables that do not fit
+                                  f64) of 2^40 elements or more, a Voronoi mesh above 2^31 slots, tables that do not fit
                                   one workgroup's LDS, or (skirt_sim_write) a path reaching the last
                                   ds_crossed bin; the message names the limit and the sizes */
 };

@@ -282,6 +282,8 @@ struct Args {
     double* labs;                // [nlambda][labsStride], device cell order
     unsigned labsBytes;          // its size (< 4 GiB: the trace kernel addresses it through a buffer descriptor)
     int labsGlobal;              // 1: a table of 4 GiB or more, added to with global atomics (no descriptor)
+    int labsHi;                  // 1: a table of 2^32 elements or more (32 GiB): the buffered adds keep the
+                                 //    element index's high bits in pendHi (implies labsGlobal)
     int labsCopies;              // > 1: `labs` holds that many replicas labsCopyStride bytes apart, wave w adding
     unsigned labsCopyStride;     //   into replica w % labsCopies (folded into the table at the phase end)
     double* tally;
@@ -1423,6 +1425,7 @@ struct Tracer {
     // atomic round trip per burst instead of one per step.
     double* pendVal;    // LDS, [kLabsBuf][kBlock]
     unsigned* pendIdx;  // LDS, [kLabsBuf][kBlock]
+    unsigned char* pendHi;  // LDS, [kLabsBuf][kBlock]: bits 32-39 of the element index (Args::labsHi only)
     __amdgpu_buffer_rsrc_t labsRsrc;  // the Labs table as a raw buffer of labsBytes (unless Args::labsGlobal)
     unsigned copyOff = 0;             // this wave's replica (Args::labsCopies), in bytes
     unsigned labsOob = 0;             // a byte offset past every replica: the empty lanes' adds are dropped
@@ -1451,16 +1454,18 @@ struct Tracer {
         const int n = __shfl(npend, src);
         const int q = j * kBlock + wbase + src;
         const unsigned idx = pendIdx[q];
+        // the element index: 32 bits, or 40 with the high byte of a table of 2^32 elements or more
+        const size_t eidx = a.labsHi ? ((size_t)pendHi[q] << 32 | idx) : (size_t)idx;
         // the requests of this instruction: a lane starts one unless the lane before it (the same
         // ray's previous add) hit the same 64-byte line (these statistics cost nothing measurable: C3 +0.05 %,
         // C2 +0.6 % without them, timing only; profiles/r06_ab.txt)
-        const unsigned line = (unsigned)(reinterpret_cast<size_t>(a.labs + idx) >> 6);
+        const unsigned line = (unsigned)(reinterpret_cast<size_t>(a.labs + eidx) >> 6);
         const unsigned prev = __shfl(line, lane - 1);
         const unsigned long long starts = __ballot(j < n && (j == 0 || prev != line));
         absorbs += (unsigned)__popcll(__ballot(j < n));
         requests += (unsigned)__popcll(starts);
         if (a.labsGlobal) {  // a table of 4 GiB or more (wave-uniform): global atomics
-            if (j < n) atomicAddF64(a.labs + idx, pendVal[q]);
+            if (j < n) atomicAddF64(a.labs + eidx, pendVal[q]);
         } else {
             // every lane issues; a lane without an add adds 0 at the first byte past the table (dropped)
             const double v = j < n ? pendVal[q] : 0.0;
@@ -1532,7 +1537,13 @@ struct Tracer {
 #endif
                 if (STORE && a.store) {
                     pendVal[npend * kBlock + threadIdx.x] = (1.0 - albedo) * Lintm;
-                    pendIdx[npend * kBlock + threadIdx.x] = (unsigned)r.ell * (unsigned)a.labsStride + (unsigned)m;
+                    if (a.labsHi) {  // (wave-uniform) a table of 2^32 elements or more
+                        const unsigned long long e = (unsigned long long)r.ell * (unsigned)a.labsStride + (unsigned)m;
+                        pendIdx[npend * kBlock + threadIdx.x] = (unsigned)e;
+                        pendHi[npend * kBlock + threadIdx.x] = (unsigned char)(e >> 32);
+                    } else {
+                        pendIdx[npend * kBlock + threadIdx.x] = (unsigned)r.ell * (unsigned)a.labsStride + (unsigned)m;
+                    }
                     npend++;
                 }
             }
@@ -1961,6 +1972,7 @@ __device__ __forceinline__ void traceBody(const Args& a) {
     T.waveSegs = reinterpret_cast<unsigned*>(lds + a.ldsInstrOff);
     T.pendVal = lds + a.ldsInstrOff + kSegWords;
     T.pendIdx = reinterpret_cast<unsigned*>(T.pendVal + kLabsBuf * kBlock);
+    T.pendHi = reinterpret_cast<unsigned char*>(T.pendIdx + kLabsBuf * kBlock);  // (allocated when a.labsHi)
     if (threadIdx.x < 3 * (kBlock / 64)) T.waveSegs[threadIdx.x] = 0;
     __syncthreads();
     const int lane = threadIdx.x & 63;
@@ -4274,12 +4286,15 @@ static int runPhase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, uint6
     if (a.store && !c->dLabs) return fail(c, SKIRT_ERR_STATE, "no Labs buffer");
     // the trace kernel adds to Labs through a buffer descriptor (32-bit byte offsets, one byte past the end
     // for the drain's empty lanes) while the table holds at most 4 GiB - 8 (e.g. 2^21 cells x 255
-    // wavelengths), with global atomics beyond (SKIRT_AMD_LABS_GLOBAL=1 forces them: tests); the buffered
-    // adds carry 32-bit element indices, so 2^32 doubles (32 GiB) at most
+    // wavelengths), with global atomics beyond (SKIRT_AMD_LABS_GLOBAL=1 forces them: tests)
     const uint64_t labsElems = (uint64_t)c->labsStride * (uint64_t)c->nlambda;
-    if (a.store && labsElems > 0xffffffffull) return fail(c, SKIRT_ERR_UNSUPPORTED, "Labs table larger than 32 GiB");
+    // 2^32 elements or more (32 GiB): the buffered adds carry 40-bit element indices (SKIRT_AMD_LABS_HI=1 forces
+    // that path: tests); 2^40 elements at most
+    if (a.store && labsElems >= (1ull << 40)) return fail(c, SKIRT_ERR_UNSUPPORTED, "Labs table of 2^40 elements or more");
+    const bool forceHi = getenv("SKIRT_AMD_LABS_HI") && atoi(getenv("SKIRT_AMD_LABS_HI")) != 0;
+    a.labsHi = (a.store && (forceHi || labsElems > 0xffffffffull)) ? 1 : 0;
     const bool forceGlobal = getenv("SKIRT_AMD_LABS_GLOBAL") && atoi(getenv("SKIRT_AMD_LABS_GLOBAL")) != 0;
-    a.labsGlobal = (forceGlobal || labsElems * sizeof(double) > 0xfffffff8ull) ? 1 : 0;
+    a.labsGlobal = (forceGlobal || a.labsHi || labsElems * sizeof(double) > 0xfffffff8ull) ? 1 : 0;
     a.labs = phase == SKIRT_PHASE_DUST_SELFABS ? c->dLabsDust : c->dLabs;
     a.labsBytes = a.labsGlobal ? 0u : (unsigned)(labsElems * sizeof(double));
     // The trace waves add into K replicas of the table (wave w into w % K), folded into it at the phase end:
@@ -4342,7 +4357,8 @@ static int runPhase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, uint6
                          !getenv("SKIRT_AMD_NO_NOSTORE");
     const size_t ldsTrace = (size_t)a.ldsInstrOff * sizeof(double)          // grid tables + optics
                             + (size_t)kSegWords * sizeof(double)                          // + segment counts
-                            + (noStore ? 0 : (size_t)kLabsBuf * kBlock * (sizeof(double) + sizeof(unsigned)));  // + Labs buffers
+                            + (noStore ? 0 : (size_t)kLabsBuf * kBlock * (sizeof(double) + sizeof(unsigned)))  // + Labs buffers
+                            + (a.labsHi ? (size_t)kLabsBuf * kBlock : 0);  // + their high index bytes
     const size_t ldsEvent = (size_t)a.ldsSedOff * sizeof(double);           // + instruments
     // budget: what one workgroup may allocate (160 KiB on gfx950). The trace and event kernels need their
     // tables; the detect kernel keeps as many SED copies as fit (8, 4, 2, 1), or none (SEDs to the tally)
