@@ -43,7 +43,10 @@ namespace {
 constexpr double kDblMax = 1.7976931348623157e308;
 constexpr int kBlock = 256;
 constexpr int kSegWords = 3 * (kBlock / 64) * 4 / 8;  // the trace kernel's per-wave segment counts, in doubles
-constexpr int kLabsBuf = 16;      // buffered Labs adds per trace lane (LDS)
+#ifndef SKIRT_LABS_BUF
+#define SKIRT_LABS_BUF 16
+#endif
+constexpr int kLabsBuf = SKIRT_LABS_BUF;  // buffered Labs adds per trace lane (LDS)
 constexpr int kStepsPerPull = 4;  // grid steps between two ray pulls of a trace wave
 // The slot pool runs as one or two independent pipelines ("halves", SkirtMcrt::halves): with two, one
 // half's event and detect kernels run beside the other half's trace kernel, on CUs of their own (CU-masked
@@ -63,7 +66,10 @@ constexpr int kPollRing = 3;       // copies in flight per half (the host reads 
 // occupancy of the trace kernel: 3 waves per SIMD, i.e. at most 168 VGPRs (the grid entry on the pull
 // path would otherwise take the octree kernel to 175 and 2 waves; C3 1.91e8 -> 2.15e8 pkt/s at 3). The
 // Voronoi walk has its own kernel and attribute below.
-#define SKIRT_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(3)))
+#ifndef SKIRT_TRACE_WAVES  // (variant builds: tools/build_variant.sh TAG -DSKIRT_TRACE_WAVES=4)
+#define SKIRT_TRACE_WAVES 3
+#endif
+#define SKIRT_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(SKIRT_TRACE_WAVES)))
 #define SKIRT_NOSTORE_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(4)))
 // the Voronoi trace kernel at 2 waves per SIMD: its branch-free bounds keep several entries in flight
 // and run without spills in 256 VGPRs (C4 5.72e7 pkt/s at 3 waves, 6.08e7 at 2)
