@@ -76,7 +76,10 @@ constexpr int kPollRing = 3;       // copies in flight per half (the host reads 
 #define SKIRT_VOR_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(2)))
 // the event kernel at 2 waves per SIMD: the Voronoi instantiation (cellIndex on the grid entry of every
 // queued ray) would otherwise take 256 VGPRs + AGPRs and run at 1
-#define SKIRT_EVENT_ATTR __attribute__((amdgpu_waves_per_eu(2)))
+#ifndef SKIRT_EVENT_WAVES  // (variant builds)
+#define SKIRT_EVENT_WAVES 2
+#endif
+#define SKIRT_EVENT_ATTR __attribute__((amdgpu_waves_per_eu(SKIRT_EVENT_WAVES)))
 
 // ------------------------------------------------------------------ descriptors
 struct DevInstr {
@@ -4423,7 +4426,10 @@ static int runPhase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, uint6
     // event kernel blocks per CU: 3 (3 waves/SIMD, the registers allow it). Voronoi: C4 +0.6 % against 2
     // (profiles/r04_event_bpc_sweep.txt); the other grids, once the block reservations no longer serialize on
     // one counter line: C3 +0.7 %, C2 +2.3 % against 2, 4 the same as 3 (profiles/r05_event_bpc_ab.txt)
-    const int ebpc = 3;
+#ifndef SKIRT_EVENT_BPC
+#define SKIRT_EVENT_BPC 3
+#endif
+    const int ebpc = SKIRT_EVENT_BPC;
     const int egrid = std::max(1, std::min((slots + kBlock - 1) / kBlock, std::max(1, c->nCusE) * ebpc));
     const int dgrid = std::max(1, std::max(1, c->nCusE) * 4);
 
