@@ -108,10 +108,13 @@ def cpu_baseline(ski, target_seconds=20.0):
     import oracle_lib
 
     threads = max(1, min(16, os.cpu_count() or 1))  # the GPU box grants 16 CPUs per GPU
-    probe = oracle_lib.run(ski, rng=oracle_lib.RNG_PHILOX, threads=threads, packages=200)
-    rate = probe.packets / max(probe.seconds, 1e-6)
+    # the probe's rate in the sample's own unit (packages x wavelengths, launched or not), from enough packets
+    # that the threads' start-up does not dominate it (200 packages gave samples of ~7 s for a 20 s target)
+    probe_pk = 1000
+    probe = oracle_lib.run(ski, rng=oracle_lib.RNG_PHILOX, threads=threads, packages=probe_pk)
     nl = probe.nlambda
-    per = int(max(200, min(1e6, rate * target_seconds / nl)))
+    rate = probe_pk * nl / max(probe.seconds, 1e-6)
+    per = int(max(probe_pk, min(1e6, rate * target_seconds / nl)))
     r = oracle_lib.run(ski, rng=oracle_lib.RNG_PHILOX, threads=threads, packages=per)
     # counted like the GPU line: packages x wavelengths (wavelengths without source luminosity launch none)
     return per * nl / r.seconds, threads, "%d packets/wavelength x %d wavelengths = %d packets (%d launched) in %.1f s" % (

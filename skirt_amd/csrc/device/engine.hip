@@ -73,7 +73,10 @@ constexpr int kPollRing = 3;       // copies in flight per half (the host reads 
 #define SKIRT_NOSTORE_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(4)))
 // the Voronoi trace kernel at 2 waves per SIMD: its branch-free bounds keep several entries in flight
 // and run without spills in 256 VGPRs (C4 5.72e7 pkt/s at 3 waves, 6.08e7 at 2)
-#define SKIRT_VOR_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(2)))
+#ifndef SKIRT_VOR_TRACE_WAVES  // (variant builds)
+#define SKIRT_VOR_TRACE_WAVES 2
+#endif
+#define SKIRT_VOR_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(SKIRT_VOR_TRACE_WAVES)))
 // the event kernel at 2 waves per SIMD: the Voronoi instantiation (cellIndex on the grid entry of every
 // queued ray) would otherwise take 256 VGPRs + AGPRs and run at 1
 #ifndef SKIRT_EVENT_WAVES  // (variant builds)
@@ -210,7 +213,10 @@ constexpr int kVorUnroll = 4;
 // cell's list padded to whole groups with NaN entries (no per-entry count check): 1.0155e8 -> 1.0243e8
 // (profiles/r04_vor_groups4.txt). Measured and removed (git history): the neighbour-parallel drain step
 // (profiles/r03_vor_wide.txt), the drain split around the step's loads (profiles/r04_c4_variants.txt).
-constexpr int kVorGroups = 4;
+#ifndef SKIRT_VOR_GROUPS
+#define SKIRT_VOR_GROUPS 4
+#endif
+constexpr int kVorGroups = SKIRT_VOR_GROUPS;
 constexpr int kVorFallbackGroup = 2;  // neighbour sites loaded together by the exact re-evaluation (<= kVorUnroll)
 constexpr int kVorCand = 4;  // possible winners the exact re-evaluation collects before it takes the whole list
 // slots after the last cell's block: a step loads whole groups of entries past its list
