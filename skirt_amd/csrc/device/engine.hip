@@ -207,6 +207,27 @@ __device__ __forceinline__ void vorEntries(const VorEntry* B, int q0, VorEntry (
 // 6: 7.26e7 with 28 B/lane spilled; one group of 8: 7.25e7; profiles/r03_vor_pipe.txt, r03_exact_attenuation.txt)
 // FILL segments: exp(-tau) carried as a product while the segments' optical depths stay below this
 constexpr double kCarryTau = 0.5;
+#ifndef SKIRT_POLY_EXPM1
+#define SKIRT_POLY_EXPM1 1
+#endif
+// 1 - exp(-x) = -expm1(-x) for 0 <= x < kCarryTau (the FILL segments' absorbed fraction,
+// MonteCarloSimulation.cpp:458-462) as x + x^2 q(x), q a degree-9 polynomial fitted at Chebyshev nodes of
+// [0, 0.5] (approximation error 0.04 ulp): within 1 ulp of glibc's expm1 over 2e7 arguments, as ocml's is,
+// in 11 VALU operations and 18 register moves against ocml's ~53 (range reduction, ldexp, the constants'
+// moves): C2, C4, C5 +0.4 %, C3 +0.1 % (the trace kernels are not VALU-bound; profiles/r06_poly_expm1_ab.txt)
+__device__ __forceinline__ double oneMinusExpNeg(double x) {
+    double q = 2.0367415268789147e-08;
+    q = fma(q, x, -2.7077568604087168e-07);
+    q = fma(q, x, 2.7529604741385112e-06);
+    q = fma(q, x, -2.4800612392596861e-05);
+    q = fma(q, x, 0.00019841248533674491);
+    q = fma(q, x, -0.0013888888604734388);
+    q = fma(q, x, 0.0083333333311535578);
+    q = fma(q, x, -0.04166666666658167);
+    q = fma(q, x, 0.16666666666666538);
+    q = fma(q, x, -0.5);
+    return fma(x, x * q, x);
+}
 constexpr int kVorUnroll = 4;
 // groups of entries in flight per step: loaded with the header, each reloaded once consumed. 3: C4 trace
 // launch 23.64 -> 23.19 ms, 9.64e7 -> 9.89e7 pkt/s, profiles/r04_ktrace_groups_nolicm.txt; 4 with each
@@ -1421,7 +1442,12 @@ struct Grid<SKIRT_GRID_VORONOI> {
 };
 
 // ================================================================== trace kernel
-template <int GRID, bool ONECOMP, bool CONT, bool STORE>
+// GLOBAL: the Labs adds as global atomics (a table of 4 GiB or more, Args::labsGlobal), a kernel of its own:
+// a run-time choice between the buffer atomic every lane issues and a global atomic only lanes with an add
+// issue leaves the waitcnt pass a path with no vector-memory operation in the drain, and the next step's
+// leaf-map entry then waited with vmcnt(0), i.e. for the drain's atomic as well. Now vmcnt(1): C3 +0.3 %,
+// C2 +0.4 %, C4 and C5 within the spread (the atomic had mostly finished by then; profiles/r06_decode_wait_ab.txt)
+template <int GRID, bool ONECOMP, bool CONT, bool STORE, bool GLOBAL = false>
 struct Tracer {
     const Args& a;
     const Shared& sh;
@@ -1479,7 +1505,7 @@ struct Tracer {
         const unsigned long long starts = __ballot(j < n && (j == 0 || prev != line));
         absorbs += (unsigned)__popcll(__ballot(j < n));
         requests += (unsigned)__popcll(starts);
-        if (a.labsGlobal) {  // a table of 4 GiB or more (wave-uniform): global atomics
+        if constexpr (GLOBAL) {  // a table of 4 GiB or more: global atomics
             if (j < n) atomicAddF64(a.labs + eidx, pendVal[q]);
         } else {
             // every lane issues; a lane without an add adds 0 at the first byte past the table (dropped)
@@ -1532,7 +1558,9 @@ struct Tracer {
                 // 1 - ef loses digits: rounds 1-3 carried it unconditionally and the thick pan_oct_sa models'
                 // deep cells drifted) it is evaluated anew. One f64 exp less per segment: C2 +0.6 %, C5 +0.5 %,
                 // C3 within the spread (profiles/r05_exp_carry_ab.txt)
-                const double ef = -expm1(-dtau);
+                double ef;
+                if (SKIRT_POLY_EXPM1 && dtau < kCarryTau) ef = oneMinusExpNeg(dtau);
+                else ef = -expm1(-dtau);
                 const double Lintm = r.param * r.f1 * ef;
                 if (dtau < kCarryTau) r.f1 -= r.f1 * ef;
                 else r.f1 = exp(-r.tau);
@@ -1955,7 +1983,7 @@ __global__ void __launch_bounds__(kBlock) buildLeafMapKernel(LeafEntry* map, con
 // the recording out of the other kernels' registers
 // STORE false: a phase that stores no absorption (a.store = 0), one dust component, no continuous
 // scattering: no Labs buffers and no drain (its own instantiation, traceKernelNoStore)
-template <int GRID, bool ONECOMP, bool CONT, bool STORE>
+template <int GRID, bool ONECOMP, bool CONT, bool STORE, bool GLOBAL = false>
 __device__ __forceinline__ void traceBody(const Args& a) {
     extern __shared__ __attribute__((aligned(16))) double lds[];
     if (blockIdx.x == 0 && threadIdx.x == 0) {
@@ -1978,7 +2006,7 @@ __device__ __forceinline__ void traceBody(const Args& a) {
     }
     Shared sh = stageTables(a, lds, gridParts<GRID>() | STAGE_OPTICS);
 
-    Tracer<GRID, ONECOMP, CONT, STORE> T{a, sh};
+    Tracer<GRID, ONECOMP, CONT, STORE, GLOBAL> T{a, sh};
     T.labsOob = a.labsCopies > 1 ? (unsigned)a.labsCopies * a.labsCopyStride : a.labsBytes;
     T.labsRsrc = __builtin_amdgcn_make_buffer_rsrc(a.labs, 0, (int)T.labsOob, 0x00020000);
     if (a.labsCopies > 1)
@@ -2056,9 +2084,9 @@ __device__ __forceinline__ void traceBody(const Args& a) {
     flushStats(a, vals);
 }
 
-template <int GRID, bool ONECOMP, bool CONT>
+template <int GRID, bool ONECOMP, bool CONT, bool GLOBAL = false>
 __global__ void __launch_bounds__(kBlock) SKIRT_TRACE_ATTR traceKernel(const Args a) {
-    traceBody<GRID, ONECOMP, CONT, true>(a);
+    traceBody<GRID, ONECOMP, CONT, true, GLOBAL>(a);
 }
 
 // a phase that stores no absorption (the dust emission phase), one component, no continuous scattering:
@@ -2069,9 +2097,9 @@ __global__ void __launch_bounds__(kBlock) SKIRT_NOSTORE_TRACE_ATTR traceKernelNo
 }
 
 // the Voronoi walk at its own occupancy (SKIRT_VOR_TRACE_ATTR)
-template <bool ONECOMP, bool CONT>
+template <bool ONECOMP, bool CONT, bool GLOBAL = false>
 __global__ void __launch_bounds__(kBlock) SKIRT_VOR_TRACE_ATTR traceKernelVor(const Args a) {
-    traceBody<SKIRT_GRID_VORONOI, ONECOMP, CONT, true>(a);
+    traceBody<SKIRT_GRID_VORONOI, ONECOMP, CONT, true, GLOBAL>(a);
 }
 
 // the detections of this iteration's peel-off rays (their optical depths are in the queue now)
@@ -4409,17 +4437,24 @@ static int runPhase(SkirtMcrt* c, int phase, uint32_t cycle, uint64_t npp, uint6
         traceFn = continuous ? (one ? (const void*)fn1c : (const void*)fnNc) : (one ? (const void*)fn1 : (const void*)fnN);
         if (noStore) traceFn = fnNoStore;
     };
-#define SKIRT_PICK(G) pick(traceKernel<G, true, false>, traceKernel<G, false, false>, traceKernel<G, true, true>, \
-                           traceKernel<G, false, true>, (const void*)traceKernelNoStore<G>)
+#define SKIRT_PICK4(G, L) pick(traceKernel<G, true, false, L>, traceKernel<G, false, false, L>, traceKernel<G, true, true, L>, \
+                              traceKernel<G, false, true, L>, (const void*)traceKernelNoStore<G>)
+#define SKIRT_PICK(G) (a.labsGlobal ? SKIRT_PICK4(G, true) : SKIRT_PICK4(G, false))
     if (kind == SKIRT_GRID_CARTESIAN) SKIRT_PICK(SKIRT_GRID_CARTESIAN);
     else if (kind == SKIRT_GRID_OCTREE) SKIRT_PICK(SKIRT_GRID_OCTREE);
     else if (kind == kBinTreeMap) SKIRT_PICK(kBinTreeMap);
     else if (kind == kOctreeBookkeeping) SKIRT_PICK(kOctreeBookkeeping);
-    else if (kind == SKIRT_GRID_VORONOI)
-        pick(traceKernelVor<true, false>, traceKernelVor<false, false>, traceKernelVor<true, true>, traceKernelVor<false, true>,
-             nullptr);
+    else if (kind == SKIRT_GRID_VORONOI) {
+        if (a.labsGlobal)
+            pick(traceKernelVor<true, false, true>, traceKernelVor<false, false, true>, traceKernelVor<true, true, true>,
+                 traceKernelVor<false, true, true>, nullptr);
+        else
+            pick(traceKernelVor<true, false>, traceKernelVor<false, false>, traceKernelVor<true, true>,
+                 traceKernelVor<false, true>, nullptr);
+    }
     else SKIRT_PICK(kOctreeNodes);
 #undef SKIRT_PICK
+#undef SKIRT_PICK4
     if (ldsTrace > 64 * 1024)
         HIPCHECK(c, hipFuncSetAttribute(traceFn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ldsTrace));
     int tgrid = c->traceGrid;
