@@ -2053,6 +2053,10 @@ __device__ __forceinline__ void traceBody(const Args& a) {
                 if (id >= nrays) done = true;
                 else T.load(r, id < nfront ? id : (unsigned)a.rayCap - 1u - (id - nfront));  // a RAY_NONE record (empty path) leaves the lane idle
             }
+            // vmcnt(0) here, on the pull's path: without it the waitcnt pass put one at the join with the steps,
+            // where a while-iteration without a pull then also waited for the last step's Labs atomic (C2 +1-2 %,
+            // C3, C4, C5 within the spread; profiles/r06_pull_wait_ab.txt)
+            __builtin_amdgcn_s_waitcnt(0x0F70);
         }
 #pragma unroll 1
         for (int it = 0; it < kStepsPerPull; it++) {
