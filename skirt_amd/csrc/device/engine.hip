@@ -47,6 +47,9 @@ constexpr int kSegWords = 3 * (kBlock / 64) * 4 / 8;  // the trace kernel's per-
 #define SKIRT_LABS_BUF 16
 #endif
 constexpr int kLabsBuf = SKIRT_LABS_BUF;  // buffered Labs adds per trace lane (LDS)
+#ifndef SKIRT_VOR_DRAIN2
+#define SKIRT_VOR_DRAIN2 1
+#endif
 constexpr int kStepsPerPull = 4;  // grid steps between two ray pulls of a trace wave
 // The slot pool runs as one or two independent pipelines ("halves", SkirtMcrt::halves): with two, one
 // half's event and detect kernels run beside the other half's trace kernel, on CUs of their own (CU-masked
@@ -1524,6 +1527,19 @@ struct Tracer {
         issue(i);
         if (((threadIdx.x & 63) / G) == i) npend = 0;
     }
+    // The same for steps of up to two adds (the Voronoi walk, kSegsPerStep 2): two drain instructions every
+    // step, so every lane's buffer is emptied every kLabsBuf / 2 steps. It replaces a full drain whenever a
+    // buffer might overflow: the same instructions on average, but that drain sat behind a branch, and after it
+    // the waitcnt pass could count no atomics with certainty, so the walk's next load waits (vmcnt(0)) covered
+    // the 16 atomics of any drain before them. C4 +0.3 %, 230 -> 211 VGPRs (profiles/r06_vor_drain_ab.txt)
+    __device__ __forceinline__ void drainStep2() {
+        constexpr int G = 64 / kLabsBuf;
+        const int i = (int)(gstep++ & (kLabsBuf / 2 - 1)) * 2;
+        issue(i);
+        issue(i + 1);
+        const int grp = (threadIdx.x & 63) / G;
+        if (grp == i || grp == i + 1) npend = 0;
+    }
 
     __device__ __forceinline__ double rho(int m, int h) const { return a.rho[(size_t)m * a.ncomp + h]; }
 
@@ -2073,6 +2089,9 @@ __device__ __forceinline__ void traceBody(const Args& a) {
             if constexpr (!STORE) {
             } else if constexpr (kSegsPerStep<GRID> == 1) {
                 T.drainStep();  // one drain instruction per step
+            } else if (SKIRT_VOR_DRAIN2) {
+                static_assert(kSegsPerStep<GRID> == 2, "two drains per step hold two adds per step");
+                T.drainStep2();
             } else {
                 // a buffer without room for another step's adds: issue the wave's adds
                 if (__ballot(T.npend > kLabsBuf - kSegsPerStep<GRID>)) T.drain();
