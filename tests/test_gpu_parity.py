@@ -106,6 +106,22 @@ def test_walk_ray_queue_order_does_not_change_results(name, packages, dust, monk
     _assert_same_packets(*runs)
 
 
+@pytest.mark.parametrize("name,packages,dust", [("pan_oct", 2000, False), ("pan_oct_sa", 500, True),
+                                                ("pan_oct_cs", 200, True), ("pan_cart16_sa", 500, True),
+                                                ("vor_pan", 1000, False), ("vor_pan_cs", 150, False),
+                                                ("oligo_2comp", 3000, False)])
+def test_global_atomic_kernels_equal_buffer_atomic_kernels(name, packages, dust, monkeypatch):
+    """The trace kernels of a Labs table of 4 GiB or more (global atomics, their own instantiations since round
+    6: Tracer GLOBAL) against the buffer-atomic kernels, forced by SKIRT_AMD_LABS_GLOBAL=1 on small tables, for
+    each family: octree leaf map, Cartesian, Voronoi, continuous scattering, the dust phases, several dust
+    components. The same packets take the same paths; the tallies agree up to the order of the additions."""
+    runs = []
+    for glob in ("1", "0"):
+        monkeypatch.setenv("SKIRT_AMD_LABS_GLOBAL", glob)
+        runs.append(run_gpu(name, packages=packages, dust=dust))
+    _assert_same_packets(*runs)
+
+
 @pytest.mark.parametrize("name,packages,dust", [("pan_cart16", 2000, False), ("pan_oct", 2000, True),
                                                 ("vor_pan", 1000, False)])
 def test_two_pipeline_halves_do_not_change_results(name, packages, dust, monkeypatch):
